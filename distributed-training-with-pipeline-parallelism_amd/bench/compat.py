@@ -1,0 +1,191 @@
+"""Reference-compatible benchmark API (reference helper:98-235, notebook cells 19-26).
+
+* :func:`run_train_iterations` -- 2 untimed warmup steps, ``num_iterations`` timed
+  ``schedule.step`` calls; returns ``{'elapsed_time','throughput','tokens_processed'}``
+  (helper:98-143).  Timing matches the reference (wall clock on the calling rank,
+  global tokens), with a device synchronize so GPU work is inside the window.
+* :func:`worker_process` -- per-rank bootstrap (helper:150-235): rendezvous, group
+  init (gloo on CPU, RCCL on GPU), the interleave rule (v=2 iff
+  ``n_layers % (2*world) == 0``, helper:181-185), synthetic tokens, token-wise CE
+  loss, loop placement ``stage = rank + world*i`` (helper:204-211), schedule factory
+  with ``num_mb`` microbatches (default 4, helper:214), last-rank result reporting
+  and ``{'error': ...}`` capture (helper:226-235).
+* :func:`run_one_experiment`, :func:`run_all_experiments`,
+  :func:`compute_speedup_and_efficiency` -- the notebook's launcher, sweep and
+  analysis (nb:306-333, nb:345-392, nb:405-433), with a per-experiment timeout and a
+  free port per run instead of the reference's fixed 29500 + unbounded join
+  (SURVEY §2.8 item 11).
+
+``engine='native'`` runs the same reference architecture on the MI355X HIP path
+(explicit backward, hand-written kernels); ``engine='torch'`` is the nn.Module /
+autograd path the reference uses.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import time
+import traceback
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..models.ref_transformer import ModelArgs, Transformer, manual_model_split, tokenwise_loss_fn
+from ..parallel.api import get_schedule_class
+
+
+def _sync(device) -> None:
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize()
+
+
+def run_train_iterations(schedule, x: torch.Tensor, y: torch.Tensor, rank: int, world_size: int,
+                         num_iterations: int = 10, warmup: int = 2, device=None) -> Dict[str, float]:
+    total_toks = x.shape[0] * x.shape[1] * num_iterations
+    first = rank == 0
+    last = rank == world_size - 1
+    dev = device if device is not None else x.device
+
+    def one():
+        if first and last:
+            schedule.step(x, target=y, losses=[])
+        elif first:
+            schedule.step(x)
+        elif last:
+            schedule.step(target=y, losses=[])
+        else:
+            schedule.step()
+
+    for _ in range(warmup):
+        one()
+    _sync(dev)
+    start_t = time.time()
+    for _ in range(num_iterations):
+        one()
+    _sync(dev)
+    elapsed = time.time() - start_t
+    return {"elapsed_time": elapsed, "throughput": total_toks / elapsed, "tokens_processed": total_toks}
+
+
+def stages_per_worker(schedule_type: str, n_layers: int, world_size: int) -> int:
+    """Interleave policy (helper:181-183)."""
+    return 2 if schedule_type == "Interleaved1F1B" and n_layers % (world_size * 2) == 0 else 1
+
+
+def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_size, seq_length, num_iterations,
+                   results_queue, num_microbatches: int = 4, device: Optional[str] = None, port: int = 29500,
+                   engine: str = "torch", dropout: float = 0.1, seed: Optional[int] = None):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        os.environ["RANK"] = str(rank)
+        os.environ["LOCAL_RANK"] = str(rank)
+        os.environ["WORLD_SIZE"] = str(world_size)
+        use_gpu = (device == "cuda") or (device is None and torch.cuda.is_available())
+        if use_gpu:
+            torch.cuda.set_device(rank)
+            dev = torch.device("cuda", rank)
+            dist.init_process_group(backend="nccl", rank=rank, world_size=world_size, device_id=dev)
+        else:
+            dev = torch.device("cpu")
+            dist.init_process_group(backend="gloo", rank=rank, world_size=world_size)
+        if seed is not None:
+            torch.manual_seed(seed)
+        spw = stages_per_worker(schedule_type, n_layers, world_size)
+        num_stages = world_size * spw
+        args = ModelArgs(n_layers=n_layers, n_heads=n_heads, dropout=dropout)
+        x = torch.randint(0, args.vocab_size, (batch_size, seq_length), dtype=torch.long, device=dev)
+        y = torch.randint(0, args.vocab_size, (batch_size, seq_length), dtype=torch.long, device=dev)
+        loss_fn = tokenwise_loss_fn(args.vocab_size)
+        stages = []
+        for i in range(spw):
+            stage_idx = rank + world_size * i
+            if engine == "native":
+                from ..models.native import build_reference_stage
+                stages.append(build_reference_stage(args, stage_idx, num_stages, dev))
+            else:
+                model = Transformer(args)
+                stages.append(manual_model_split(model, stage_idx, num_stages, dev))
+        cls = get_schedule_class(schedule_type)
+        schedule = cls(stages if spw > 1 or schedule_type == "Interleaved1F1B" else stages[0],
+                       n_microbatches=num_microbatches, loss_fn=loss_fn)
+        metrics = run_train_iterations(schedule, x, y, rank, world_size, num_iterations, device=dev)
+        if rank == world_size - 1:
+            results_queue.put(metrics)
+        dist.destroy_process_group()
+    except Exception as e:  # reference helper:231-235
+        print(f"Error in rank {rank}: {e}")
+        traceback.print_exc()
+        results_queue.put({"error": str(e)})
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_one_experiment(n_layers, n_heads, num_processes, schedule_type, batch_size=32, seq_length=128,
+                       num_iterations=10, timeout: float = 900.0, **kw) -> Dict:
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=worker_process, args=(r, num_processes, n_layers, n_heads, schedule_type, batch_size,
+                                                        seq_length, num_iterations, q), kwargs=dict(port=port, **kw))
+             for r in range(num_processes)]
+    for p in procs:
+        p.start()
+    deadline = time.time() + timeout
+    result = None
+    try:
+        result = q.get(timeout=timeout)
+    except Exception:
+        result = {"error": "No results returned"}
+    for p in procs:
+        p.join(timeout=max(1.0, deadline - time.time()))
+        if p.is_alive():
+            p.terminate()
+            p.join(5)
+    return result
+
+
+def run_all_experiments(n_heads_list=(4, 8, 12), n_layers_list=(4, 8, 12), num_processes_list=(2, 4),
+                        schedules=("GPipe", "1F1B", "Interleaved1F1B"), num_iterations=5, **kw):
+    import pandas as pd
+    rows = []
+    for n_heads in n_heads_list:
+        for n_layers in n_layers_list:
+            for P in num_processes_list:
+                for sched in schedules:
+                    try:
+                        m = run_one_experiment(n_layers, n_heads, P, sched, num_iterations=num_iterations, **kw)
+                        if "error" not in m:
+                            rows.append(dict(n_layers=n_layers, n_heads=n_heads, num_processes=P, schedule=sched,
+                                             throughput=m["throughput"], elapsed_time=m["elapsed_time"],
+                                             tokens_processed=m["tokens_processed"]))
+                            print(f"L{n_layers} H{n_heads} P{P} {sched}: {m['throughput']:.1f} tok/s")
+                        else:
+                            print(f"L{n_layers} H{n_heads} P{P} {sched}: error {m['error']}")
+                    except Exception as e:  # nb:388-390
+                        print(f"experiment failed: {e}")
+    return pd.DataFrame(rows)
+
+
+def compute_speedup_and_efficiency(df):
+    """speedup = thr / thr_GPipe for the same (L,H,P); efficiency = speedup / P * 100 (nb:403-433)."""
+    import pandas as pd
+    out = []
+    for (L, H, P), g in df.groupby(["n_layers", "n_heads", "num_processes"]):
+        base = g[g["schedule"] == "GPipe"]["throughput"]
+        if base.empty:
+            continue
+        b = float(base.iloc[0])
+        for _, row in g.iterrows():
+            if row["schedule"] == "GPipe":
+                continue
+            sp = row["throughput"] / b
+            out.append(dict(n_layers=L, n_heads=H, num_processes=P, schedule=row["schedule"],
+                            throughput=row["throughput"], speedup=sp, efficiency=sp / P * 100))
+    return pd.DataFrame(out)

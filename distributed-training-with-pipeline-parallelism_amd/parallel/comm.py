@@ -1,0 +1,101 @@
+"""Point-to-point transport between pipeline stages.
+
+On MI355X the backend is RCCL (``torch.distributed`` backend ``"nccl"``) over the
+point-to-point xGMI links; on CPU it is gloo (reference plumbing config,
+helper:175).  The executor hands this module :class:`~.ir.CommGroup` s whose
+per-peer order is already globally consistent (:mod:`.lower`), so each group is
+posted as one ``batch_isend_irecv`` (= one RCCL group: both directions of a link
+progress together) and nothing here needs to sort or retry.
+
+Static shapes: unlike the dependency's runtime shape inference with pickled
+meta-tensors (stage.py:1410-1519, C4 in SURVEY §2.6), stages declare their tensor
+specs; when a user module's specs are unknown, :func:`exchange_specs` ships them
+as small int64 tensors once at init (no pickling).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+_DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32, torch.float64, torch.uint8,
+           torch.bool, torch.int8]
+_MAX_DIMS = 8
+
+Spec = Tuple[Tuple[int, ...], torch.dtype]
+
+
+class P2P:
+    """Thin wrapper around ``torch.distributed`` p2p for one pipeline group.
+
+    ``ranks[i]`` is the global rank of pipeline rank ``i``.
+    """
+
+    def __init__(self, group: Optional[dist.ProcessGroup], ranks: Sequence[int], device: torch.device):
+        self.group = group
+        self.ranks = list(ranks)
+        self.device = device
+
+    def global_rank(self, pipe_rank: int) -> int:
+        return self.ranks[pipe_rank]
+
+    def post(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
+        """Post one group; returns (send_works, recv_works) aligned with the inputs."""
+        ops = []
+        for t, peer in sends:
+            ops.append(dist.P2POp(dist.isend, t, self.global_rank(peer), self.group))
+        for t, peer in recvs:
+            ops.append(dist.P2POp(dist.irecv, t, self.global_rank(peer), self.group))
+        if not ops:
+            return [], []
+        works = dist.batch_isend_irecv(ops)
+        return works[: len(sends)], works[len(sends):]
+
+    # -------------------------------------------------------------- spec exchange
+    def _pack(self, specs: Sequence[Spec]) -> torch.Tensor:
+        buf = torch.zeros(1 + 8 * (2 + _MAX_DIMS), dtype=torch.int64)
+        buf[0] = len(specs)
+        for i, (shape, dtype) in enumerate(specs):
+            base = 1 + i * (2 + _MAX_DIMS)
+            buf[base] = _DTYPES.index(dtype)
+            buf[base + 1] = len(shape)
+            for j, d in enumerate(shape):
+                buf[base + 2 + j] = d
+        return buf.to(self.device)
+
+    @staticmethod
+    def _unpack(buf: torch.Tensor) -> List[Spec]:
+        buf = buf.cpu().tolist()
+        out = []
+        for i in range(int(buf[0])):
+            base = 1 + i * (2 + _MAX_DIMS)
+            dt = _DTYPES[int(buf[base])]
+            nd = int(buf[base + 1])
+            out.append((tuple(int(x) for x in buf[base + 2: base + 2 + nd]), dt))
+        return out
+
+    def send_specs(self, specs: Sequence[Spec], peer: int) -> None:
+        if len(specs) > 8:
+            raise ValueError("at most 8 tensors per stage boundary")
+        dist.send(self._pack(specs), self.global_rank(peer), group=self.group)
+
+    def recv_specs(self, peer: int) -> List[Spec]:
+        buf = torch.zeros(1 + 8 * (2 + _MAX_DIMS), dtype=torch.int64, device=self.device)
+        dist.recv(buf, self.global_rank(peer), group=self.group)
+        return self._unpack(buf)
+
+    def warmup(self, peers: Sequence[int], my_rank: int) -> None:
+        """Establish the communicators to every neighbor once (torch stage.py:925-979).
+
+        Pairs are exchanged in ascending (low, high) order on both sides so the
+        first RCCL p2p on each link cannot cross-wait.
+        """
+        for peer in sorted(set(peers)):
+            if peer == my_rank:
+                continue
+            t_send = torch.ones(1, device=self.device)
+            t_recv = torch.zeros(1, device=self.device)
+            s, r = self.post([(t_send, peer)], [(t_recv, peer)])
+            for w in s + r:
+                w.wait()

@@ -1,0 +1,149 @@
+"""Lowering: compute order -> executable per-rank program with grouped p2p.
+
+RCCL (like NCCL) executes the point-to-point operations a rank posts on one
+communicator strictly in order, and a send of a large message completes only when
+the peer's matching receive runs.  A per-rank program is therefore safe only if
+every pair of ranks posts its shared messages in one consistent order.  The
+reference dependency reaches that with per-peer sorted batching
+(schedules.py:508-532) and a topological SEND/RECV placement
+(schedules.py:1223-1336).  Here the order is derived once, globally:
+
+1. :func:`.simulate.simulate` times the compute order (F=1, B=2, p2p latency
+   ``comm``), giving every message a send time stamp.
+2. All messages are sorted by (time, src rank, dst rank, kind, stage, mb); each
+   rank posts its own sends/receives in that global order.  A receive is posted
+   no later than right before its consumer; a send right after its producer.
+3. Comm ops posted at the same point form one :class:`~.ir.CommGroup`
+   (one ``batch_isend_irecv`` = one RCCL group), so bidirectional traffic on a
+   link (1F1B steady state, interleaved wrap-around P-1 -> 0) runs concurrently.
+4. ``REDUCE_GRAD`` is placed right after each stage's last backward
+   (schedules.py:1069-1099 semantics) so the DP all-reduce of that stage can
+   overlap the rest of the flush.
+
+:func:`.simulate.check_lowered` then proves the program cannot hang.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .ir import Action, CommGroup, CommOp, Entry, Op
+from .schedules import stage_to_rank
+from .simulate import check_lowered, simulate, uses_split_backward
+
+
+@dataclass
+class Message:
+    key: tuple            # (kind 'F'|'B', dst_stage, mb)
+    src: int
+    dst: int
+    t: float
+    producer: Action
+    consumer_stage: int
+
+    def order_key(self):
+        kind, stage, mb = self.key
+        return (self.t, self.src, self.dst, kind, stage, mb)
+
+
+def _producers(a: Action, S: int, split: bool):
+    """Messages (kind, dst_stage) produced by a compute action."""
+    if a.op == Op.F and a.stage < S - 1:
+        return [("F", a.stage + 1)]
+    if a.op == (Op.I if split else Op.B) and a.stage > 0:
+        return [("B", a.stage - 1)]
+    return []
+
+
+def lower(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1, style: str = "loop",
+          comm: float = 0.05, add_reduce_grad: bool = True, check: bool = True) -> Dict[int, List[Entry]]:
+    S = pp * v
+    s2r = [stage_to_rank(s, pp, style) for s in range(S)]
+    seq = {r: [a for a in orders.get(r, []) if a is not None and a.op.is_compute] for r in range(pp)}
+    split = uses_split_backward(seq)
+    sim = simulate(seq, pp, v, style, comm_latency=comm)
+
+    msgs: List[Message] = []
+    for r in range(pp):
+        for a in seq[r]:
+            for kind, dst_stage in _producers(a, S, split):
+                dst = s2r[dst_stage]
+                if dst == r:
+                    continue  # same-rank hand-off, no comm
+                msgs.append(Message((kind, dst_stage, a.mb), r, dst, sim.end[a], a, dst_stage))
+    msgs.sort(key=Message.order_key)
+
+    program: Dict[int, List[Entry]] = {}
+    for r in range(pp):
+        mine = [mm for mm in msgs if mm.src == r or mm.dst == r]
+        # index of consumer compute for each recv / producer compute for each send
+        pos = {a: i for i, a in enumerate(seq[r])}
+
+        def consumer_idx(mm: Message) -> int:
+            kind, st, mb = mm.key
+            op = Op.F if kind == "F" else (Op.I if split else Op.B)
+            return pos[Action(st, op, mb)]
+
+        ops_ordered: List[Tuple[CommOp, int, bool]] = []  # (op, anchor compute idx, is_send)
+        for mm in mine:
+            kind, st, mb = mm.key
+            if mm.src == r:
+                act = Action(mm.producer.stage, Op.SEND_F if kind == "F" else Op.SEND_B, mb)
+                ops_ordered.append((CommOp(act, mm.dst, mm.key), pos[mm.producer], True))
+            else:
+                act = Action(st, Op.RECV_F if kind == "F" else Op.RECV_B, mb)
+                ops_ordered.append((CommOp(act, mm.src, mm.key), consumer_idx(mm), False))
+
+        # slot p = "posted right before compute p".  Walk the global order; each op goes
+        # at max(previous op's slot, earliest allowed): sends after their producer,
+        # receives as early as the order allows (RCCL streams wait on the compute
+        # issued before a post, so early receives overlap the transfer with compute).
+        n = len(ops_ordered)
+        slots = []
+        cur = 0
+        for op, anchor, is_send in ops_ordered:
+            earliest = anchor + 1 if is_send else 0
+            s_ = max(cur, earliest)
+            if not is_send and s_ > anchor:
+                raise RuntimeError(f"rank {r}: cannot post {op} before its consumer (order conflict)")
+            slots.append(s_)
+            cur = s_
+        # Group contiguous ops posted at the same point, but never put receives for two
+        # different consumer computes in one group: a coalesced RCCL group completes as
+        # a unit, so a compute waiting on it would also wait for the other transfers.
+        entries: List[Entry] = []
+        k = 0
+        for p in range(len(seq[r]) + 1):
+            grp: List[CommOp] = []
+            grp_consumer = None
+            while k < n and slots[k] == p:
+                op, anchor, is_send = ops_ordered[k]
+                if not is_send:
+                    if grp_consumer is not None and anchor != grp_consumer:
+                        entries.append(CommGroup(grp))
+                        grp = []
+                    grp_consumer = anchor
+                grp.append(op)
+                k += 1
+            if grp:
+                entries.append(CommGroup(grp))
+            if p < len(seq[r]):
+                entries.append(seq[r][p])
+        program[r] = entries
+
+    if add_reduce_grad:
+        for r in range(pp):
+            last_bwd: Dict[int, int] = {}
+            for i, e in enumerate(program[r]):
+                if isinstance(e, Action) and e.op in (Op.B, Op.W):
+                    last_bwd[e.stage] = i
+            # insert after the last backward, in descending index order
+            for st, i in sorted(last_bwd.items(), key=lambda kv: -kv[1]):
+                program[r].insert(i + 1, Action(st, Op.REDUCE_GRAD))
+    if check:
+        check_lowered(program, S)
+    return program
+
+
+def format_program(program: Dict[int, List[Entry]]) -> str:
+    return "\n".join(f"rank {r}: " + " ".join(str(e) for e in program[r]) for r in sorted(program))

@@ -1,0 +1,294 @@
+"""Pipeline executor: runs one rank's lowered program each ``step``.
+
+Per action (dependency analogue: ``_PipelineScheduleRuntime._step_microbatches``,
+torch schedules.py:2037-2284, and the single-stage loops schedules.py:727-994):
+
+* ``CommGroup``  -> one grouped post (RCCL group / gloo batch).  Receives land in
+  pre-allocated per-(stage, microbatch) buffers, so every receive can be posted as
+  early as the global order allows and no buffer is ever re-allocated.
+* ``F``          -> wait for this microbatch's receive (stream wait on GPU, not a
+  host block), run the stage forward; the last stage also computes the loss
+  (scaled by 1/m when ``scale_grads`` -- equivalent to the dependency's
+  ``scale_grads`` div after the step, stage.py:570-584, but free).
+* ``B`` / ``I`` / ``W`` -> backward (full or split).
+* ``REDUCE_GRAD`` -> the stage's grad finalisation + async DP all-reduce, issued
+  right after its last backward so it overlaps the rest of the flush.
+
+Same-rank stage hand-offs (several virtual stages on one rank) bypass the
+transport.  With ``profile=True`` every compute action is bracketed by timing
+events (HIP events on GPU) and :attr:`last_timeline` / :meth:`bubble` report
+the measured pipeline bubble (1 - busy / step time).
+"""
+from __future__ import annotations
+
+import logging
+import time
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .comm import P2P
+from .ir import Action, CommGroup, Entry, Op, format_compute_grid
+from .lower import lower
+from .schedules import canonical_name, generate, stage_to_rank
+from .stage import StageBase, specs_of
+from .validate import validate
+
+log = logging.getLogger("mipipe.pipeline")
+
+
+class _Timer:
+    """Per-action interval recorder: HIP events on GPU, perf_counter on CPU."""
+
+    def __init__(self, device: torch.device):
+        self.gpu = device.type == "cuda"
+        self.records: List[Tuple[Action, object, object]] = []
+        self.t0 = None
+
+    def begin_step(self):
+        self.records = []
+        if self.gpu:
+            self.t0 = torch.cuda.Event(enable_timing=True)
+            self.t0.record()
+        else:
+            self.t0 = time.perf_counter()
+
+    def mark(self):
+        if self.gpu:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            return e
+        return time.perf_counter()
+
+    def add(self, a: Action, s, e):
+        self.records.append((a, s, e))
+
+    def finish(self) -> Tuple[List[Tuple[str, float, float]], float]:
+        end = self.mark()
+        if self.gpu:
+            torch.cuda.synchronize()
+            tl = [(str(a), self.t0.elapsed_time(s), self.t0.elapsed_time(e)) for a, s, e in self.records]
+            total = self.t0.elapsed_time(end)
+        else:
+            tl = [(str(a), (s - self.t0) * 1e3, (e - self.t0) * 1e3) for a, s, e in self.records]
+            total = (end - self.t0) * 1e3
+        return tl, total
+
+
+class PipelineRuntime:
+    def __init__(self, stages: Sequence[StageBase], schedule: str, n_microbatches: int, pp_rank: int,
+                 pp_size: int, p2p: P2P, loss_fn: Optional[Callable] = None, scale_grads: bool = True,
+                 style: str = "loop", program: Optional[Dict[int, List[Entry]]] = None, profile: bool = False):
+        self.stages: Dict[int, StageBase] = {s.stage_index: s for s in stages}
+        self.schedule = canonical_name(schedule)
+        self.m = n_microbatches
+        self.rank = pp_rank
+        self.pp = pp_size
+        self.p2p = p2p
+        self.loss_fn = loss_fn
+        self.scale_grads = scale_grads
+        self.style = style
+        any_stage = stages[0]
+        self.num_stages = any_stage.num_stages
+        if self.num_stages % pp_size != 0:
+            raise ValueError(f"{self.num_stages} stages do not divide over {pp_size} ranks")
+        self.v = self.num_stages // pp_size
+        if pp_size > self.num_stages:
+            raise ValueError("group size must be <= number of stages (torch stage.py:173-176)")
+        expected = [s for s in range(self.num_stages) if stage_to_rank(s, pp_size, style) == pp_rank]
+        if sorted(self.stages) != expected:
+            raise ValueError(f"rank {pp_rank} holds stages {sorted(self.stages)}, placement '{style}' expects {expected}")
+        self.s2r = [stage_to_rank(s, pp_size, style) for s in range(self.num_stages)]
+        if program is None:
+            orders = generate(self.schedule, pp_size, n_microbatches, self.v, style)
+            validate(orders, pp_size, self.v, n_microbatches, style)
+            self.orders = orders
+            program = lower(orders, pp_size, self.v, style)
+        else:
+            self.orders = {r: [e for e in es if isinstance(e, Action) and e.op.is_compute] for r, es in program.items()}
+        self.program_all = program
+        self.program = program[pp_rank]
+        self.device = any_stage.device
+        self.profile = profile
+        self.timer = _Timer(self.device)
+        self.last_timeline: List[Tuple[str, float, float]] = []
+        self.last_step_ms: float = 0.0
+        self._initialized = False
+        self._recv_bufs: Dict[tuple, List[torch.Tensor]] = {}
+
+    # ------------------------------------------------------------------ init
+    def _needs_inference(self) -> bool:
+        local = any(s.input_specs is None or s.output_specs is None for s in self.stages.values())
+        if self.pp == 1 or self.p2p.group is None and not dist.is_initialized():
+            return local
+        flag = torch.tensor([1.0 if local else 0.0], device=self.device)
+        dist.all_reduce(flag, group=self.p2p.group)
+        return bool(flag.item() > 0)
+
+    def _initialize(self, first_inputs: Optional[Tuple[torch.Tensor, ...]]):
+        if self.pp > 1:
+            peers = set()
+            for s in self.stages:
+                if s > 0:
+                    peers.add(self.s2r[s - 1])
+                if s < self.num_stages - 1:
+                    peers.add(self.s2r[s + 1])
+            self.p2p.warmup(sorted(peers), self.rank)
+        if self._needs_inference():
+            prev_out = None
+            for s in range(self.num_stages):
+                if self.s2r[s] != self.rank:
+                    continue
+                st = self.stages[s]
+                if s == 0:
+                    if first_inputs is None:
+                        raise RuntimeError("stage 0 needs inputs for shape inference")
+                    args = tuple(first_inputs)
+                    st.input_specs = specs_of(args)
+                else:
+                    if self.s2r[s - 1] == self.rank:
+                        specs = prev_out
+                    else:
+                        specs = self.p2p.recv_specs(self.s2r[s - 1])
+                    st.input_specs = specs
+                    args = tuple(torch.zeros(sh, dtype=dt, device=self.device) for sh, dt in specs)
+                out_specs = st.infer_output_specs(args)
+                prev_out = out_specs
+                if s < self.num_stages - 1 and self.s2r[s + 1] != self.rank:
+                    self.p2p.send_specs(out_specs, self.s2r[s + 1])
+        self._initialized = True
+
+    def _recv_buf(self, key: tuple) -> List[torch.Tensor]:
+        buf = self._recv_bufs.get(key)
+        if buf is None:
+            kind, stage, mb = key
+            st = self.stages[stage]
+            specs = st.input_specs if kind == "F" else st.output_specs
+            buf = [torch.empty(sh, dtype=dt, device=self.device) for sh, dt in specs]
+            self._recv_bufs[key] = buf
+        return buf
+
+    # ------------------------------------------------------------------ step
+    def step(self, inputs: Optional[Sequence[Tuple[torch.Tensor, ...]]] = None,
+             targets: Optional[Sequence[torch.Tensor]] = None, losses: Optional[list] = None,
+             return_outputs: bool = True) -> Optional[List[Tuple[torch.Tensor, ...]]]:
+        if not self._initialized:
+            self._initialize(inputs[0] if inputs is not None else None)
+        for st in self.stages.values():
+            st.clear_runtime_states()
+        recv_works: Dict[tuple, List] = {}
+        send_keep: List = []
+        send_tensors: Dict[tuple, Tuple[torch.Tensor, ...]] = {}
+        handoff: Dict[tuple, Tuple[torch.Tensor, ...]] = {}
+        outputs: Dict[int, Tuple[torch.Tensor, ...]] = {}
+        mb_losses: Dict[int, torch.Tensor] = {}
+        reduce_works = []
+        loss_scale = 1.0 / self.m if self.scale_grads else 1.0
+        S = self.num_stages
+        if self.profile:
+            self.timer.begin_step()
+
+        def wait_recv(key):
+            for w in recv_works.pop(key, []):
+                w.wait()
+
+        for idx, e in enumerate(self.program):
+            try:
+                if isinstance(e, CommGroup):
+                    sends, recvs, rkeys = [], [], []
+                    for op in e.ops:
+                        if op.action.op.is_send:
+                            ts = send_tensors.pop(op.key)
+                            sends += [(t, op.peer) for t in ts]
+                            send_keep.append(ts)
+                        else:
+                            bufs = self._recv_buf(op.key)
+                            recvs += [(t, op.peer) for t in bufs]
+                            rkeys += [op.key] * len(bufs)
+                    sw, rw = self.p2p.post(sends, recvs)
+                    send_keep.extend(sw)
+                    for k, w in zip(rkeys, rw):
+                        recv_works.setdefault(k, []).append(w)
+                    continue
+                a = e
+                st = self.stages.get(a.stage)
+                if a.op == Op.REDUCE_GRAD:
+                    w = st.reduce_grad(self.m, scaled_in_loss=self.scale_grads)
+                    if w is not None:
+                        reduce_works.append(w)
+                    continue
+                t_s = self.timer.mark() if self.profile else None
+                if a.op == Op.F:
+                    key = ("F", a.stage, a.mb)
+                    if a.stage == 0:
+                        args = tuple(inputs[a.mb])
+                    elif key in handoff:
+                        args = handoff.pop(key)
+                    else:
+                        wait_recv(key)
+                        args = tuple(self._recv_buf(key))
+                    tgt = targets[a.mb] if (st.is_last and targets is not None) else None
+                    out, loss = st.forward_mb(a.mb, args, tgt, self.loss_fn, loss_scale)
+                    if st.is_last:
+                        if return_outputs:
+                            outputs[a.mb] = out
+                        if loss is not None:
+                            mb_losses[a.mb] = loss
+                    else:
+                        nk = ("F", a.stage + 1, a.mb)
+                        if self.s2r[a.stage + 1] == self.rank:
+                            handoff[nk] = out
+                        else:
+                            send_tensors[nk] = out
+                elif a.op in (Op.B, Op.I):
+                    key = ("B", a.stage, a.mb)
+                    if a.stage == S - 1:
+                        g = None
+                    elif key in handoff:
+                        g = handoff.pop(key)
+                    else:
+                        wait_recv(key)
+                        g = tuple(self._recv_buf(key))
+                    gin = st.backward_mb(a.mb, g) if a.op == Op.B else st.backward_input_mb(a.mb, g)
+                    if a.stage > 0:
+                        nk = ("B", a.stage - 1, a.mb)
+                        gin = tuple(x for x in gin if x is not None)
+                        if self.s2r[a.stage - 1] == self.rank:
+                            handoff[nk] = gin
+                        else:
+                            send_tensors[nk] = gin
+                elif a.op == Op.W:
+                    st.backward_weight_mb(a.mb)
+                if self.profile:
+                    self.timer.add(a, t_s, self.timer.mark())
+            except Exception:
+                self._report_failure(idx)
+                raise
+        for w in send_keep:
+            if hasattr(w, "wait"):
+                w.wait()
+        for w in reduce_works:
+            w.wait()
+        if self.profile:
+            self.last_timeline, self.last_step_ms = self.timer.finish()
+        if losses is not None and mb_losses:
+            losses.extend(mb_losses[i] for i in sorted(mb_losses))
+        self._last_losses = mb_losses
+        if self.stages.get(S - 1) is not None and return_outputs:
+            return [outputs[i] for i in sorted(outputs)]
+        return None
+
+    # ------------------------------------------------------------------ diagnostics
+    def bubble(self) -> float:
+        """Measured bubble of the last profiled step on this rank: 1 - busy / step time."""
+        if not self.last_timeline or self.last_step_ms <= 0:
+            return float("nan")
+        busy = sum(e - s for _, s, e in self.last_timeline)
+        return max(0.0, 1.0 - busy / self.last_step_ms)
+
+    def _report_failure(self, idx: int) -> None:
+        grid = {r: [e for e in es if isinstance(e, Action)] for r, es in self.program_all.items()}
+        step = sum(1 for e in self.program[:idx] if isinstance(e, Action))
+        log.error("pipeline rank %d failed at action #%d (%s)\n%s", self.rank, idx, self.program[idx],
+                  format_compute_grid(grid, error_step=step, error_rank=self.rank))

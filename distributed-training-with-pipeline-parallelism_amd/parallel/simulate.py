@@ -1,0 +1,222 @@
+"""Schedule simulators: timing/bubble model and RCCL-semantics deadlock checker.
+
+* :func:`simulate` replays per-rank compute orders with per-op costs and a p2p
+  latency, honouring cross-stage dependencies, and reports makespan, per-rank busy
+  time and the bubble fraction ``1 - busy / (P * makespan)``.  It plays the role of
+  the dependency's ``_simulate_comms_compute`` (torch schedules.py:3246-3376) but
+  also produces *time stamps*, which :mod:`.lower` uses to build a globally
+  consistent p2p order.
+* :func:`check_lowered` models the executor on a GPU: per rank one in-order compute
+  stream and one in-order comm stream; a comm group starts after the previous group
+  completed and after every compute issued before it; a message completes when both
+  endpoint groups have started; a compute waits for the groups that carry its
+  inputs.  A fixpoint that does not finish means the lowered program can hang.
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+from .ir import Action, CommGroup, Entry, Op
+from .schedules import stage_to_rank
+
+DEFAULT_COSTS = {Op.F: 1.0, Op.B: 2.0, Op.I: 1.0, Op.W: 1.0, Op.REDUCE_GRAD: 0.0}
+
+
+@dataclass
+class SimResult:
+    start: Dict[Action, float]
+    end: Dict[Action, float]
+    rank_of: Dict[Action, int]
+    makespan: float
+    busy: Dict[int, float]
+    bubble: float
+    per_rank_bubble: Dict[int, float] = field(default_factory=dict)
+
+    def chrome_trace(self) -> dict:
+        ev = []
+        for a, t0 in self.start.items():
+            ev.append({"name": str(a), "ph": "X", "pid": self.rank_of[a], "tid": 0,
+                       "ts": t0 * 1000.0, "dur": (self.end[a] - t0) * 1000.0,
+                       "args": {"stage": a.stage, "mb": a.mb, "op": a.op.value}})
+        return {"traceEvents": ev, "displayTimeUnit": "ms"}
+
+    def dump_chrome_trace(self, path: str) -> None:
+        with open(path, "w") as f:
+            json.dump(self.chrome_trace(), f)
+
+
+def _deps(a: Action, num_stages: int, split: bool) -> List[Action]:
+    """Cross-stage data dependencies of a compute action."""
+    bwd = Op.I if split else Op.B
+    if a.op == Op.F:
+        return [] if a.stage == 0 else [Action(a.stage - 1, Op.F, a.mb)]
+    if a.op in (Op.B, Op.I):
+        deps = [Action(a.stage, Op.F, a.mb)]
+        if a.stage < num_stages - 1:
+            deps.append(Action(a.stage + 1, bwd, a.mb))
+        return deps
+    if a.op == Op.W:
+        return [Action(a.stage, Op.I, a.mb)]
+    return []
+
+
+def uses_split_backward(orders: Dict[int, Sequence[Optional[Action]]]) -> bool:
+    return any(a is not None and a.op in (Op.I, Op.W) for v in orders.values() for a in v)
+
+
+def simulate(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1, style: str = "loop",
+             costs: Optional[Dict[Op, float]] = None, comm_latency: float = 0.0,
+             stage_costs: Optional[Sequence[float]] = None) -> SimResult:
+    """Time a per-rank compute order.  ``stage_costs`` scales each stage's op costs
+    (non-uniform partitions)."""
+    costs = dict(DEFAULT_COSTS, **(costs or {}))
+    S = pp * v
+    split = uses_split_backward(orders)
+    s2r = [stage_to_rank(s, pp, style) for s in range(S)]
+    seq = {r: [a for a in orders[r] if a is not None and a.op.is_compute] for r in orders}
+    ptr = {r: 0 for r in seq}
+    t_rank = {r: 0.0 for r in seq}
+    start: Dict[Action, float] = {}
+    end: Dict[Action, float] = {}
+    remaining = sum(len(v_) for v_ in seq.values())
+    while remaining:
+        progressed = False
+        for r in seq:
+            while ptr[r] < len(seq[r]):
+                a = seq[r][ptr[r]]
+                ready = t_rank[r]
+                ok = True
+                for d in _deps(a, S, split):
+                    if d not in end:
+                        ok = False
+                        break
+                    lat = comm_latency if s2r[d.stage] != s2r[a.stage] else 0.0
+                    ready = max(ready, end[d] + lat)
+                if not ok:
+                    break
+                c = costs[a.op] * (stage_costs[a.stage] if stage_costs is not None else 1.0)
+                start[a] = ready
+                end[a] = ready + c
+                t_rank[r] = end[a]
+                ptr[r] += 1
+                remaining -= 1
+                progressed = True
+        if not progressed:
+            stuck = {r: str(seq[r][ptr[r]]) for r in seq if ptr[r] < len(seq[r])}
+            raise RuntimeError(f"schedule deadlocks (compute dependencies); stuck at {stuck}")
+    makespan = max(end.values()) if end else 0.0
+    busy = {r: sum(end[a] - start[a] for a in seq[r]) for r in seq}
+    bubble = 1.0 - sum(busy.values()) / (len(seq) * makespan) if makespan > 0 else 0.0
+    prb = {r: 1.0 - busy[r] / makespan if makespan > 0 else 0.0 for r in seq}
+    rank_of = {a: r for r in seq for a in seq[r]}
+    return SimResult(start, end, rank_of, makespan, busy, bubble, prb)
+
+
+def to_grid(res: SimResult, pp: int) -> Dict[int, List[Optional[Action]]]:
+    """Unit-time grid (for printing) from a simulation with integer costs."""
+    grid: Dict[int, List[Optional[Action]]] = {r: [] for r in range(pp)}
+    for a, t0 in sorted(res.start.items(), key=lambda kv: kv[1]):
+        r = res.rank_of[a]
+        slot = int(round(t0))
+        while len(grid[r]) < slot:
+            grid[r].append(None)
+        grid[r].append(a)
+    return grid
+
+
+# ----------------------------------------------------------------------------------------
+# deadlock check of a lowered program
+# ----------------------------------------------------------------------------------------
+
+
+def check_lowered(program: Dict[int, List[Entry]], num_stages: int) -> None:
+    """Raise RuntimeError if the lowered program can hang under RCCL semantics."""
+    split = uses_split_backward({r: [e for e in es if isinstance(e, Action)] for r, es in program.items()})
+    ranks = sorted(program)
+    # message key -> (sender group id, receiver group id)
+    msg_groups: Dict[tuple, List[Tuple[int, int]]] = {}
+    groups: Dict[Tuple[int, int], CommGroup] = {}
+    for r in ranks:
+        gi = 0
+        for e in program[r]:
+            if isinstance(e, CommGroup):
+                groups[(r, gi)] = e
+                for op in e.ops:
+                    msg_groups.setdefault(op.key, []).append((r, gi))
+                gi += 1
+    for k, gs in msg_groups.items():
+        if len(gs) != 2:
+            raise RuntimeError(f"message {k} has {len(gs)} endpoints (expected send+recv)")
+    # recv-group needed by each compute (by message key of its inputs)
+    entries = {r: program[r] for r in ranks}
+    comp_done: Dict[Tuple[int, int], bool] = {}
+    grp_started: Dict[Tuple[int, int], bool] = {}
+    grp_done: Dict[Tuple[int, int], bool] = {}
+    # compute index -> set of (rank, group) it must wait on
+    comp_waits: Dict[Tuple[int, int], List[Tuple[int, int]]] = {}
+    # group -> computes issued before it (last compute index)
+    grp_after_comp: Dict[Tuple[int, int], int] = {}
+    comp_list: Dict[int, List[Action]] = {}
+    recv_group_of: Dict[tuple, Tuple[int, int]] = {}
+    for r in ranks:
+        ci, gi = 0, 0
+        comp_list[r] = []
+        for e in entries[r]:
+            if isinstance(e, CommGroup):
+                grp_after_comp[(r, gi)] = ci - 1
+                for op in e.ops:
+                    if op.action.op.is_recv:
+                        recv_group_of[(r,) + op.key] = (r, gi)
+                gi += 1
+            else:
+                comp_list[r].append(e)
+                ci += 1
+    for r in ranks:
+        for ci, a in enumerate(comp_list[r]):
+            waits = []
+            for d in _deps(a, num_stages, split):
+                kind = "F" if d.op == Op.F else "B"
+                key = (r, kind, a.stage, a.mb)  # message into (a.stage) carrying d's output
+                if (r,) + (kind, a.stage, a.mb) in recv_group_of:
+                    waits.append(recv_group_of[(r,) + (kind, a.stage, a.mb)])
+            comp_waits[(r, ci)] = waits
+    ncomp = {r: len(comp_list[r]) for r in ranks}
+    ngrp = {r: sum(1 for e in entries[r] if isinstance(e, CommGroup)) for r in ranks}
+    cptr = {r: 0 for r in ranks}
+    gptr = {r: 0 for r in ranks}
+    changed = True
+    while changed:
+        changed = False
+        for r in ranks:
+            # compute stream
+            while cptr[r] < ncomp[r] and all(grp_done.get(g, False) for g in comp_waits[(r, cptr[r])]):
+                comp_done[(r, cptr[r])] = True
+                cptr[r] += 1
+                changed = True
+            # comm stream: start next group
+            g = gptr[r]
+            if g < ngrp[r] and (r, g) not in grp_started:
+                prev_ok = g == 0 or grp_done.get((r, g - 1), False)
+                last_c = grp_after_comp[(r, g)]
+                if prev_ok and (last_c < 0 or comp_done.get((r, last_c), False)):
+                    grp_started[(r, g)] = True
+                    changed = True
+        # group completion
+        for (r, g), grp in groups.items():
+            if grp_done.get((r, g)) or not grp_started.get((r, g)):
+                continue
+            if all(all(grp_started.get(x, False) for x in msg_groups[op.key]) for op in grp.ops):
+                grp_done[(r, g)] = True
+                if gptr[r] == g:
+                    gptr[r] += 1
+                changed = True
+        for r in ranks:
+            while gptr[r] < ngrp[r] and grp_done.get((r, gptr[r]), False):
+                gptr[r] += 1
+                changed = True
+    stuck = {r: (cptr[r], ncomp[r], gptr[r], ngrp[r]) for r in ranks if cptr[r] < ncomp[r] or gptr[r] < ngrp[r]}
+    if stuck:
+        detail = {r: (str(comp_list[r][cptr[r]]) if cptr[r] < ncomp[r] else "-") for r in stuck}
+        raise RuntimeError(f"lowered schedule can deadlock; stuck computes: {detail}")

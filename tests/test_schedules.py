@@ -1,0 +1,132 @@
+"""Pure-Python schedule tests (SURVEY §4 tier 1): golden IR, validator, lowering
+deadlock-freedom under RCCL semantics, analytic vs simulated bubble."""
+import itertools
+
+import pytest
+
+import mipipe  # noqa: F401
+from mipipe.parallel import Action, Op, analytic_bubble, generate, lower, simulate
+from mipipe.parallel.ir import from_csv, to_csv
+from mipipe.parallel.schedules import stage_to_rank
+from mipipe.parallel.simulate import check_lowered
+from mipipe.parallel.validate import ScheduleError, validate
+
+
+def seq(s):
+    return [Action.parse(x) for x in s.split()]
+
+
+def test_action_roundtrip():
+    for s in ["2F0", "1SEND_B3", "0REDUCE_GRAD", "12W7", "3RECV_F10"]:
+        assert str(Action.parse(s)) == s
+    with pytest.raises(ValueError):
+        Action.parse("xF0")
+
+
+def test_gpipe_golden():
+    # rank r runs rF0..rF3 rB0..rB3
+    o = generate("GPipe", 2, 4)
+    assert o[1] == seq("1F0 1F1 1F2 1F3 1B0 1B1 1B2 1B3")
+
+
+def test_1f1b_execution_order():
+    # dependency schedules.py:873-994 execution order for PP=4, m=4
+    o = generate("1F1B", 4, 4)
+    assert o[0] == seq("0F0 0F1 0F2 0F3 0B0 0B1 0B2 0B3")
+    assert o[3] == seq("3F0 3B0 3F1 3B1 3F2 3B2 3F3 3B3")
+    assert o[1] == seq("1F0 1F1 1F2 1B0 1F3 1B1 1B2 1B3")
+
+
+def test_interleaved_golden_appendix_a():
+    o = generate("Interleaved1F1B", 2, 4, 2)
+    assert o[0] == seq("0F0 0F1 2F0 2F1 0F2 2B0 0F3 2B1 2F2 0B0 2F3 0B1 2B2 2B3 0B2 0B3")
+    assert o[1] == seq("1F0 1F1 3F0 3B0 3F1 3B1 1F2 1B0 1F3 1B1 3F2 3B2 3F3 3B3 1B2 1B3")
+
+
+def test_interleaved_m_equals_p_is_fill_drain_like():
+    # PP=4, v=2, m=4 -> every rank does all 8 forwards first
+    o = generate("Interleaved1F1B", 4, 4, 2)
+    assert all(a.op == Op.F for a in o[0][:8])
+
+
+CASES = [(n, P, m, v) for n, v in [("GPipe", 1), ("1F1B", 1), ("Interleaved1F1B", 2), ("Interleaved1F1B", 3),
+                                    ("LoopedBFS", 2), ("ZBH1", 1)]
+         for P in (1, 2, 4, 8) for m in (P, 2 * P, 4 * P, 4)]
+
+
+@pytest.mark.parametrize("name,P,m,v", CASES)
+def test_validate_lower_and_no_deadlock(name, P, m, v):
+    if name == "Interleaved1F1B" and m % max(1, m // P):
+        pytest.skip("torch-style interleave requires m % rounds == 0")
+    o = generate(name, P, m, v)
+    validate(o, P, v, m)
+    prog = lower(o, P, v)  # runs check_lowered
+    # every send has exactly one matching recv with the same key, posted by the peer
+    sends, recvs = {}, {}
+    for r, es in prog.items():
+        for e in es:
+            if not isinstance(e, Action):
+                for op in e.ops:
+                    (sends if op.action.op.is_send else recvs)[op.key] = (r, op.peer)
+    assert set(sends) == set(recvs)
+    for k, (r, peer) in sends.items():
+        assert recvs[k] == (peer, r)
+    # one REDUCE_GRAD per stage
+    rg = [e for es in prog.values() for e in es if isinstance(e, Action) and e.op == Op.REDUCE_GRAD]
+    assert sorted(a.stage for a in rg) == list(range(P * v))
+
+
+def test_validator_catches_errors():
+    o = generate("1F1B", 2, 4)
+    bad = {0: o[0][:-1], 1: o[1]}
+    with pytest.raises(ScheduleError):
+        validate(bad, 2, 1, 4)
+    swapped = {0: o[0], 1: [o[1][1], o[1][0]] + o[1][2:]}
+    with pytest.raises(ScheduleError):
+        validate(swapped, 2, 1, 4)
+
+
+def test_checker_detects_deadlock():
+    # hand-built program where both ranks send before receiving in separate groups in
+    # crossed order -> must be rejected
+    from mipipe.parallel.ir import CommGroup, CommOp
+    prog = {
+        0: [Action(0, Op.F, 0), CommGroup([CommOp(Action(0, Op.RECV_B, 0), 1, ("B", 0, 0))]),
+            CommGroup([CommOp(Action(0, Op.SEND_F, 0), 1, ("F", 1, 0))]), Action(0, Op.B, 0)],
+        1: [CommGroup([CommOp(Action(1, Op.RECV_F, 0), 0, ("F", 1, 0))]), Action(1, Op.F, 0), Action(1, Op.B, 0),
+            CommGroup([CommOp(Action(1, Op.SEND_B, 0), 0, ("B", 0, 0))])],
+    }
+    with pytest.raises(RuntimeError):
+        check_lowered(prog, 2)
+
+
+@pytest.mark.parametrize("P,m", [(2, 4), (4, 4), (4, 8), (8, 16)])
+def test_bubble_analytic_matches_simulation(P, m):
+    for name in ("GPipe", "1F1B"):
+        sim = simulate(generate(name, P, m), P)
+        assert sim.bubble == pytest.approx(analytic_bubble(name, P, m), abs=1e-9)
+    sim = simulate(generate("Interleaved1F1B", P, 2 * P, 2), P, 2)
+    assert sim.bubble == pytest.approx(analytic_bubble("Interleaved1F1B", P, 2 * P, 2), abs=1e-9)
+
+
+def test_zero_bubble_beats_1f1b():
+    for P, m in [(4, 8), (8, 16)]:
+        assert simulate(generate("ZBH1", P, m), P).bubble < simulate(generate("1F1B", P, m), P).bubble
+
+
+def test_csv_roundtrip_and_placement():
+    o = generate("Interleaved1F1B", 4, 8, 2)
+    assert from_csv(to_csv(o)) == o
+    assert [stage_to_rank(s, 4, "v") for s in range(8)] == [0, 1, 2, 3, 3, 2, 1, 0]
+    assert [stage_to_rank(s, 4, "loop") for s in range(8)] == [0, 1, 2, 3, 0, 1, 2, 3]
+
+
+def test_v_placement_interleaved_lowering():
+    with pytest.raises(ValueError):
+        generate("Interleaved1F1B", 4, 8, 2, style="v")
+    o = generate("LoopedBFS", 4, 8, 2, style="v")
+    validate(o, 4, 2, 8, style="v")
+    prog = lower(o, 4, 2, style="v")
+    # the chunk boundary 3 -> 4 is on the same rank under 'v': no comm for it
+    keys = {op.key for es in prog.values() for e in es if not isinstance(e, Action) for op in e.ops}
+    assert ("F", 4, 0) not in keys
