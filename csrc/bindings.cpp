@@ -1,0 +1,259 @@
+// Python bindings of the mipipe HIP kernels (torch tensors in, launches on the current
+// HIP stream).  Kernels live in csrc/kernels/*.hip behind plain C launchers so only
+// this file pays for the torch headers.  No hipify: written against HIP directly.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+extern "C" {
+int mp_norm_fwd(int rms, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
+                float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed, hipStream_t st);
+int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
+                const void* dres, void* ds, void* dbranch, float* dw, float* dbias, int rows, int D, float p,
+                uint64_t seed, hipStream_t st);
+int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss, int T, int V, int Vp, float grad_scale,
+                    int64_t ignore_index, int write_grad, hipStream_t st);
+int mp_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int T, int S, int D, int pos_offset,
+                 hipStream_t st);
+int mp_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int T, int S, int D, int pos_offset,
+                 hipStream_t st);
+int mp_sumsq(const float* g, int64_t n, float* out, hipStream_t st);
+int mp_adamw(float* p, float* g, float* m, float* v, void* w16, int64_t n, int64_t n_decay, float lr, float b1,
+             float b2, float eps, float wd, int step, const float* sumsq, float max_norm, float grad_scale,
+             int zero_grad, hipStream_t st);
+int mp_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t st);
+int mp_act_fwd(const void* a, void* g, int64_t n, int act, float p, uint64_t seed, hipStream_t st);
+int mp_act_bwd(const void* dg, const void* a, void* da, float* dbias, int rows, int cols, int act, float p,
+               uint64_t seed, hipStream_t st);
+int mp_colsum(const void* x, float* dbias, int rows, int cols, hipStream_t st);
+int mp_swiglu_fwd(const void* gu, void* y, int T, int F, hipStream_t st);
+int mp_swiglu_bwd(const void* gu, const void* dy, void* dgu, int T, int F, hipStream_t st);
+int mp_rope(void* qkv, const float* cs, const float* sn, int T, int S, int H, int Hkv, int Dh, int pos_offset,
+            int inverse, hipStream_t st);
+int mp_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq, int Sk, int H,
+                int Hkv, int D, int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride, int causal,
+                float scale, float p_drop, uint64_t seed, hipStream_t st);
+int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                float* delta, void* dq, void* dk, void* dv, float* dq_acc, int B, int Sq, int Sk, int H, int Hkv, int D,
+                int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride, int64_t dq_stride,
+                int64_t dk_stride, int64_t dv_stride, int causal, float scale, float p_drop, uint64_t seed,
+                hipStream_t st);
+int mp_gemm(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
+            int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
+            int epilogue, int c_f32_accum, float alpha, hipStream_t st);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check(int rc, const char* what) { TORCH_CHECK(rc == 0, "mipipe kernel ", what, " failed with code ", rc); }
+
+const void* ptr_or_null(const c10::optional<torch::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+void* mptr_or_null(const c10::optional<torch::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+void req(const torch::Tensor& t, torch::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be on the GPU");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has wrong dtype ", t.scalar_type());
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void norm_fwd(bool rms, torch::Tensor a, c10::optional<torch::Tensor> b, torch::Tensor w,
+              c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> s_out, torch::Tensor y,
+              c10::optional<torch::Tensor> mean, torch::Tensor rstd, double eps, double p, int64_t seed) {
+  req(a, torch::kBFloat16, "a");
+  req(y, torch::kBFloat16, "y");
+  req(rstd, torch::kFloat32, "rstd");
+  const int D = a.size(-1);
+  const int rows = a.numel() / D;
+  TORCH_CHECK(!b.has_value() || (s_out.has_value() && b->numel() == a.numel()), "b needs s_out");
+  TORCH_CHECK(rms || mean.has_value(), "LayerNorm needs mean");
+  TORCH_CHECK(rstd.numel() >= rows && w.numel() == D, "bad norm shapes");
+  check(mp_norm_fwd(rms, a.data_ptr(), ptr_or_null(b), w.data_ptr(), ptr_or_null(bias), mptr_or_null(s_out),
+                    y.data_ptr(), mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), rows,
+                    D, (float)eps, (float)p, (uint64_t)seed, cur_stream()),
+        "norm_fwd");
+}
+
+void norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c10::optional<torch::Tensor> mean,
+              torch::Tensor rstd, c10::optional<torch::Tensor> dres, torch::Tensor ds,
+              c10::optional<torch::Tensor> dbranch, torch::Tensor dw, c10::optional<torch::Tensor> dbias, double p,
+              int64_t seed) {
+  req(dy, torch::kBFloat16, "dy");
+  req(s, torch::kBFloat16, "s");
+  req(ds, torch::kBFloat16, "ds");
+  req(dw, torch::kFloat32, "dw");
+  const int D = dy.size(-1);
+  const int rows = dy.numel() / D;
+  TORCH_CHECK(s.numel() == dy.numel() && ds.numel() == dy.numel() && dw.numel() == D, "bad norm_bwd shapes");
+  check(mp_norm_bwd(rms, dy.data_ptr(), s.data_ptr(), w.data_ptr(),
+                    mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), ptr_or_null(dres),
+                    ds.data_ptr(), mptr_or_null(dbranch), dw.data_ptr<float>(),
+                    dbias.has_value() ? dbias->data_ptr<float>() : nullptr, rows, D, (float)p, (uint64_t)seed,
+                    cur_stream()),
+        "norm_bwd");
+}
+
+void xent(torch::Tensor logits, torch::Tensor target, torch::Tensor loss, int64_t V, double grad_scale,
+          int64_t ignore_index, bool write_grad) {
+  req(logits, torch::kBFloat16, "logits");
+  req(target, torch::kInt64, "target");
+  req(loss, torch::kFloat32, "loss");
+  const int Vp = logits.size(-1);
+  const int T = logits.numel() / Vp;
+  TORCH_CHECK(target.numel() == T && loss.numel() == T, "bad xent shapes");
+  check(mp_xent_fwd_bwd(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(), T, V, Vp,
+                        (float)grad_scale, ignore_index, write_grad, cur_stream()),
+        "xent");
+}
+
+void embed_fwd(torch::Tensor idx, torch::Tensor wte, c10::optional<torch::Tensor> wpe, torch::Tensor out, int64_t S,
+               int64_t pos_offset) {
+  req(idx, torch::kInt64, "idx");
+  req(out, torch::kBFloat16, "out");
+  const int D = wte.size(1);
+  const int T = idx.numel();
+  TORCH_CHECK(out.numel() == (int64_t)T * D, "bad embed shapes");
+  check(mp_embed_fwd(idx.data_ptr<int64_t>(), wte.data_ptr(), ptr_or_null(wpe), out.data_ptr(), T, S, D, pos_offset,
+                     cur_stream()),
+        "embed_fwd");
+}
+
+void embed_bwd(torch::Tensor idx, torch::Tensor dout, torch::Tensor dwte, c10::optional<torch::Tensor> dwpe,
+               int64_t S, int64_t pos_offset) {
+  req(idx, torch::kInt64, "idx");
+  req(dwte, torch::kFloat32, "dwte");
+  const int D = dwte.size(-1);
+  const int T = idx.numel();
+  check(mp_embed_bwd(idx.data_ptr<int64_t>(), dout.data_ptr(), dwte.data_ptr<float>(),
+                     dwpe.has_value() ? dwpe->data_ptr<float>() : nullptr, T, S, D, pos_offset, cur_stream()),
+        "embed_bwd");
+}
+
+void sumsq(torch::Tensor g, torch::Tensor out) {
+  req(g, torch::kFloat32, "g");
+  check(mp_sumsq(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), cur_stream()), "sumsq");
+}
+
+void adamw(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> w16,
+           int64_t n_decay, double lr, double b1, double b2, double eps, double wd, int64_t step,
+           c10::optional<torch::Tensor> sumsq_buf, double max_norm, double grad_scale, bool zero_grad) {
+  req(p, torch::kFloat32, "p");
+  req(g, torch::kFloat32, "g");
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "bad adamw shapes");
+  check(mp_adamw(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), mptr_or_null(w16),
+                 p.numel(), n_decay, (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step,
+                 sumsq_buf.has_value() ? sumsq_buf->data_ptr<float>() : nullptr, (float)max_norm, (float)grad_scale,
+                 zero_grad, cur_stream()),
+        "adamw");
+}
+
+void cast_f32_bf16(torch::Tensor src, torch::Tensor dst) {
+  req(src, torch::kFloat32, "src");
+  check(mp_cast_f32_bf16(src.data_ptr<float>(), dst.data_ptr(), src.numel(), cur_stream()), "cast");
+}
+
+void act_fwd(torch::Tensor a, torch::Tensor g, int64_t act, double p, int64_t seed) {
+  req(a, torch::kBFloat16, "a");
+  check(mp_act_fwd(a.data_ptr(), g.data_ptr(), a.numel(), act, (float)p, (uint64_t)seed, cur_stream()), "act_fwd");
+}
+
+void act_bwd(torch::Tensor dg, torch::Tensor a, torch::Tensor da, c10::optional<torch::Tensor> dbias, int64_t act,
+             double p, int64_t seed) {
+  req(dg, torch::kBFloat16, "dg");
+  const int cols = dg.size(-1);
+  const int rows = dg.numel() / cols;
+  check(mp_act_bwd(dg.data_ptr(), a.data_ptr(), da.data_ptr(), dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
+                   rows, cols, act, (float)p, (uint64_t)seed, cur_stream()),
+        "act_bwd");
+}
+
+void colsum(torch::Tensor x, torch::Tensor dbias) {
+  req(x, torch::kBFloat16, "x");
+  req(dbias, torch::kFloat32, "dbias");
+  const int cols = x.size(-1);
+  check(mp_colsum(x.data_ptr(), dbias.data_ptr<float>(), x.numel() / cols, cols, cur_stream()), "colsum");
+}
+
+void swiglu_fwd(torch::Tensor gu, torch::Tensor y) {
+  const int F = y.size(-1);
+  check(mp_swiglu_fwd(gu.data_ptr(), y.data_ptr(), y.numel() / F, F, cur_stream()), "swiglu_fwd");
+}
+
+void swiglu_bwd(torch::Tensor gu, torch::Tensor dy, torch::Tensor dgu) {
+  const int F = dy.size(-1);
+  check(mp_swiglu_bwd(gu.data_ptr(), dy.data_ptr(), dgu.data_ptr(), dy.numel() / F, F, cur_stream()), "swiglu_bwd");
+}
+
+void rope(torch::Tensor qkv, torch::Tensor cs, torch::Tensor sn, int64_t S, int64_t H, int64_t Hkv, int64_t Dh,
+          int64_t pos_offset, bool inverse) {
+  const int T = qkv.numel() / ((H + 2 * Hkv) * Dh);
+  check(mp_rope(qkv.data_ptr(), cs.data_ptr<float>(), sn.data_ptr<float>(), T, S, H, Hkv, Dh, pos_offset, inverse,
+                cur_stream()),
+        "rope");
+}
+
+// q/k/v/o are [B*S, stride] row views (token-major), heads at h*D inside a row.
+void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o, torch::Tensor lse, int64_t B,
+              int64_t Sq, int64_t Sk, int64_t H, int64_t Hkv, int64_t D, bool causal, double scale, double p,
+              int64_t seed) {
+  req(lse, torch::kFloat32, "lse");
+  TORCH_CHECK(q.scalar_type() == torch::kBFloat16 && o.scalar_type() == torch::kBFloat16, "attn bf16 only");
+  TORCH_CHECK(lse.numel() >= B * H * Sq, "lse too small");
+  check(mp_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), B, Sq, Sk, H, Hkv,
+                    D, q.stride(0), k.stride(0), v.stride(0), o.stride(0), causal, (float)scale, (float)p,
+                    (uint64_t)seed, cur_stream()),
+        "attn_fwd");
+}
+
+void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o, torch::Tensor dout,
+              torch::Tensor lse, torch::Tensor delta, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv,
+              torch::Tensor dq_acc, int64_t B, int64_t Sq, int64_t Sk, int64_t H, int64_t Hkv, int64_t D, bool causal,
+              double scale, double p, int64_t seed) {
+  TORCH_CHECK(o.stride(0) == dout.stride(0), "o and dout must share a row stride");
+  check(mp_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
+                    delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq_acc.data_ptr<float>(), B,
+                    Sq, Sk, H, Hkv, D, q.stride(0), k.stride(0), v.stride(0), o.stride(0), dq.stride(0), dk.stride(0),
+                    dv.stride(0), causal, (float)scale, (float)p, (uint64_t)seed, cur_stream()),
+        "attn_bwd");
+}
+
+// C[M,N] (+)= alpha * op(A) @ op(B) with fused epilogue.
+//   A: [M,K] row-major (transA=0) or [K,M] (transA=1); B: [N,K] (transB=0, "NT") or [K,N] (transB=1)
+void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> bias,
+          c10::optional<torch::Tensor> residual, c10::optional<torch::Tensor> aux, bool transA, bool transB,
+          int64_t epilogue, bool accum, double alpha) {
+  const int M = C.size(0), N = C.size(1);
+  const int K = transA ? A.size(0) : A.size(1);
+  TORCH_CHECK((transA ? A.size(1) : A.size(0)) == M, "gemm: A/M mismatch");
+  TORCH_CHECK((transB ? B.size(0) : B.size(1)) == K && (transB ? B.size(1) : B.size(0)) == N, "gemm: B mismatch");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm: inner dims must be contiguous");
+  TORCH_CHECK(!accum || C.scalar_type() == torch::kFloat32, "gemm: accumulate needs f32 C");
+  check(mp_gemm(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual), mptr_or_null(aux),
+                M, N, K, A.stride(0), B.stride(0), C.stride(0), residual.has_value() ? residual->stride(0) : 0,
+                aux.has_value() ? aux->stride(0) : 0, transA, transB, epilogue, accum, (float)alpha, cur_stream()),
+        "gemm");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "mipipe gfx950 HIP kernels";
+  m.def("norm_fwd", &norm_fwd);
+  m.def("norm_bwd", &norm_bwd);
+  m.def("xent", &xent);
+  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_bwd", &embed_bwd);
+  m.def("sumsq", &sumsq);
+  m.def("adamw", &adamw);
+  m.def("cast_f32_bf16", &cast_f32_bf16);
+  m.def("act_fwd", &act_fwd);
+  m.def("act_bwd", &act_bwd);
+  m.def("colsum", &colsum);
+  m.def("swiglu_fwd", &swiglu_fwd);
+  m.def("swiglu_bwd", &swiglu_bwd);
+  m.def("rope", &rope);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
+  m.def("gemm", &gemm);
+}

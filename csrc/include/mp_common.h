@@ -1,0 +1,107 @@
+// Shared device helpers for the mipipe gfx950 (CDNA4) kernels.
+//
+// Conventions:
+//  * bf16 tensors are moved as raw 16-bit words (uint16_t) in 16-byte vectors
+//    (8 x bf16 per lane): hipcc does not vectorise scalar bf16 loads on its own.
+//  * f32 <-> bf16: bf16 -> f32 is an exact shift; f32 -> bf16 uses the compiler's
+//    cast (lowers to v_cvt_pk_bf16_f32 on gfx950, round-to-nearest-even, NaN-safe).
+//  * Wave = 64 lanes.  Reductions use DPP/shuffle over 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define MP_WAVE 64
+
+namespace mp {
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(8))) uint16_t u16x8;
+typedef __attribute__((ext_vector_type(4))) uint16_t u16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64).  `red` is >= NT/64 floats of LDS.
+template <int NT>
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (NT == 64) return v;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  return t;
+}
+
+template <int NT>
+__device__ __forceinline__ float block_max(float v, float* red) {
+  v = wave_max(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (NT == 64) return v;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// Counter-based RNG (Philox-lite: 2 rounds of a 64-bit multiply-xorshift hash).
+// Deterministic in (seed, offset, index) so dropout masks are regenerated in the
+// backward pass instead of stored.
+__device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
+  uint64_t x = idx * 0x9E3779B97F4A7C15ull ^ (seed + 0xD1B54A32D192ED03ull);
+  x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+// keep with probability (1-p): returns scale (1/(1-p)) or 0
+__device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, float p) {
+  const uint32_t thr = (uint32_t)(p * 4294967296.0f);
+  return hash_u32(seed, idx) >= thr ? 1.0f / (1.0f - p) : 0.0f;
+}
+
+__device__ __forceinline__ float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float u = k0 * (x + k1 * x * x * x);
+  return 0.5f * x * (1.0f + tanhf(u));
+}
+
+__device__ __forceinline__ float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float u = k0 * (x + k1 * x2 * x);
+  float t = tanhf(u);
+  return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * k1 * x2);
+}
+
+__device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
+
+}  // namespace mp

@@ -1,0 +1,675 @@
+// Flash attention forward / backward for gfx950 (bf16 in, f32 accumulate, MFMA 32x32x16).
+// SURVEY §2.5 K4 (self + cross attention, causal / non-causal, head dims 64..256,
+// GQA, in-kernel counter-based dropout regenerated in the backward).
+//
+// Layout: q/k/v/o are token-major rows ([B*S, row_stride] bf16), head h at column h*D,
+// i.e. exactly what the fused QKV projection writes and the output projection reads:
+// no transposes or head-major copies anywhere.  LSE is kept per (b, h, query) in log2
+// units (lse2 = m + log2(l)) for the backward.
+//
+// Forward (one workgroup = 4 waves = 128 queries of one (b, h); 64-key tiles):
+//   * "swapped" QK^T: each wave computes S^T = K . Q^T so the QUERY is on the MFMA lane and
+//     the 32 keys of a 32x32 tile are in its registers: the row max / row sum are
+//     in-lane (+1 cross-half shuffle), and the online-softmax rescale of O is a per-lane
+//     scalar because O is also kept transposed (O^T = V^T . P^T).
+//   * P^T never leaves registers: the S^T accumulator is already the B operand of
+//     V^T . P^T (k order permuted, see cdna guide §3); V^T fragments come from
+//     ds_read_b64_tr_b16 hardware-transposed LDS reads.
+//   * K and V tiles are register-staged into a double-buffered LDS ring (loads for tile
+//     j+1 issued before computing tile j, written after), XOR-swizzled in 16-byte chunks
+//     so both the b128 row reads (K) and the transposed reads (V) are bank-conflict free.
+//   * causal: heavy query blocks launch first; per-wave skip of fully masked tiles.
+// Backward = two deterministic kernels (no f32 atomics):
+//   dkdv: one workgroup = 128 keys of one (b, kv-head), loops over all query heads of the
+//         group (GQA) and all query tiles; key on the MFMA lane so P and dS are directly
+//         the B operands of dV^T += dO^T P and dK^T += Q^T dS.
+//   dq:   one workgroup = 128 queries (forward structure), recomputes P^T and dP^T and
+//         accumulates dQ^T += K^T dS^T.
+#include "mp_common.h"
+
+using namespace mp;
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+#define LOG2E 1.4426950408889634f
+
+// ------------------------------------------------------------------------------------------
+// LDS image: [rows][DP] bf16, 16-byte chunks XOR-swizzled per row.
+// ------------------------------------------------------------------------------------------
+template <int DP>
+__device__ __forceinline__ int chunk_swz(int row) {
+  if constexpr (DP == 64) return (((row >> 1) & 1) << 2) | ((row >> 2) & 3);
+  else return ((row & 3) << 2) | ((row >> 2) & 3);
+}
+
+template <int DP>
+__device__ __forceinline__ int lds_off(int row, int chunk) {  // byte offset of a 16-byte chunk
+  return row * (DP * 2) + 16 * (chunk ^ chunk_swz<DP>(row));
+}
+
+// 16-byte row read (A operand: rows on lanes 0..31, 8 consecutive columns)
+template <int DP>
+__device__ __forceinline__ bf16x8 lds_row8(const char* base, int row, int chunk) {
+  return *reinterpret_cast<const bf16x8*>(base + lds_off<DP>(row, chunk));
+}
+
+// Transposed read: returns for this lane the 4 rows r0..r0+3 of column (c0 + (lane&15)).
+// Lane 4q+p of each 16-lane group addresses row r0+q, columns c0+4p..c0+4p+3.
+template <int DP>
+__device__ __forceinline__ s16x4 lds_tr4(const char* base, int r0, int c0) {
+  const int i = threadIdx.x & 15;
+  const int q = i >> 2, p = i & 3;
+  const int row = r0 + q;
+  const int col = c0 + 4 * p;
+  const char* a = base + lds_off<DP>(row, col >> 3) + ((col & 7) << 1);
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
+}
+
+__device__ __forceinline__ bf16x8 cat44(s16x4 lo, s16x4 hi) {
+  s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, r);
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)acc[8 * s + j];
+  return r;
+}
+
+// load 8 bf16 of a global row (zero outside [0, D) or invalid row)
+__device__ __forceinline__ u16x8 gload8(const bf16_t* rowp, int col, int D, bool valid) {
+  u16x8 z = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (!valid || col >= D) return z;
+  return *reinterpret_cast<const u16x8*>(rowp + col);
+}
+
+// Stage a [64][DP] tile of rows (row0 .. row0+63 of a token-major tensor) into registers.
+template <int DP>
+struct Stage64 {
+  static constexpr int PER = DP / 32;  // 16-byte chunks per thread
+  u16x8 v[PER];
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t stride, int row0, int nrows, int D) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / (DP / 8), c = idx % (DP / 8);
+      const int gr = row0 + r;
+      v[i] = gload8(base + (int64_t)gr * stride, c * 8, D, gr < nrows);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int r = idx / (DP / 8), c = idx % (DP / 8);
+      *reinterpret_cast<u16x8*>(lds + lds_off<DP>(r, c)) = v[i];
+    }
+  }
+};
+
+__device__ __forceinline__ uint64_t drop_idx(int bh, int q, int k, int Sk) {
+  return ((uint64_t)bh * 0x100000000ull) + (uint64_t)q * (uint64_t)Sk + (uint64_t)k;
+}
+
+// ==========================================================================================
+// forward
+// ==========================================================================================
+template <int DP, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+    float* __restrict__ LSE, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
+    int64_t os, float scale, float p_drop, uint64_t seed) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;  // bytes per [64][DP] tile
+#define kbuf(i) (smem + (i) * TILE)
+#define vbuf(i) (smem + (2 + (i)) * TILE)
+
+  const int nmb = (Sq + 127) / 128;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heavy blocks first
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int m0 = mb * 128;
+  const int qrow = m0 + 32 * w + l32;  // this lane's query
+  const bool qvalid = qrow < Sq;
+  const bf16_t* Qb = Q + (int64_t)b * Sq * qs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * Sk * ks + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * Sk * vs + (int64_t)hk * D;
+
+  // Q as the B operand of S^T = K Q^T: lane holds Q[qrow][16s + 8hl + j]
+  bf16x8 qf[DP / 16];
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    u16x8 t = gload8(Qb + (int64_t)qrow * qs, 16 * s + 8 * hl, D, qvalid);
+    qf[s] = __builtin_bit_cast(bf16x8, t);
+  }
+  const float c = scale * LOG2E;
+  f32x16 o[DP / 32];
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d) o[d] = {};
+  float m_run = -INFINITY, l_run = 0.f;
+
+  // causal alignment: query i may attend keys <= i + (Sk - Sq)
+  const int shift = Sk - Sq;
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, m0 + 128 + shift);
+  const int ntiles = (n_end + 63) / 64;
+
+  Stage64<DP> kst, vst;
+  kst.load(Kb, ks, 0, Sk, D);
+  vst.load(Vb, vs, 0, Sk, D);
+  kst.store(kbuf(0));
+  vst.store(vbuf(0));
+  const int wave_last_q = m0 + 32 * w + 31 + shift;
+
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const int n0 = t * 64;
+    if (t + 1 < ntiles) {
+      kst.load(Kb, ks, n0 + 64, Sk, D);
+      vst.load(Vb, vs, n0 + 64, Sk, D);
+    }
+    __syncthreads();
+    const bool skip = CAUSAL && n0 > wave_last_q;
+    if (!skip) {
+      const char* kb = kbuf(cur);
+      const char* vb = vbuf(cur);
+      // ---- S^T = K Q^T (two 32-key sub tiles)
+      f32x16 s0 = {}, s1 = {};
+#pragma unroll
+      for (int s = 0; s < DP / 16; ++s) {
+        bf16x8 a0 = lds_row8<DP>(kb, l32, 2 * s + hl);
+        bf16x8 a1 = lds_row8<DP>(kb, 32 + l32, 2 * s + hl);
+        s0 = mfma32(a0, qf[s], s0);
+        s1 = mfma32(a1, qf[s], s1);
+      }
+      // ---- scale, mask, tile max
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+        const int k0 = n0 + kr, k1 = n0 + 32 + kr;
+        float v0 = s0[r] * c, v1 = s1[r] * c;
+        if (k0 >= Sk || (CAUSAL && k0 > qrow + shift)) v0 = -INFINITY;
+        if (k1 >= Sk || (CAUSAL && k1 > qrow + shift)) v1 = -INFINITY;
+        s0[r] = v0;
+        s1[r] = v1;
+        mx = fmaxf(mx, fmaxf(v0, v1));
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = exp2f(m_run - m_use);
+      float rs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p0 = exp2f(s0[r] - m_use), p1 = exp2f(s1[r] - m_use);
+        rs += p0 + p1;
+        if (DROP) {
+          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+          p0 *= dropout_scale(seed, drop_idx(bh, qrow, n0 + kr, Sk), p_drop);
+          p1 *= dropout_scale(seed, drop_idx(bh, qrow, n0 + 32 + kr, Sk), p_drop);
+        }
+        s0[r] = p0;
+        s1[r] = p1;
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) o[d] *= alpha;
+      // ---- O^T += V^T P^T
+      const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+        const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
+        bf16x8 a;
+        a = cat44(lds_tr4<DP>(vb, 0 + 4 * hl, c0), lds_tr4<DP>(vb, 8 + 4 * hl, c0));
+        o[d] = mfma32(a, p00, o[d]);
+        a = cat44(lds_tr4<DP>(vb, 16 + 4 * hl, c0), lds_tr4<DP>(vb, 24 + 4 * hl, c0));
+        o[d] = mfma32(a, p01, o[d]);
+        a = cat44(lds_tr4<DP>(vb, 32 + 4 * hl, c0), lds_tr4<DP>(vb, 40 + 4 * hl, c0));
+        o[d] = mfma32(a, p10, o[d]);
+        a = cat44(lds_tr4<DP>(vb, 48 + 4 * hl, c0), lds_tr4<DP>(vb, 56 + 4 * hl, c0));
+        o[d] = mfma32(a, p11, o[d]);
+      }
+    }
+    if (t + 1 < ntiles) {
+      kst.store(kbuf(cur ^ 1));
+      vst.store(vbuf(cur ^ 1));
+    }
+  }
+  // ---- epilogue: O = O^T / l ; LSE
+  if (qvalid) {
+    const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+    bf16_t* orow = O + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 32 * d + 8 * g + 4 * hl;
+        if (col < D) {
+          u16x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = f2bf(o[d][4 * g + e] * inv);
+          *reinterpret_cast<u16x4*>(orow + col) = pk;
+        }
+      }
+    }
+    if (hl == 0) LSE[(int64_t)bh * Sq + qrow] = l_run > 0.f ? m_run + log2f(l_run) : INFINITY;
+  }
+}
+
+// ==========================================================================================
+// backward preprocess: delta = rowsum(dO * O)  (f32, per (b, h, query))
+// ==========================================================================================
+__global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
+                                                         float* __restrict__ delta, int B, int Sq, int H, int D,
+                                                         int64_t os) {
+  const int lane = threadIdx.x & 63;
+  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (b, q, h)
+  if (item >= (int64_t)B * Sq * H) return;
+  const int h = item % H;
+  const int64_t tq = item / H;  // b*Sq + q
+  const bf16_t* orow = O + tq * os + (int64_t)h * D;
+  const bf16_t* drow = dO + tq * os + (int64_t)h * D;
+  float acc = 0.f;
+  for (int c = lane * 4; c < D; c += 256) {
+    u16x4 a = *reinterpret_cast<const u16x4*>(orow + c);
+    u16x4 g = *reinterpret_cast<const u16x4*>(drow + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc += bf2f(a[e]) * bf2f(g[e]);
+  }
+  acc = wave_sum(acc);
+  if (lane == 0) {
+    const int64_t b = tq / Sq, q = tq % Sq;
+    delta[(b * H + h) * Sq + q] = acc;
+  }
+}
+
+// ==========================================================================================
+// backward dK / dV: workgroup = 128 keys (4 waves x 32) of one (b, kv head)
+// ==========================================================================================
+template <int DP, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs,
+    int64_t ks, int64_t vs, int64_t os, int64_t dks, int64_t dvs, float scale, float p_drop, uint64_t seed) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;
+#define qbuf(i) (smem + (i) * TILE)
+#define gbuf(i) (smem + (2 + (i)) * TILE)
+  float* lse_s = reinterpret_cast<float*>(smem + 4 * TILE);  // [2][64]
+  float* del_s = lse_s + 128;                                 // [2][64]
+
+  const int nkb = (Sk + 127) / 128;
+  const int kb = (int)blockIdx.x;
+  const int bhk = blockIdx.y;
+  const int b = bhk / Hkv, hk = bhk % Hkv;
+  const int grp = H / Hkv;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int k0 = kb * 128;
+  const int key = k0 + 32 * w + l32;  // this lane's key (MFMA column)
+  const bool kvalid = key < Sk;
+  const int shift = Sk - Sq;
+  (void)nkb;
+
+  // K and V of this wave's 32 keys as B operands: lane holds K[key][16s + 8hl + j]
+  bf16x8 kf[DP / 16], vf[DP / 16];
+  const bf16_t* Krow = K + ((int64_t)b * Sk + key) * ks + (int64_t)hk * D;
+  const bf16_t* Vrow = V + ((int64_t)b * Sk + key) * vs + (int64_t)hk * D;
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    kf[s] = __builtin_bit_cast(bf16x8, gload8(Krow, 16 * s + 8 * hl, D, kvalid));
+    vf[s] = __builtin_bit_cast(bf16x8, gload8(Vrow, 16 * s + 8 * hl, D, kvalid));
+  }
+  f32x16 dk[DP / 32], dv[DP / 32];
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d) {
+    dk[d] = {};
+    dv[d] = {};
+  }
+  const float c = scale * LOG2E;
+  const float keep = DROP ? 1.f / (1.f - p_drop) : 1.f;
+  // first query that can see key k0: q >= k0 - shift
+  const int q_begin = CAUSAL ? max(0, ((k0 - shift) / 64) * 64) : 0;
+  const int ntq = (Sq - q_begin + 63) / 64;
+  const int total = ntq * grp;
+
+  Stage64<DP> qst, gst;
+  auto issue = [&](int it) {
+    const int hq = hk * grp + it / ntq;
+    const int q0 = q_begin + (it % ntq) * 64;
+    qst.load(Q + (int64_t)b * Sq * qs + (int64_t)hq * D, qs, q0, Sq, D);
+    gst.load(dO + (int64_t)b * Sq * os + (int64_t)hq * D, os, q0, Sq, D);
+  };
+  auto stats = [&](int it, int buf) {
+    const int hq = hk * grp + it / ntq;
+    const int q0 = q_begin + (it % ntq) * 64;
+    if (threadIdx.x < 64) {
+      const int q = q0 + threadIdx.x;
+      const int64_t idx = ((int64_t)b * H + hq) * Sq + q;
+      lse_s[buf * 64 + threadIdx.x] = q < Sq ? LSE[idx] : INFINITY;
+      del_s[buf * 64 + threadIdx.x] = q < Sq ? DELTA[idx] : 0.f;
+    }
+  };
+  if (total > 0) {
+    issue(0);
+    qst.store(qbuf(0));
+    gst.store(gbuf(0));
+    stats(0, 0);
+  }
+  for (int it = 0; it < total; ++it) {
+    const int cur = it & 1;
+    const int hq = hk * grp + it / ntq;
+    const int q0 = q_begin + (it % ntq) * 64;
+    const int bhq = b * H + hq;
+    if (it + 1 < total) issue(it + 1);
+    __syncthreads();
+    const char* qb = qbuf(cur);
+    const char* gb = gbuf(cur);
+    const float* ls = lse_s + cur * 64;
+    const float* dl = del_s + cur * 64;
+    const bool skip = CAUSAL && (k0 + 32 * w > q0 + 63 + shift);  // all of this wave's keys masked
+    if (!skip) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // S[q][key] = Q K^T, dP[q][key] = dO V^T   (query rows u*32.. in registers, key on lane)
+        f32x16 sacc = {}, pacc = {};
+#pragma unroll
+        for (int s = 0; s < DP / 16; ++s) {
+          bf16x8 aq = lds_row8<DP>(qb, 32 * u + l32, 2 * s + hl);
+          bf16x8 ag = lds_row8<DP>(gb, 32 * u + l32, 2 * s + hl);
+          sacc = mfma32(aq, kf[s], sacc);
+          pacc = mfma32(ag, vf[s], pacc);
+        }
+        f32x16 pm, ds;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int qr = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          const int q = q0 + qr;
+          float p = exp2f(sacc[r] * c - ls[qr]);
+          if (!kvalid || q >= Sq || (CAUSAL && key > q + shift)) p = 0.f;
+          float dpv = pacc[r];
+          float pd = p;
+          if (DROP) {
+            const float msk = dropout_scale(seed, drop_idx(bhq, q, key, Sk), p_drop);
+            pd = p * msk;
+            dpv = dpv * msk;
+          }
+          pm[r] = pd;                      // dropped P for dV
+          ds[r] = p * (dpv - dl[qr]);      // dS
+        }
+        (void)keep;
+        // dV^T += dO^T P ;  dK^T += Q^T dS     (A via transposed LDS reads of the row images)
+        const bf16x8 pb0 = pack8(pm, 0), pb1 = pack8(pm, 1);
+        const bf16x8 db0 = pack8(ds, 0), db1 = pack8(ds, 1);
+#pragma unroll
+        for (int d = 0; d < DP / 32; ++d) {
+          const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
+          const int rb = 32 * u + 4 * hl;
+          bf16x8 ag0 = cat44(lds_tr4<DP>(gb, rb + 0, c0), lds_tr4<DP>(gb, rb + 8, c0));
+          bf16x8 ag1 = cat44(lds_tr4<DP>(gb, rb + 16, c0), lds_tr4<DP>(gb, rb + 24, c0));
+          dv[d] = mfma32(ag0, pb0, dv[d]);
+          dv[d] = mfma32(ag1, pb1, dv[d]);
+          bf16x8 aq0 = cat44(lds_tr4<DP>(qb, rb + 0, c0), lds_tr4<DP>(qb, rb + 8, c0));
+          bf16x8 aq1 = cat44(lds_tr4<DP>(qb, rb + 16, c0), lds_tr4<DP>(qb, rb + 24, c0));
+          dk[d] = mfma32(aq0, db0, dk[d]);
+          dk[d] = mfma32(aq1, db1, dk[d]);
+        }
+      }
+    }
+    if (it + 1 < total) {
+      qst.store(qbuf(cur ^ 1));
+      gst.store(gbuf(cur ^ 1));
+      stats(it + 1, cur ^ 1);
+    }
+  }
+  // ---- epilogue: lane = key, registers = d
+  if (kvalid) {
+    bf16_t* dkrow = dK + ((int64_t)b * Sk + key) * dks + (int64_t)hk * D;
+    bf16_t* dvrow = dV + ((int64_t)b * Sk + key) * dvs + (int64_t)hk * D;
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 32 * d + 8 * g + 4 * hl;
+        if (col < D) {
+          u16x4 a, bb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] = f2bf(dk[d][4 * g + e] * scale);
+            bb[e] = f2bf(dv[d][4 * g + e]);
+          }
+          *reinterpret_cast<u16x4*>(dkrow + col) = a;
+          *reinterpret_cast<u16x4*>(dvrow + col) = bb;
+        }
+      }
+    }
+  }
+}
+
+// ==========================================================================================
+// backward dQ: workgroup = 128 queries of one (b, h) (forward structure)
+// ==========================================================================================
+template <int DP, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16_t* __restrict__ dQ, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
+    int64_t os, int64_t dqs, float scale, float p_drop, uint64_t seed) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;
+#define kbuf(i) (smem + (i) * TILE)
+#define vbuf(i) (smem + (2 + (i)) * TILE)
+  const int nmb = (Sq + 127) / 128;
+  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
+  const int bh = blockIdx.y;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int m0 = mb * 128;
+  const int qrow = m0 + 32 * w + l32;
+  const bool qvalid = qrow < Sq;
+  const int shift = Sk - Sq;
+  const bf16_t* Kb = K + (int64_t)b * Sk * ks + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * Sk * vs + (int64_t)hk * D;
+  bf16x8 qf[DP / 16], gf[DP / 16];
+  const bf16_t* Qrow = Q + ((int64_t)b * Sq + qrow) * qs + (int64_t)h * D;
+  const bf16_t* Grow = dO + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    qf[s] = __builtin_bit_cast(bf16x8, gload8(Qrow, 16 * s + 8 * hl, D, qvalid));
+    gf[s] = __builtin_bit_cast(bf16x8, gload8(Grow, 16 * s + 8 * hl, D, qvalid));
+  }
+  const int64_t sidx = (int64_t)bh * Sq + qrow;
+  const float lse = qvalid ? LSE[sidx] : INFINITY;
+  const float dlt = qvalid ? DELTA[sidx] : 0.f;
+  const float c = scale * LOG2E;
+  f32x16 dq[DP / 32];
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d) dq[d] = {};
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, m0 + 128 + shift);
+  const int ntiles = (n_end + 63) / 64;
+  Stage64<DP> kst, vst;
+  kst.load(Kb, ks, 0, Sk, D);
+  vst.load(Vb, vs, 0, Sk, D);
+  kst.store(kbuf(0));
+  vst.store(vbuf(0));
+  const int wave_last_q = m0 + 32 * w + 31 + shift;
+  for (int t = 0; t < ntiles; ++t) {
+    const int cur = t & 1;
+    const int n0 = t * 64;
+    if (t + 1 < ntiles) {
+      kst.load(Kb, ks, n0 + 64, Sk, D);
+      vst.load(Vb, vs, n0 + 64, Sk, D);
+    }
+    __syncthreads();
+    if (!(CAUSAL && n0 > wave_last_q)) {
+      const char* kb = kbuf(cur);
+      const char* vb = vbuf(cur);
+      f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+#pragma unroll
+      for (int s = 0; s < DP / 16; ++s) {
+        bf16x8 ak0 = lds_row8<DP>(kb, l32, 2 * s + hl);
+        bf16x8 ak1 = lds_row8<DP>(kb, 32 + l32, 2 * s + hl);
+        bf16x8 av0 = lds_row8<DP>(vb, l32, 2 * s + hl);
+        bf16x8 av1 = lds_row8<DP>(vb, 32 + l32, 2 * s + hl);
+        s0 = mfma32(ak0, qf[s], s0);
+        s1 = mfma32(ak1, qf[s], s1);
+        p0 = mfma32(av0, gf[s], p0);  // dP^T = V dO^T
+        p1 = mfma32(av1, gf[s], p1);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int kk = n0 + 32 * half + kr;
+          float sv = half ? s1[r] : s0[r];
+          float dpv = half ? p1[r] : p0[r];
+          float p = exp2f(sv * c - lse);
+          if (kk >= Sk || (CAUSAL && kk > qrow + shift) || !qvalid) p = 0.f;
+          if (DROP) dpv *= dropout_scale(seed, drop_idx(bh, qrow, kk, Sk), p_drop);
+          const float dsv = p * (dpv - dlt);
+          if (half) s1[r] = dsv; else s0[r] = dsv;
+        }
+      }
+      const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 1), d10 = pack8(s1, 0), d11 = pack8(s1, 1);
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+        const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
+        bf16x8 a;
+        a = cat44(lds_tr4<DP>(kb, 0 + 4 * hl, c0), lds_tr4<DP>(kb, 8 + 4 * hl, c0));
+        dq[d] = mfma32(a, d00, dq[d]);
+        a = cat44(lds_tr4<DP>(kb, 16 + 4 * hl, c0), lds_tr4<DP>(kb, 24 + 4 * hl, c0));
+        dq[d] = mfma32(a, d01, dq[d]);
+        a = cat44(lds_tr4<DP>(kb, 32 + 4 * hl, c0), lds_tr4<DP>(kb, 40 + 4 * hl, c0));
+        dq[d] = mfma32(a, d10, dq[d]);
+        a = cat44(lds_tr4<DP>(kb, 48 + 4 * hl, c0), lds_tr4<DP>(kb, 56 + 4 * hl, c0));
+        dq[d] = mfma32(a, d11, dq[d]);
+      }
+    }
+    if (t + 1 < ntiles) {
+      kst.store(kbuf(cur ^ 1));
+      vst.store(vbuf(cur ^ 1));
+    }
+  }
+  if (qvalid) {
+    bf16_t* drow = dQ + ((int64_t)b * Sq + qrow) * dqs + (int64_t)h * D;
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 32 * d + 8 * g + 4 * hl;
+        if (col < D) {
+          u16x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = f2bf(dq[d][4 * g + e] * scale);
+          *reinterpret_cast<u16x4*>(drow + col) = pk;
+        }
+      }
+    }
+  }
+}
+
+#undef kbuf
+#undef vbuf
+#undef qbuf
+#undef gbuf
+// ==========================================================================================
+// launchers
+// ==========================================================================================
+template <int DP, bool CAUSAL, bool DROP>
+static int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq, int Sk, int H,
+                      int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, float p,
+                      uint64_t seed, hipStream_t st) {
+  const size_t lds = 4 * 64 * DP * 2;
+  auto kern = attn_fwd_kernel<DP, CAUSAL, DROP>;
+  if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  dim3 grid((Sq + 127) / 128, B * H);
+  kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, B, Sq, Sk, H,
+                               Hkv, D, qs, ks, vs, os, scale, p, seed);
+  return (int)hipGetLastError();
+}
+
+template <int DP, bool CAUSAL, bool DROP>
+static int launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
+                      float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int Hkv, int D,
+                      int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs, int64_t dks, int64_t dvs,
+                      float scale, float p, uint64_t seed, hipStream_t st) {
+  {
+    const int64_t items = (int64_t)B * Sq * H;
+    attn_delta_kernel<<<(int)((items + 3) / 4), 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dout, delta, B, Sq, H,
+                                                              D, os);
+  }
+  {
+    const size_t lds = 4 * 64 * DP * 2 + 4 * 128 * sizeof(float);
+    auto kern = attn_bwd_dkdv_kernel<DP, CAUSAL, DROP>;
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dim3 grid((Sk + 127) / 128, B * Hkv);
+    kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse,
+                                 delta, (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, dks, dvs,
+                                 scale, p, seed);
+  }
+  {
+    const size_t lds = 4 * 64 * DP * 2;
+    auto kern = attn_bwd_dq_kernel<DP, CAUSAL, DROP>;
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dim3 grid((Sq + 127) / 128, B * H);
+    kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse,
+                                 delta, (bf16_t*)dq, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, dqs, scale, p, seed);
+  }
+  return (int)hipGetLastError();
+}
+
+static int pick_dp(int D) { return D <= 64 ? 64 : (D <= 128 ? 128 : (D <= 256 ? 256 : -1)); }
+
+extern "C" int mp_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq, int Sk,
+                           int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int causal,
+                           float scale, float p_drop, uint64_t seed, hipStream_t st) {
+  const int DP = pick_dp(D);
+  if (DP < 0 || D % 8 || H % Hkv) return -1;
+  const bool drop = p_drop > 0.f;
+#define MP_F(DPV)                                                                                                     \
+  if (DP == DPV) {                                                                                                    \
+    if (causal) return drop ? launch_fwd<DPV, true, true>(q, k, v, o, lse, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, scale, \
+                                                          p_drop, seed, st)                                           \
+                            : launch_fwd<DPV, true, false>(q, k, v, o, lse, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os,     \
+                                                           scale, p_drop, seed, st);                                  \
+    return drop ? launch_fwd<DPV, false, true>(q, k, v, o, lse, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, scale, p_drop,  \
+                                               seed, st)                                                              \
+                : launch_fwd<DPV, false, false>(q, k, v, o, lse, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, scale, p_drop, \
+                                                seed, st);                                                            \
+  }
+  MP_F(64) MP_F(128) MP_F(256)
+#undef MP_F
+  return -1;
+}
+
+extern "C" int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
+                           const float* lse, float* delta, void* dq, void* dk, void* dv, float* dq_acc, int B, int Sq,
+                           int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs,
+                           int64_t dks, int64_t dvs, int causal, float scale, float p_drop, uint64_t seed,
+                           hipStream_t st) {
+  (void)dq_acc;
+  const int DP = pick_dp(D);
+  if (DP < 0 || D % 8 || H % Hkv) return -1;
+  const bool drop = p_drop > 0.f;
+#define MP_B(DPV, C, DR)                                                                                             \
+  if (DP == DPV && (bool)causal == C && drop == DR)                                                                  \
+    return launch_bwd<DPV, C, DR>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, dqs, \
+                                  dks, dvs, scale, p_drop, seed, st);
+  MP_B(64, true, false) MP_B(64, false, false) MP_B(64, true, true) MP_B(64, false, true)
+  MP_B(128, true, false) MP_B(128, false, false) MP_B(128, true, true) MP_B(128, false, true)
+  MP_B(256, true, false) MP_B(256, false, false) MP_B(256, true, true) MP_B(256, false, true)
+#undef MP_B
+  return -1;
+}

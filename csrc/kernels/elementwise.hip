@@ -1,0 +1,218 @@
+// Memory-bound elementwise kernels of the transformer block, all with 16-byte
+// bf16 vectors and, where a bias gradient is needed, a fused column reduction
+// (per-block partials in registers -> LDS across waves -> one f32 atomic per column).
+//
+//   act_fwd         g = dropout(act(a))                 (FFN activation when not fused in a GEMM)
+//   act_bwd         da = dg * dropout_mask * act'(a);  dbias += colsum(da)
+//   colsum          dbias += colsum(x)                  (bias grads of the projections)
+//   swiglu_fwd/bwd  y = silu(gate) * up  over a [T, 2F] gate|up buffer (Llama-3 FFN)
+//   rope            rotate-half RoPE on the q/k heads of the packed qkv buffer, in place
+//                   (forward: +theta, backward: -theta), f32 cos/sin table from the host
+#include "mp_common.h"
+
+using namespace mp;
+
+enum Act { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_RELU = 2 };
+
+__device__ __forceinline__ float act_f(float x, int act) {
+  if (act == ACT_GELU_TANH) return gelu_tanh(x);
+  if (act == ACT_RELU) return fmaxf(x, 0.f);
+  return x;
+}
+__device__ __forceinline__ float act_g(float x, int act) {
+  if (act == ACT_GELU_TANH) return gelu_tanh_grad(x);
+  if (act == ACT_RELU) return x > 0.f ? 1.f : 0.f;
+  return 1.f;
+}
+
+__global__ void __launch_bounds__(256) act_fwd_kernel(const bf16_t* __restrict__ a, bf16_t* __restrict__ g, int64_t n,
+                                                      int act, float p, uint64_t seed) {
+  const int64_t n8 = n / 8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    u16x8 v = reinterpret_cast<const u16x8*>(a)[i];
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float y = act_f(bf2f(v[e]), act);
+      if (p > 0.f) y *= dropout_scale(seed, i * 8 + e, p);
+      o[e] = f2bf(y);
+    }
+    reinterpret_cast<u16x8*>(g)[i] = o;
+  }
+}
+
+// MODE 0: colsum(x) -> dbias ; MODE 1: da = dg*act'(a)*mask (written), dbias += colsum(da)
+template <int MODE>
+__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ a,
+                                                     bf16_t* __restrict__ da, float* __restrict__ dbias, int rows,
+                                                     int cols, int rows_per_block, int act, float p, uint64_t seed) {
+  __shared__ float red[4][64 * 8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int chunk = blockIdx.y * 64 + lane;
+  const bool active = chunk * 8 < cols;
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  const int r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  if (active) {
+    for (int r = r0 + wv; r < r1; r += 4) {
+      const size_t off = (size_t)r * cols + chunk * 8;
+      u16x8 xv = *reinterpret_cast<const u16x8*>(x + off);
+      if (MODE == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += bf2f(xv[e]);
+      } else {
+        u16x8 av = *reinterpret_cast<const u16x8*>(a + off);
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = bf2f(xv[e]) * act_g(bf2f(av[e]), act);
+          if (p > 0.f) d *= dropout_scale(seed, off + e, p);
+          o[e] = f2bf(d);
+          acc[e] += bf2f(o[e]);
+        }
+        *reinterpret_cast<u16x8*>(da + off) = o;
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[wv][lane * 8 + e] = acc[e];
+  __syncthreads();
+  if (dbias == nullptr) return;
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int col = blockIdx.y * 512 + i;
+    if (col < cols) atomicAdd(dbias + col, red[0][i] + red[1][i] + red[2][i] + red[3][i]);
+  }
+}
+
+__global__ void __launch_bounds__(256) swiglu_fwd_kernel(const bf16_t* __restrict__ gu, bf16_t* __restrict__ y, int T,
+                                                         int F) {
+  const int64_t n8 = (int64_t)T * F / 8;
+  const int f8 = F / 8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t t = i / f8, c = i % f8;
+    u16x8 g = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + c * 8);
+    u16x8 u = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + F + c * 8);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = f2bf(silu(bf2f(g[e])) * bf2f(u[e]));
+    reinterpret_cast<u16x8*>(y)[i] = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) swiglu_bwd_kernel(const bf16_t* __restrict__ gu, const bf16_t* __restrict__ dy,
+                                                         bf16_t* __restrict__ dgu, int T, int F) {
+  const int64_t n8 = (int64_t)T * F / 8;
+  const int f8 = F / 8;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t t = i / f8, c = i % f8;
+    u16x8 g = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + c * 8);
+    u16x8 u = *reinterpret_cast<const u16x8*>(gu + t * 2 * F + F + c * 8);
+    u16x8 d = reinterpret_cast<const u16x8*>(dy)[i];
+    u16x8 og, ou;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float gf = bf2f(g[e]), uf = bf2f(u[e]), df = bf2f(d[e]);
+      const float sg = 1.f / (1.f + __expf(-gf));
+      const float sl = gf * sg;
+      ou[e] = f2bf(df * sl);
+      og[e] = f2bf(df * uf * sg * (1.f + gf * (1.f - sg)));
+    }
+    *reinterpret_cast<u16x8*>(dgu + t * 2 * F + c * 8) = og;
+    *reinterpret_cast<u16x8*>(dgu + t * 2 * F + F + c * 8) = ou;
+  }
+}
+
+// qkv: [T, (H + 2*Hkv) * Dh] with heads laid out q(H) | k(Hkv) | v(Hkv).  Rotates q and k
+// in place; cos/sin: [S, Dh/2] f32.  sign = +1 forward, -1 backward (inverse rotation).
+__global__ void __launch_bounds__(256) rope_kernel(bf16_t* __restrict__ qkv, const float* __restrict__ cs,
+                                                   const float* __restrict__ sn, int T, int S, int H, int Hkv, int Dh,
+                                                   int pos_offset, float sign) {
+  const int half = Dh / 2;
+  const int nh = H + Hkv;  // rotated heads per token
+  const int64_t total = (int64_t)T * nh * (half / 4);
+  const int stride = (H + 2 * Hkv) * Dh;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int q4 = (int)(i % (half / 4));
+    const int64_t th = i / (half / 4);
+    const int h = (int)(th % nh);
+    const int64_t t = th / nh;
+    const int pos = (int)(t % S) + pos_offset;
+    bf16_t* base = qkv + t * stride + (int64_t)h * Dh;
+    u16x4 x1 = *reinterpret_cast<u16x4*>(base + q4 * 4);
+    u16x4 x2 = *reinterpret_cast<u16x4*>(base + half + q4 * 4);
+    u16x4 o1, o2;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int j = q4 * 4 + e;
+      const float c = cs[(int64_t)pos * half + j], s = sign * sn[(int64_t)pos * half + j];
+      const float a = bf2f(x1[e]), b = bf2f(x2[e]);
+      o1[e] = f2bf(a * c - b * s);
+      o2[e] = f2bf(b * c + a * s);
+    }
+    *reinterpret_cast<u16x4*>(base + q4 * 4) = o1;
+    *reinterpret_cast<u16x4*>(base + half + q4 * 4) = o2;
+  }
+}
+
+static int grid_n8(int64_t n) {
+  int64_t b = (n / 8 + 255) / 256;
+  return (int)(b < 4096 ? (b < 1 ? 1 : b) : 4096);
+}
+
+extern "C" int mp_act_fwd(const void* a, void* g, int64_t n, int act, float p, uint64_t seed, hipStream_t st) {
+  if (n % 8) return -1;
+  act_fwd_kernel<<<grid_n8(n), 256, 0, st>>>((const bf16_t*)a, (bf16_t*)g, n, act, p, seed);
+  return (int)hipGetLastError();
+}
+
+static void colsum_grid(int rows, int cols, dim3& grid, int& rpb) {
+  const int ny = (cols / 8 + 63) / 64;
+  int nx = 1024 / ny;
+  if (nx < 1) nx = 1;
+  if (nx > (rows + 3) / 4) nx = (rows + 3) / 4;
+  rpb = (rows + nx - 1) / nx;
+  grid = dim3((rows + rpb - 1) / rpb, ny);
+}
+
+extern "C" int mp_act_bwd(const void* dg, const void* a, void* da, float* dbias, int rows, int cols, int act, float p,
+                          uint64_t seed, hipStream_t st) {
+  if (cols % 8) return -1;
+  dim3 grid;
+  int rpb;
+  colsum_grid(rows, cols, grid, rpb);
+  colsum_kernel<1><<<grid, 256, 0, st>>>((const bf16_t*)dg, (const bf16_t*)a, (bf16_t*)da, dbias, rows, cols, rpb, act,
+                                         p, seed);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp_colsum(const void* x, float* dbias, int rows, int cols, hipStream_t st) {
+  if (cols % 8) return -1;
+  dim3 grid;
+  int rpb;
+  colsum_grid(rows, cols, grid, rpb);
+  colsum_kernel<0><<<grid, 256, 0, st>>>((const bf16_t*)x, nullptr, nullptr, dbias, rows, cols, rpb, 0, 0.f, 0);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp_swiglu_fwd(const void* gu, void* y, int T, int F, hipStream_t st) {
+  if (F % 8) return -1;
+  swiglu_fwd_kernel<<<grid_n8((int64_t)T * F), 256, 0, st>>>((const bf16_t*)gu, (bf16_t*)y, T, F);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp_swiglu_bwd(const void* gu, const void* dy, void* dgu, int T, int F, hipStream_t st) {
+  if (F % 8) return -1;
+  swiglu_bwd_kernel<<<grid_n8((int64_t)T * F), 256, 0, st>>>((const bf16_t*)gu, (const bf16_t*)dy, (bf16_t*)dgu, T, F);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp_rope(void* qkv, const float* cs, const float* sn, int T, int S, int H, int Hkv, int Dh,
+                       int pos_offset, int inverse, hipStream_t st) {
+  if (Dh % 8) return -1;
+  const int64_t total = (int64_t)T * (H + Hkv) * (Dh / 8);
+  int64_t b = (total + 255) / 256;
+  rope_kernel<<<(int)(b < 4096 ? b : 4096), 256, 0, st>>>((bf16_t*)qkv, cs, sn, T, S, H, Hkv, Dh, pos_offset,
+                                                          inverse ? -1.f : 1.f);
+  return (int)hipGetLastError();
+}

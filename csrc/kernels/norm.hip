@@ -1,0 +1,282 @@
+// Fused residual-add (+dropout) + LayerNorm / RMSNorm, forward and backward.
+//
+// Forward (one wave per row, 16-byte bf16 vectors, row kept in registers):
+//     s = a + dropout(b)        (optional; written out as the new residual stream)
+//     y = norm(s) * w (+ bias)  (LayerNorm or RMSNorm)
+//     mean / rstd saved in f32 for the backward
+// Backward:
+//     dxhat = dy * w
+//     ds = rstd * (dxhat - mean(dxhat) - xhat * mean(dxhat * xhat))   (LN; RMS drops the mean term)
+//     ds += dres                 (gradient arriving through the residual path, fused)
+//     db_branch = ds * mask      (optional: grad into the dropout branch)
+//     dw += sum_rows(dy * xhat), dbias += sum_rows(dy): per-block partials in
+//     registers, reduced across the block's waves in LDS, one f32 atomic per column.
+// SURVEY §2.5 K7 (post-LN: 3 per layer + final) and the pre-norm GPT-2 / Llama blocks.
+#include "mp_common.h"
+
+using namespace mp;
+
+template <int MAXJ, bool RMS, bool HAS_B, bool HAS_BIAS>
+__global__ void __launch_bounds__(256) norm_fwd_kernel(
+    const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, const bf16_t* __restrict__ w,
+    const bf16_t* __restrict__ bias, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y, float* __restrict__ mean_out,
+    float* __restrict__ rstd_out, int rows, int D, float eps, float p_drop, uint64_t seed) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nchunk = D >> 3;
+  float v[MAXJ][8];
+  const size_t base = (size_t)row * D;
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nchunk) {
+      u16x8 av = *reinterpret_cast<const u16x8*>(a + base + c * 8);
+      u16x8 bv;
+      if (HAS_B) bv = *reinterpret_cast<const u16x8*>(b + base + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float x = bf2f(av[e]);
+        if (HAS_B) {
+          float bb = bf2f(bv[e]);
+          if (p_drop > 0.f) bb *= dropout_scale(seed, base + c * 8 + e, p_drop);
+          x = bf2f(f2bf(x + bb));  // residual stream is stored in bf16: normalise what is stored
+        }
+        v[j][e] = x;
+        sum += x;
+      }
+      if (HAS_B) {
+        u16x8 sv;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv[e] = f2bf(v[j][e]);
+        *reinterpret_cast<u16x8*>(s_out + base + c * 8) = sv;
+      }
+    }
+  }
+  float mean = 0.f;
+  if (!RMS) mean = wave_sum(sum) / D;
+  float sq = 0.f;
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nchunk) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float d = v[j][e] - mean;
+        sq += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) / D + eps);
+  if (lane == 0) {
+    if (!RMS) mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c = lane + 64 * j;
+    if (c < nchunk) {
+      u16x8 wv = *reinterpret_cast<const u16x8*>(w + c * 8);
+      u16x8 bv;
+      if (HAS_BIAS) bv = *reinterpret_cast<const u16x8*>(bias + c * 8);
+      u16x8 out;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float o = (v[j][e] - mean) * rstd * bf2f(wv[e]);
+        if (HAS_BIAS) o += bf2f(bv[e]);
+        out[e] = f2bf(o);
+      }
+      *reinterpret_cast<u16x8*>(y + base + c * 8) = out;
+    }
+  }
+}
+
+// Backward.  grid.x blocks, each handling a contiguous slab of rows (4 waves, wave-strided).
+template <int MAXJ, bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BRANCH_GRAD>
+__global__ void __launch_bounds__(256) norm_bwd_kernel(
+    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
+    bf16_t* __restrict__ ds_out, bf16_t* __restrict__ dbranch, float* __restrict__ dw, float* __restrict__ dbias,
+    int rows, int D, int rows_per_block, float p_drop, uint64_t seed) {
+  __shared__ float red[4][2][MAXJ * 64 * 8 > 1024 ? 1024 : MAXJ * 64 * 8];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int nchunk = D >> 3;
+  float acc_w[MAXJ][8], acc_b[MAXJ][8];
+  float wreg[MAXJ][8];
+#pragma unroll
+  for (int j = 0; j < MAXJ; ++j) {
+    const int c = lane + 64 * j;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc_w[j][e] = 0.f;
+      acc_b[j][e] = 0.f;
+      wreg[j][e] = 0.f;
+    }
+    if (c < nchunk) {
+      u16x8 wvv = *reinterpret_cast<const u16x8*>(w + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wreg[j][e] = bf2f(wvv[e]);
+    }
+  }
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + wv; row < r1; row += 4) {
+    const size_t base = (size_t)row * D;
+    const float mean = RMS ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float xh[MAXJ][8], g[MAXJ][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nchunk) {
+        u16x8 dv = *reinterpret_cast<const u16x8*>(dy + base + c * 8);
+        u16x8 sv = *reinterpret_cast<const u16x8*>(s + base + c * 8);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float d = bf2f(dv[e]);
+          float x = (bf2f(sv[e]) - mean) * rstd;
+          xh[j][e] = x;
+          float gg = d * wreg[j][e];
+          g[j][e] = gg;
+          s1 += gg;
+          s2 += gg * x;
+          acc_w[j][e] += d * x;
+          if (HAS_BIAS) acc_b[j][e] += d;
+        }
+      }
+    }
+    s1 = RMS ? 0.f : wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nchunk) {
+        u16x8 rv;
+        if (HAS_DRES) rv = *reinterpret_cast<const u16x8*>(dres + base + c * 8);
+        u16x8 out, bout;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = rstd * (g[j][e] - s1 - xh[j][e] * s2);
+          if (HAS_DRES) v += bf2f(rv[e]);
+          out[e] = f2bf(v);
+          if (BRANCH_GRAD) bout[e] = f2bf(v * dropout_scale(seed, base + c * 8 + e, p_drop));
+        }
+        *reinterpret_cast<u16x8*>(ds_out + base + c * 8) = out;
+        if (BRANCH_GRAD) *reinterpret_cast<u16x8*>(dbranch + base + c * 8) = bout;
+      }
+    }
+  }
+  // reduce per-column partials over the 4 waves, then one atomic per column
+  constexpr int CAP = MAXJ * 64 * 8 > 1024 ? 1024 : MAXJ * 64 * 8;
+#pragma unroll
+  for (int j0 = 0; j0 < MAXJ; j0 += CAP / 512) {
+    __syncthreads();
+#pragma unroll
+    for (int jj = 0; jj < CAP / 512; ++jj) {
+      const int j = j0 + jj;
+      if (j < MAXJ) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          red[wv][0][(jj * 64 + lane) * 8 + e] = acc_w[j][e];
+          red[wv][1][(jj * 64 + lane) * 8 + e] = acc_b[j][e];
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < CAP; i += 256) {
+      const int jj = i / 512, rem = i % 512, ln = rem / 8, e = rem % 8;
+      const int j = j0 + jj;
+      const int c = ln + 64 * j;
+      if (j < MAXJ && c < nchunk) {
+        float sw = red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i];
+        atomicAdd(dw + c * 8 + e, sw);
+        if (HAS_BIAS) {
+          float sb = red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i];
+          atomicAdd(dbias + c * 8 + e, sb);
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ launchers
+template <bool RMS, bool HAS_B, bool HAS_BIAS>
+static void launch_fwd(int maxj, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
+                       float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed, hipStream_t st) {
+  dim3 grid((rows + 3) / 4), block(256);
+#define MP_FWD(J)                                                                                                  \
+  case J:                                                                                                          \
+    norm_fwd_kernel<J, RMS, HAS_B, HAS_BIAS><<<grid, block, 0, st>>>(                                             \
+        (const bf16_t*)a, (const bf16_t*)b, (const bf16_t*)w, (const bf16_t*)bias, (bf16_t*)s_out, (bf16_t*)y, mean, \
+        rstd, rows, D, eps, p, seed);                                                                              \
+    break;
+  switch (maxj) { MP_FWD(1) MP_FWD(2) MP_FWD(4) MP_FWD(8) MP_FWD(10) MP_FWD(16) }
+#undef MP_FWD
+}
+
+static int pick_j(int D) {
+  int n = (D / 8 + 63) / 64;
+  if (n <= 1) return 1;
+  if (n <= 2) return 2;
+  if (n <= 4) return 4;
+  if (n <= 8) return 8;
+  if (n <= 10) return 10;
+  return 16;
+}
+
+extern "C" int mp_norm_fwd(int rms, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
+                           float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed,
+                           hipStream_t st) {
+  if (D % 8 != 0 || D > 16 * 512) return -1;
+  const int J = pick_j(D);
+  const bool hb = b != nullptr, hbias = bias != nullptr;
+  if (rms) {
+    if (hb) hbias ? launch_fwd<true, true, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+            : launch_fwd<true, true, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+    else hbias ? launch_fwd<true, false, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+               : launch_fwd<true, false, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+  } else {
+    if (hb) hbias ? launch_fwd<false, true, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+            : launch_fwd<false, true, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+    else hbias ? launch_fwd<false, false, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+               : launch_fwd<false, false, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+  }
+  return (int)hipGetLastError();
+}
+
+template <bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG>
+static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
+                       const void* dres, void* ds, void* dbr, float* dw, float* db, int rows, int D, float p,
+                       uint64_t seed, hipStream_t st) {
+  const int nblk = rows < 512 ? (rows + 3) / 4 : 512;
+  const int rpb = (rows + nblk - 1) / nblk;
+  dim3 grid((rows + rpb - 1) / rpb), block(256);
+#define MP_BWD(J)                                                                                                   \
+  case J:                                                                                                           \
+    norm_bwd_kernel<J, RMS, HAS_DRES, HAS_BIAS, BG><<<grid, block, 0, st>>>(                                        \
+        (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)ds,        \
+        (bf16_t*)dbr, dw, db, rows, D, rpb, p, seed);                                                               \
+    break;
+  switch (maxj) { MP_BWD(1) MP_BWD(2) MP_BWD(4) MP_BWD(8) MP_BWD(10) MP_BWD(16) }
+#undef MP_BWD
+}
+
+extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean,
+                           const float* rstd, const void* dres, void* ds, void* dbranch, float* dw, float* dbias,
+                           int rows, int D, float p, uint64_t seed, hipStream_t st) {
+  if (D % 8 != 0 || D > 16 * 512) return -1;
+  const int J = pick_j(D);
+  const bool hd = dres != nullptr, hb = dbias != nullptr, bg = dbranch != nullptr;
+#define MP_B(R, HD, HB, BG_)                                                                                  \
+  if (rms == R && hd == HD && hb == HB && bg == BG_) {                                                         \
+    launch_bwd<R, HD, HB, BG_>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, rows, D, p, seed, st); \
+    return (int)hipGetLastError();                                                                           \
+  }
+  MP_B(0, 0, 0, 0) MP_B(0, 0, 0, 1) MP_B(0, 0, 1, 0) MP_B(0, 0, 1, 1)
+  MP_B(0, 1, 0, 0) MP_B(0, 1, 0, 1) MP_B(0, 1, 1, 0) MP_B(0, 1, 1, 1)
+  MP_B(1, 0, 0, 0) MP_B(1, 0, 0, 1) MP_B(1, 1, 0, 0) MP_B(1, 1, 0, 1)
+#undef MP_B
+  return -2;
+}

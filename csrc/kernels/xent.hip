@@ -1,0 +1,78 @@
+// Fused softmax cross-entropy, forward + backward in one kernel.
+//
+// One 256-thread block per token row of the [T, Vp] bf16 logits:
+//   pass 1: online max / sum-exp over the row (16-byte loads), block-reduced;
+//   pass 2: dlogits = (softmax - onehot(target)) * grad_scale written IN PLACE over
+//           the logits (the row is L2-resident from pass 1), so the [T, V] logits are
+//           never re-read by a separate backward kernel and no second buffer exists.
+// Columns >= V (vocab padded to a multiple of 64 for the GEMMs, e.g. GPT-2's 50257
+// -> 50304) are excluded from the softmax and get zero gradient.  Targets equal to
+// ignore_index produce zero loss and zero gradient.
+#include "mp_common.h"
+
+using namespace mp;
+
+template <bool WRITE_GRAD>
+__global__ void __launch_bounds__(256) xent_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ target,
+                                                   float* __restrict__ loss, int T, int V, int Vp, float grad_scale,
+                                                   int64_t ignore_index) {
+  __shared__ float red[8];
+  const int row = blockIdx.x;
+  bf16_t* x = logits + (size_t)row * Vp;
+  const int64_t tgt = target[row];
+  const int nvec = V >> 3;  // full 8-wide chunks inside the real vocab
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x; c < nvec; c += 256) {
+    u16x8 v = *reinterpret_cast<const u16x8*>(x + c * 8);
+    float f[8];
+    float lm = m;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      f[e] = bf2f(v[e]);
+      lm = fmaxf(lm, f[e]);
+    }
+    s *= __expf(m - lm);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s += __expf(f[e] - lm);
+    m = lm;
+  }
+  for (int j = nvec * 8 + threadIdx.x; j < V; j += 256) {
+    float f = bf2f(x[j]);
+    float lm = fmaxf(m, f);
+    s = s * __expf(m - lm) + __expf(f - lm);
+    m = lm;
+  }
+  const float gm = block_max<256>(m, red);
+  s = (m == -INFINITY) ? 0.f : s * __expf(m - gm);
+  __syncthreads();
+  const float gs = block_sum<256>(s, red);
+  const float lse = gm + __logf(gs);
+  const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
+  if (threadIdx.x == 0) loss[row] = valid ? lse - bf2f(x[tgt]) : 0.f;
+  if (!WRITE_GRAD) return;
+  __syncthreads();  // everyone has read x[tgt] before it is overwritten
+  const float sc = valid ? grad_scale : 0.f;
+  const int nvec_p = Vp >> 3;
+  for (int c = threadIdx.x; c < nvec_p; c += 256) {
+    u16x8 v = *reinterpret_cast<const u16x8*>(x + c * 8);
+    u16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int j = c * 8 + e;
+      float g = 0.f;
+      if (j < V) g = (__expf(bf2f(v[e]) - lse) - (j == tgt ? 1.f : 0.f)) * sc;
+      o[e] = f2bf(g);
+    }
+    *reinterpret_cast<u16x8*>(x + c * 8) = o;
+  }
+}
+
+extern "C" int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss, int T, int V, int Vp,
+                               float grad_scale, int64_t ignore_index, int write_grad, hipStream_t st) {
+  if (Vp % 8 != 0 || V > Vp) return -1;
+  if (write_grad)
+    xent_kernel<true><<<T, 256, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale, ignore_index);
+  else
+    xent_kernel<false><<<T, 256, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale, ignore_index);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,536 @@
+"""Op wrappers: GPU -> HIP kernels in ``_C.so``; CPU -> PyTorch f32 reference math."""
+from __future__ import annotations
+
+import importlib.util
+import math
+import os
+from typing import Optional, Tuple
+
+import torch
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_EXT = None
+_EXT_ERR: Optional[str] = None
+
+ACT = {"none": 0, "gelu_tanh": 1, "gelu": 1, "relu": 2}
+EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RELU, EPI_BIAS_RES, EPI_RES, EPI_DGELU, EPI_DRELU = range(8)
+LOG2E = 1.4426950408889634
+
+# GEMM backend for plain (epilogue-free) GEMMs on GPU: "hip" (our MFMA kernel) or "blas"
+# (hipBLASLt through torch).  Fused-epilogue GEMMs always use the HIP kernel.
+GEMM_BACKEND = os.environ.get("MIPIPE_GEMM", "hip")
+
+
+def load_ext():
+    global _EXT, _EXT_ERR
+    if _EXT is not None or _EXT_ERR is not None:
+        return _EXT
+    path = os.path.join(_PKG_DIR, "_C.so")
+    if not os.path.exists(path):
+        _EXT_ERR = f"{path} not found (build it with: python tools/build_ext.py)"
+        return None
+    try:
+        import torch  # noqa: F401  (libtorch must be loaded first)
+        spec = importlib.util.spec_from_file_location("mipipe._C", path)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _EXT = mod
+    except Exception as e:  # pragma: no cover - depends on build
+        _EXT_ERR = f"failed to load {path}: {e}"
+    return _EXT
+
+
+def ext_available() -> bool:
+    return load_ext() is not None
+
+
+def _ext():
+    e = load_ext()
+    if e is None:
+        raise RuntimeError(f"mipipe HIP extension unavailable on a GPU tensor: {_EXT_ERR}")
+    return e
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+# ======================================================================================
+# normalisation (+ fused residual add / dropout)
+# ======================================================================================
+def _cpu_dropout_mask(shape, p, seed, device):
+    g = torch.Generator(device="cpu").manual_seed(int(seed) & 0x7FFFFFFFFFFFFFFF)
+    keep = (torch.rand(shape, generator=g) >= p).float() / (1.0 - p)
+    return keep.to(device)
+
+
+def norm_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None,
+             branch: Optional[torch.Tensor] = None, kind: str = "layernorm", eps: float = 1e-5,
+             p_drop: float = 0.0, seed: int = 0, y=None, s=None, mean=None, rstd=None):
+    """s = x + dropout(branch) (if branch given); y = norm(s) * w (+ bias).  Returns (y, s, mean, rstd)."""
+    rms = kind == "rmsnorm"
+    D = x.shape[-1]
+    rows = x.numel() // D
+    if y is None:
+        y = torch.empty_like(x)
+    if branch is not None and s is None:
+        s = torch.empty_like(x)
+    if rstd is None:
+        rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    if mean is None and not rms:
+        mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    if _gpu(x):
+        _ext().norm_fwd(rms, x, branch, w, bias, s if branch is not None else None, y, mean, rstd, float(eps),
+                        float(p_drop), int(seed))
+        return y, (s if branch is not None else x), mean, rstd
+    xf = x.float()
+    if branch is not None:
+        bf = branch.float()
+        if p_drop > 0:
+            bf = bf * _cpu_dropout_mask(bf.shape, p_drop, seed, x.device)
+        xf = (xf + bf).to(x.dtype).float()
+        s.copy_(xf.to(x.dtype))
+    src = xf.reshape(rows, D)
+    mu = torch.zeros(rows) if rms else src.mean(-1)
+    var = (src - mu[:, None]).pow(2).mean(-1)
+    r = torch.rsqrt(var + eps)
+    out = (src - mu[:, None]) * r[:, None] * w.float()
+    if bias is not None:
+        out = out + bias.float()
+    y.copy_(out.reshape(x.shape).to(y.dtype))
+    rstd.copy_(r)
+    if not rms:
+        mean.copy_(mu)
+    return y, (s if branch is not None else x), mean, rstd
+
+
+def norm_bwd(dy: torch.Tensor, s: torch.Tensor, w: torch.Tensor, mean, rstd, kind: str = "layernorm",
+             dres: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
+             dbias: Optional[torch.Tensor] = None, p_drop: float = 0.0, seed: int = 0, ds=None, dbranch=None,
+             want_branch: bool = False):
+    """ds = d(norm input) (+ dres); dw/dbias (f32) accumulate.  Returns (ds, dbranch)."""
+    rms = kind == "rmsnorm"
+    D = dy.shape[-1]
+    rows = dy.numel() // D
+    if ds is None:
+        ds = torch.empty_like(dy)
+    need_branch = want_branch and p_drop > 0
+    if need_branch and dbranch is None:
+        dbranch = torch.empty_like(dy)
+    if _gpu(dy):
+        _ext().norm_bwd(rms, dy, s, w, mean, rstd, dres, ds, dbranch if need_branch else None, dw, dbias,
+                        float(p_drop), int(seed))
+        return ds, (dbranch if need_branch else (ds if want_branch else None))
+    d = dy.float().reshape(rows, D)
+    x = s.float().reshape(rows, D)
+    mu = torch.zeros(rows) if rms else mean.float()
+    xh = (x - mu[:, None]) * rstd[:, None]
+    g = d * w.float()
+    s1 = torch.zeros(rows, 1) if rms else g.mean(-1, keepdim=True)
+    s2 = (g * xh).mean(-1, keepdim=True)
+    v = rstd[:, None] * (g - s1 - xh * s2)
+    if dres is not None:
+        v = v + dres.float().reshape(rows, D)
+    ds.copy_(v.reshape(dy.shape).to(ds.dtype))
+    if dw is not None:
+        dw += (d * xh).sum(0)
+    if dbias is not None:
+        dbias += d.sum(0)
+    if need_branch:
+        m = _cpu_dropout_mask(dy.shape, p_drop, seed, dy.device)
+        dbranch.copy_((v.reshape(dy.shape) * m).to(dbranch.dtype))
+        return ds, dbranch
+    return ds, (ds if want_branch else None)
+
+
+# ======================================================================================
+# fused softmax cross-entropy
+# ======================================================================================
+def xent_fwd_bwd(logits: torch.Tensor, target: torch.Tensor, vocab: int, grad_scale: float,
+                 ignore_index: int = -100, write_grad: bool = True, loss: Optional[torch.Tensor] = None):
+    """Per-row CE loss (f32 [T]); if write_grad, logits are overwritten IN PLACE by
+    (softmax - onehot) * grad_scale (padded vocab columns -> 0)."""
+    Vp = logits.shape[-1]
+    T = logits.numel() // Vp
+    if loss is None:
+        loss = torch.empty(T, device=logits.device, dtype=torch.float32)
+    if _gpu(logits):
+        _ext().xent(logits, target, loss, int(vocab), float(grad_scale), int(ignore_index), bool(write_grad))
+        return loss
+    lg = logits.float().reshape(T, Vp)[:, :vocab]
+    tg = target.reshape(T)
+    lse = torch.logsumexp(lg, -1)
+    valid = tg != ignore_index
+    tsafe = torch.where(valid, tg, torch.zeros_like(tg))
+    l = lse - lg.gather(1, tsafe[:, None])[:, 0]
+    loss.copy_(torch.where(valid, l, torch.zeros_like(l)))
+    if write_grad:
+        p = torch.softmax(lg, -1)
+        p[torch.arange(T), tsafe] -= 1.0
+        p = p * grad_scale * valid[:, None].float()
+        out = torch.zeros(T, Vp)
+        out[:, :vocab] = p
+        logits.copy_(out.reshape(logits.shape).to(logits.dtype))
+    return loss
+
+
+# ======================================================================================
+# embeddings
+# ======================================================================================
+def embed_fwd(idx: torch.Tensor, wte: torch.Tensor, wpe: Optional[torch.Tensor], S: int, pos_offset: int = 0,
+              out: Optional[torch.Tensor] = None):
+    T = idx.numel()
+    D = wte.shape[1]
+    if out is None:
+        out = torch.empty(T, D, device=wte.device, dtype=wte.dtype)
+    if _gpu(wte):
+        _ext().embed_fwd(idx.reshape(-1), wte, wpe, out, int(S), int(pos_offset))
+        return out
+    e = wte.float()[idx.reshape(-1)]
+    if wpe is not None:
+        pos = torch.arange(T) % S + pos_offset
+        e = e + wpe.float()[pos]
+    out.copy_(e.to(out.dtype))
+    return out
+
+
+def embed_bwd(idx: torch.Tensor, dout: torch.Tensor, dwte: torch.Tensor, dwpe: Optional[torch.Tensor], S: int,
+              pos_offset: int = 0):
+    if _gpu(dout):
+        _ext().embed_bwd(idx.reshape(-1), dout, dwte, dwpe, int(S), int(pos_offset))
+        return
+    T = idx.numel()
+    d = dout.float().reshape(T, -1)
+    dwte.index_add_(0, idx.reshape(-1), d)
+    if dwpe is not None:
+        pos = torch.arange(T) % S + pos_offset
+        dwpe.index_add_(0, pos, d)
+
+
+# ======================================================================================
+# GEMMs (linear layers)
+# ======================================================================================
+def _gemm(A, B, C, bias=None, residual=None, aux=None, transA=False, transB=False, epi=EPI_NONE, accum=False,
+          alpha=1.0):
+    _ext().gemm(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum), float(alpha))
+    return C
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
+           residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
+           aux: Optional[torch.Tensor] = None):
+    """y = act(x @ w^T + bias) (+ residual).  x [T,K], w [N,K].  With an activation the
+    pre-activation is written to ``aux`` (needed by the backward).  Returns (y, aux)."""
+    T, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty(T, N, device=x.device, dtype=x.dtype)
+    if act != "none" and aux is None:
+        aux = torch.empty(T, N, device=x.device, dtype=x.dtype)
+    if _gpu(x):
+        if act != "none":
+            if bias is None or residual is not None:
+                raise ValueError("activation epilogue needs a bias and no residual")
+            _gemm(x, w, out, bias=bias, aux=aux, epi=EPI_BIAS_GELU if ACT[act] == 1 else EPI_BIAS_RELU)
+        elif residual is not None:
+            _gemm(x, w, out, bias=bias, residual=residual, epi=EPI_BIAS_RES if bias is not None else EPI_RES)
+        elif bias is not None:
+            _gemm(x, w, out, bias=bias, epi=EPI_BIAS)
+        elif GEMM_BACKEND == "blas":
+            torch.mm(x, w.t(), out=out)
+        else:
+            _gemm(x, w, out)
+        return out, aux
+    y = x.float() @ w.float().t()
+    if bias is not None:
+        y = y + bias.float()
+    if act != "none":
+        pre = y.to(x.dtype)
+        aux.copy_(pre)
+        y = _act_cpu(pre.float(), act)
+    if residual is not None:
+        y = y + residual.float()
+    out.copy_(y.to(out.dtype))
+    return out, aux
+
+
+def _act_cpu(x, act):
+    if ACT[act] == 1:
+        return torch.nn.functional.gelu(x, approximate="tanh")
+    if ACT[act] == 2:
+        return torch.relu(x)
+    return x
+
+
+def _act_grad_cpu(x, act):
+    if ACT[act] == 1:
+        k0, k1 = 0.7978845608028654, 0.044715
+        u = k0 * (x + k1 * x ** 3)
+        t = torch.tanh(u)
+        return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k0 * (1 + 3 * k1 * x * x)
+    if ACT[act] == 2:
+        return (x > 0).float()
+    return torch.ones_like(x)
+
+
+def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tensor] = None, act: str = "none",
+              out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None):
+    """dx = dy @ w  (w [N,K]), optionally times act'(act_input) (the previous layer's
+    pre-activation) and plus ``residual``."""
+    T, N = dy.shape
+    K = w.shape[1]
+    if out is None:
+        out = torch.empty(T, K, device=dy.device, dtype=dy.dtype)
+    if _gpu(dy):
+        if act != "none":
+            _gemm(dy, w, out, aux=act_input, transB=True, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU)
+        elif residual is not None:
+            _gemm(dy, w, out, residual=residual, transB=True, epi=EPI_RES)
+        elif GEMM_BACKEND == "blas":
+            torch.mm(dy, w, out=out)
+        else:
+            _gemm(dy, w, out, transB=True)
+        return out
+    g = dy.float() @ w.float()
+    if act != "none":
+        g = g * _act_grad_cpu(act_input.float(), act)
+    if residual is not None:
+        g = g + residual.float()
+    out.copy_(g.to(out.dtype))
+    return out
+
+
+def linear_dw(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, alpha: float = 1.0):
+    """dw (f32 [N,K]) += alpha * dy^T @ x   (dy [T,N], x [T,K])."""
+    if _gpu(dy):
+        if GEMM_BACKEND == "blas":
+            dw.add_(torch.mm(dy.t(), x, out_dtype=torch.float32), alpha=alpha)
+        else:
+            _gemm(dy, x, dw, transA=True, transB=True, accum=True, alpha=alpha)
+        return dw
+    dw += alpha * (dy.float().t() @ x.float())
+    return dw
+
+
+# ======================================================================================
+# elementwise
+# ======================================================================================
+def act_fwd(a: torch.Tensor, act: str, p_drop: float = 0.0, seed: int = 0, out=None):
+    if out is None:
+        out = torch.empty_like(a)
+    if _gpu(a):
+        _ext().act_fwd(a, out, ACT[act], float(p_drop), int(seed))
+        return out
+    y = _act_cpu(a.float(), act)
+    if p_drop > 0:
+        y = y * _cpu_dropout_mask(a.shape, p_drop, seed, a.device)
+    out.copy_(y.to(out.dtype))
+    return out
+
+
+def act_bwd(dg: torch.Tensor, a: torch.Tensor, act: str, dbias: Optional[torch.Tensor] = None,
+            p_drop: float = 0.0, seed: int = 0, out=None):
+    if out is None:
+        out = torch.empty_like(dg)
+    if _gpu(dg):
+        _ext().act_bwd(dg, a, out, dbias, ACT[act], float(p_drop), int(seed))
+        return out
+    d = dg.float() * _act_grad_cpu(a.float(), act)
+    if p_drop > 0:
+        d = d * _cpu_dropout_mask(a.shape, p_drop, seed, a.device)
+    out.copy_(d.to(out.dtype))
+    if dbias is not None:
+        dbias += out.float().reshape(-1, out.shape[-1]).sum(0)
+    return out
+
+
+def colsum(x: torch.Tensor, dbias: torch.Tensor):
+    if _gpu(x):
+        _ext().colsum(x, dbias)
+        return dbias
+    dbias += x.float().reshape(-1, x.shape[-1]).sum(0)
+    return dbias
+
+
+def swiglu_fwd(gu: torch.Tensor, out=None):
+    T, F2 = gu.shape
+    F = F2 // 2
+    if out is None:
+        out = torch.empty(T, F, device=gu.device, dtype=gu.dtype)
+    if _gpu(gu):
+        _ext().swiglu_fwd(gu, out)
+        return out
+    g, u = gu.float()[:, :F], gu.float()[:, F:]
+    out.copy_((torch.nn.functional.silu(g) * u).to(out.dtype))
+    return out
+
+
+def swiglu_bwd(gu: torch.Tensor, dy: torch.Tensor, out=None):
+    if out is None:
+        out = torch.empty_like(gu)
+    if _gpu(gu):
+        _ext().swiglu_bwd(gu, dy, out)
+        return out
+    F = dy.shape[-1]
+    g, u, d = gu.float()[:, :F], gu.float()[:, F:], dy.float()
+    sg = torch.sigmoid(g)
+    out[:, F:] = (d * g * sg).to(out.dtype)
+    out[:, :F] = (d * u * sg * (1 + g * (1 - sg))).to(out.dtype)
+    return out
+
+
+def rope_tables(S: int, Dh: int, theta: float, device) -> Tuple[torch.Tensor, torch.Tensor]:
+    inv = 1.0 / (theta ** (torch.arange(0, Dh, 2, dtype=torch.float64) / Dh))
+    ang = torch.arange(S, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.cos(ang).float().to(device), torch.sin(ang).float().to(device)
+
+
+def rope_(qkv: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, S: int, H: int, Hkv: int, Dh: int,
+          pos_offset: int = 0, inverse: bool = False):
+    """In-place rotate-half RoPE on the q and k heads of a packed [T, (H+2Hkv)*Dh] buffer."""
+    if _gpu(qkv):
+        _ext().rope(qkv, cos, sin, int(S), int(H), int(Hkv), int(Dh), int(pos_offset), bool(inverse))
+        return qkv
+    T = qkv.shape[0]
+    x = qkv.float().reshape(T, H + 2 * Hkv, Dh)
+    pos = torch.arange(T) % S + pos_offset
+    c, s = cos[pos][:, None, :], sin[pos][:, None, :]
+    if inverse:
+        s = -s
+    half = Dh // 2
+    rot = x[:, : H + Hkv]
+    a, b = rot[..., :half], rot[..., half:]
+    new = torch.cat([a * c - b * s, b * c + a * s], -1)
+    x[:, : H + Hkv] = new
+    qkv.copy_(x.reshape(T, -1).to(qkv.dtype))
+    return qkv
+
+
+# ======================================================================================
+# attention
+# ======================================================================================
+def _heads(t: torch.Tensor, B: int, S: int, nh: int, D: int):
+    """token-major [B*S, stride] view (first nh*D cols) -> [B, nh, S, D] f32"""
+    return t[:, : nh * D].float().reshape(B, S, nh, D).permute(0, 2, 1, 3)
+
+
+def _cpu_attn_mask(B, H, Sq, Sk, causal, device):
+    if not causal:
+        return None
+    shift = Sk - Sq
+    q = torch.arange(Sq)[:, None]
+    k = torch.arange(Sk)[None, :]
+    return (k > q + shift).to(device)
+
+
+def _cpu_attn_drop(B, H, Sq, Sk, p, seed, device):
+    if p <= 0:
+        return None
+    return _cpu_dropout_mask((B, H, Sq, Sk), p, seed, device)
+
+
+def attn_fwd(q, k, v, o, lse, B: int, Sq: int, Sk: int, H: int, Hkv: int, D: int, causal: bool,
+             scale: Optional[float] = None, p_drop: float = 0.0, seed: int = 0):
+    """q/k/v/o: token-major 2-D views ([B*S, row_stride], head h at cols h*D).  lse: f32
+    [B*H*Sq] (log2 units).  Writes o and lse."""
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if _gpu(q):
+        _ext().attn_fwd(q, k, v, o, lse, B, Sq, Sk, H, Hkv, D, bool(causal), float(scale), float(p_drop), int(seed))
+        return o
+    Q, K, V = _heads(q, B, Sq, H, D), _heads(k, B, Sk, Hkv, D), _heads(v, B, Sk, Hkv, D)
+    rep = H // Hkv
+    K, V = K.repeat_interleave(rep, 1), V.repeat_interleave(rep, 1)
+    s = (Q @ K.transpose(-1, -2)) * scale
+    mask = _cpu_attn_mask(B, H, Sq, Sk, causal, q.device)
+    if mask is not None:
+        s = s.masked_fill(mask, float("-inf"))
+    l2 = torch.logsumexp(s, -1) * LOG2E
+    p = torch.softmax(s, -1)
+    dm = _cpu_attn_drop(B, H, Sq, Sk, p_drop, seed, q.device)
+    if dm is not None:
+        p = p * dm
+    out = (p @ V).permute(0, 2, 1, 3).reshape(B * Sq, H * D)
+    o[:, : H * D].copy_(out.to(o.dtype))
+    lse.view(-1)[: B * H * Sq].copy_(l2.reshape(-1))
+    return o
+
+
+def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B: int, Sq: int, Sk: int, H: int, Hkv: int, D: int, causal: bool,
+             scale: Optional[float] = None, p_drop: float = 0.0, seed: int = 0, delta=None):
+    """Writes dq, dk, dv (token-major views like the inputs)."""
+    scale = 1.0 / math.sqrt(D) if scale is None else scale
+    if _gpu(q):
+        if delta is None:
+            delta = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
+        _ext().attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, delta, B, Sq, Sk, H, Hkv, D, bool(causal),
+                        float(scale), float(p_drop), int(seed))
+        return dq, dk, dv
+    rep = H // Hkv
+    Q, K, V = _heads(q, B, Sq, H, D), _heads(k, B, Sk, Hkv, D), _heads(v, B, Sk, Hkv, D)
+    dO, O = _heads(do, B, Sq, H, D), _heads(o, B, Sq, H, D)
+    Kr, Vr = K.repeat_interleave(rep, 1), V.repeat_interleave(rep, 1)
+    s = (Q @ Kr.transpose(-1, -2)) * scale
+    mask = _cpu_attn_mask(B, H, Sq, Sk, causal, q.device)
+    if mask is not None:
+        s = s.masked_fill(mask, float("-inf"))
+    p = torch.softmax(s, -1)
+    dm = _cpu_attn_drop(B, H, Sq, Sk, p_drop, seed, q.device)
+    pd = p * dm if dm is not None else p
+    dV = pd.transpose(-1, -2) @ dO
+    dP = dO @ Vr.transpose(-1, -2)
+    if dm is not None:
+        dP = dP * dm
+    delta_ = (dO * O).sum(-1, keepdim=True)
+    dS = p * (dP - delta_)
+    dQ = (dS @ Kr) * scale
+    dK = (dS.transpose(-1, -2) @ Q) * scale
+    dK = dK.reshape(B, Hkv, rep, Sk, D).sum(2)
+    dV = dV.reshape(B, Hkv, rep, Sk, D).sum(2)
+    dq[:, : H * D].copy_(dQ.permute(0, 2, 1, 3).reshape(B * Sq, H * D).to(dq.dtype))
+    dk[:, : Hkv * D].copy_(dK.permute(0, 2, 1, 3).reshape(B * Sk, Hkv * D).to(dk.dtype))
+    dv[:, : Hkv * D].copy_(dV.permute(0, 2, 1, 3).reshape(B * Sk, Hkv * D).to(dv.dtype))
+    return dq, dk, dv
+
+
+# ======================================================================================
+# optimizer
+# ======================================================================================
+def sumsq(g: torch.Tensor, out: torch.Tensor):
+    if _gpu(g):
+        _ext().sumsq(g, out)
+        return out
+    out += (g.float() ** 2).sum()
+    return out
+
+
+def adamw_(p, g, m, v, w16, n_decay: int, lr: float, b1: float, b2: float, eps: float, wd: float, step: int,
+           sumsq_buf=None, max_norm: float = 0.0, grad_scale: float = 1.0, zero_grad: bool = True):
+    """Fused AdamW over flat f32 buffers; also refreshes the bf16 copy ``w16`` and zeroes g."""
+    if _gpu(p):
+        _ext().adamw(p, g, m, v, w16, int(n_decay), float(lr), float(b1), float(b2), float(eps), float(wd), int(step),
+                     sumsq_buf, float(max_norm), float(grad_scale), bool(zero_grad))
+        return
+    coef = grad_scale
+    if max_norm > 0 and sumsq_buf is not None:
+        nrm = math.sqrt(float(sumsq_buf.item())) * grad_scale
+        coef *= min(1.0, max_norm / (nrm + 1e-6))
+    gr = g * coef
+    m.mul_(b1).add_(gr, alpha=1 - b1)
+    v.mul_(b2).addcmul_(gr, gr, value=1 - b2)
+    bc1, bc2 = 1 - b1 ** step, 1 - b2 ** step
+    upd = (m / bc1) / ((v / bc2).sqrt() + eps)
+    decay = torch.zeros_like(p)
+    decay[:n_decay] = wd
+    p.sub_(lr * (upd + decay * p))
+    if zero_grad:
+        g.zero_()
+    if w16 is not None:
+        w16.copy_(p.to(w16.dtype))
+
+
+def cast_f32_bf16(src: torch.Tensor, dst: torch.Tensor):
+    if _gpu(src):
+        _ext().cast_f32_bf16(src, dst)
+    else:
+        dst.copy_(src.to(dst.dtype))
+    return dst

@@ -1,0 +1,231 @@
+"""HIP kernel numerics vs. the PyTorch f32 reference of the same op (SURVEY §4 tier 3).
+
+Every GPU op in mipipe.ops is compared with its CPU/f32 implementation (which is itself
+checked against torch.nn.functional in test_ops_cpu.py).  bf16 tolerances."""
+import math
+
+import pytest
+import torch
+
+import mipipe  # noqa: F401
+from mipipe import ops
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def setup_module(module):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert ops.ext_available(), "HIP extension must be built for GPU tests"
+
+
+def rnd(*shape, scale=1.0, dtype=torch.bfloat16):
+    return (torch.randn(*shape) * scale).to(dtype)
+
+
+def close(a, b, atol=2e-2, rtol=2e-2):
+    torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
+
+
+@pytest.mark.parametrize("kind", ["layernorm", "rmsnorm"])
+@pytest.mark.parametrize("D", [64, 768, 1024, 4096])
+@pytest.mark.parametrize("branch", [False, True])
+def test_norm_fwd_bwd(kind, D, branch):
+    torch.manual_seed(0)
+    T = 257
+    x, w = rnd(T, D), rnd(D, scale=0.5) + 1
+    bias = rnd(D, scale=0.1) if kind == "layernorm" else None
+    br = rnd(T, D) if branch else None
+    dy, dres = rnd(T, D), rnd(T, D)
+    outs = []
+    for dev in ("cpu", DEV):
+        mv = lambda t: None if t is None else t.to(dev)
+        y, s, mean, rstd = ops.norm_fwd(mv(x), mv(w), mv(bias), mv(br), kind=kind)
+        dw = torch.zeros(D, device=dev)
+        db = torch.zeros(D, device=dev) if bias is not None else None
+        ds, _ = ops.norm_bwd(mv(dy), s, mv(w), mean, rstd, kind=kind, dres=mv(dres), dw=dw, dbias=db)
+        outs.append((y, s, rstd, ds, dw, db))
+    for a, b in zip(*outs):
+        if a is not None:
+            close(b, a, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("V,Vp", [(50257, 50304), (10000, 10000), (1000, 1024)])
+def test_xent(V, Vp):
+    torch.manual_seed(0)
+    T = 64
+    logits = rnd(T, Vp, scale=3.0)
+    tgt = torch.randint(0, V, (T,))
+    tgt[5] = -100
+    ref_l = logits.clone()
+    ref = ops.xent_fwd_bwd(ref_l, tgt, V, 1.0 / T)
+    gl = logits.to(DEV)
+    got = ops.xent_fwd_bwd(gl, tgt.to(DEV), V, 1.0 / T)
+    close(got, ref, atol=2e-3, rtol=1e-3)
+    close(gl, ref_l, atol=1e-4, rtol=2e-2)
+    # against torch.nn.functional
+    t2 = torch.nn.functional.cross_entropy(logits[:, :V].float(), tgt, reduction="none")
+    close(got, t2, atol=2e-3, rtol=1e-3)
+
+
+def test_embedding():
+    torch.manual_seed(0)
+    V, D, S, B = 1000, 768, 64, 4
+    wte, wpe = rnd(V, D), rnd(S, D)
+    idx = torch.randint(0, V, (B * S,))
+    ref = ops.embed_fwd(idx, wte, wpe, S)
+    got = ops.embed_fwd(idx.to(DEV), wte.to(DEV), wpe.to(DEV), S)
+    close(got, ref, atol=1e-2, rtol=1e-2)
+    dout = rnd(B * S, D)
+    dw1, dp1 = torch.zeros(V, D), torch.zeros(S, D)
+    ops.embed_bwd(idx, dout, dw1, dp1, S)
+    dw2, dp2 = torch.zeros(V, D, device=DEV), torch.zeros(S, D, device=DEV)
+    ops.embed_bwd(idx.to(DEV), dout.to(DEV), dw2, dp2, S)
+    close(dw2, dw1, atol=1e-3, rtol=1e-3)
+    close(dp2, dp1, atol=1e-3, rtol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 384, 128), (8192 // 8, 768, 768), (300, 136, 192), (128, 10000, 64)])
+@pytest.mark.parametrize("epi", ["none", "bias", "gelu", "relu", "bias_res"])
+def test_linear_fwd(M, N, K, epi):
+    torch.manual_seed(0)
+    x, w, b, r = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1), rnd(M, N)
+    kw = dict(bias=None, act="none", residual=None)
+    if epi in ("bias", "gelu", "relu", "bias_res"):
+        kw["bias"] = b
+    if epi in ("gelu", "relu"):
+        kw["act"] = "gelu_tanh" if epi == "gelu" else "relu"
+    if epi == "bias_res":
+        kw["residual"] = r
+    ref, ref_aux = ops.linear(x, w, **kw)
+    g = {k: (v.to(DEV) if isinstance(v, torch.Tensor) else v) for k, v in kw.items()}
+    got, got_aux = ops.linear(x.to(DEV), w.to(DEV), **g)
+    close(got, ref)
+    if ref_aux is not None:
+        close(got_aux, ref_aux)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 3072), (256, 384, 128), (200, 128, 136)])
+@pytest.mark.parametrize("act", ["none", "gelu_tanh", "relu"])
+def test_linear_dx(M, N, K, act):
+    torch.manual_seed(0)
+    dy, w, a = rnd(M, N), rnd(N, K, scale=N ** -0.5), rnd(M, K)
+    ref = ops.linear_dx(dy, w, act_input=a if act != "none" else None, act=act)
+    got = ops.linear_dx(dy.to(DEV), w.to(DEV), act_input=a.to(DEV) if act != "none" else None, act=act)
+    close(got, ref)
+
+
+@pytest.mark.parametrize("T,N,K", [(1024, 768, 768), (512, 2304, 768), (256, 136, 200), (128, 10000, 64)])
+def test_linear_dw(T, N, K):
+    torch.manual_seed(0)
+    dy, x = rnd(T, N, scale=0.1), rnd(T, K)
+    base = torch.randn(N, K)
+    ref = ops.linear_dw(dy, x, base.clone())
+    got = ops.linear_dw(dy.to(DEV), x.to(DEV), base.clone().to(DEV))
+    close(got, ref, atol=2e-2, rtol=1e-2)
+
+
+def test_gemm_asymmetric_layout_check():
+    """A = I with an asymmetric B catches transposed C writes (cdna guide §3)."""
+    n = 128
+    eye = torch.eye(n, dtype=torch.bfloat16)
+    B = (torch.arange(n * n, dtype=torch.float32).reshape(n, n) % 61 - 30).to(torch.bfloat16)
+    got, _ = ops.linear(eye.to(DEV), B.to(DEV))
+    close(got, B.t().contiguous(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("act", ["gelu_tanh", "relu"])
+def test_act_and_colsum(act):
+    torch.manual_seed(0)
+    a, dg = rnd(333, 3072), rnd(333, 3072)
+    close(ops.act_fwd(a.to(DEV), act), ops.act_fwd(a, act))
+    db1, db2 = torch.zeros(3072), torch.zeros(3072, device=DEV)
+    r = ops.act_bwd(dg, a, act, dbias=db1)
+    g = ops.act_bwd(dg.to(DEV), a.to(DEV), act, dbias=db2)
+    close(g, r)
+    close(db2, db1, atol=5e-2, rtol=2e-2)
+    c1, c2 = torch.zeros(3072), torch.zeros(3072, device=DEV)
+    close(ops.colsum(dg.to(DEV), c2), ops.colsum(dg, c1), atol=5e-2, rtol=2e-2)
+
+
+def test_swiglu_and_rope():
+    torch.manual_seed(0)
+    T, F = 130, 1024
+    gu, dy = rnd(T, 2 * F), rnd(T, F)
+    close(ops.swiglu_fwd(gu.to(DEV)), ops.swiglu_fwd(gu))
+    close(ops.swiglu_bwd(gu.to(DEV), dy.to(DEV)), ops.swiglu_bwd(gu, dy))
+    S, H, Hkv, Dh = 65, 4, 2, 128
+    qkv = rnd(2 * S, (H + 2 * Hkv) * Dh)
+    cs, sn = ops.rope_tables(S, Dh, 500000.0, "cpu")
+    r = ops.rope_(qkv.clone(), cs, sn, S, H, Hkv, Dh)
+    g = ops.rope_(qkv.clone().to(DEV), cs.to(DEV), sn.to(DEV), S, H, Hkv, Dh)
+    close(g, r)
+    back = ops.rope_(g.clone(), cs.to(DEV), sn.to(DEV), S, H, Hkv, Dh, inverse=True)
+    close(back, qkv, atol=3e-2, rtol=3e-2)
+
+
+ATTN = [  # B, S, H, Hkv, D, causal
+    (2, 256, 4, 4, 64, True), (2, 256, 4, 4, 64, False), (1, 200, 2, 2, 64, True),
+    (2, 128, 8, 8, 96, False), (1, 256, 4, 2, 128, True), (1, 128, 4, 4, 192, False), (1, 1024, 2, 2, 64, True)]
+
+
+@pytest.mark.parametrize("B,S,H,Hkv,D,causal", ATTN)
+def test_attention_fwd_bwd(B, S, H, Hkv, D, causal):
+    torch.manual_seed(0)
+    T = B * S
+    qkv = rnd(T, (H + 2 * Hkv) * D)
+    q, k, v = qkv[:, : H * D], qkv[:, H * D:(H + Hkv) * D], qkv[:, (H + Hkv) * D:]
+    do = rnd(T, H * D)
+    res = {}
+    for dev in ("cpu", DEV):
+        Q = qkv.to(dev)
+        qq, kk, vv = Q[:, : H * D], Q[:, H * D:(H + Hkv) * D], Q[:, (H + Hkv) * D:]
+        o = torch.empty(T, H * D, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B * H * S, device=dev)
+        ops.attn_fwd(qq, kk, vv, o, lse, B, S, S, H, Hkv, D, causal)
+        dqkv = torch.zeros_like(Q)
+        dq, dk, dv = dqkv[:, : H * D], dqkv[:, H * D:(H + Hkv) * D], dqkv[:, (H + Hkv) * D:]
+        ops.attn_bwd(qq, kk, vv, o, do.to(dev), lse, dq, dk, dv, B, S, S, H, Hkv, D, causal)
+        res[dev] = (o, lse, dqkv)
+    close(res[DEV][0], res["cpu"][0], atol=2e-2, rtol=2e-2)
+    close(res[DEV][1], res["cpu"][1], atol=2e-2, rtol=1e-3)
+    close(res[DEV][2], res["cpu"][2], atol=5e-2, rtol=5e-2)
+
+
+def test_attention_dropout_consistency():
+    """fwd/bwd regenerate the same mask: gradient check by finite differences in f32 space
+    is too noisy in bf16, so check the keep-rate and that dropout=0 reproduces no-dropout."""
+    torch.manual_seed(0)
+    B, S, H, D = 1, 128, 2, 64
+    T = B * S
+    qkv = rnd(T, 3 * H * D).to(DEV)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
+    o1 = torch.empty(T, H * D, dtype=torch.bfloat16, device=DEV)
+    o2 = torch.empty_like(o1)
+    lse = torch.empty(B * H * S, device=DEV)
+    ops.attn_fwd(q, k, v, o1, lse, B, S, S, H, H, D, False, p_drop=0.0)
+    ops.attn_fwd(q, k, v, o2, lse, B, S, S, H, H, D, False, p_drop=0.1, seed=7)
+    assert not torch.equal(o1, o2)
+    rel = (o2.float().mean() / o1.float().mean()).item()
+    assert abs(rel - 1.0) < 0.2
+
+
+def test_adamw():
+    torch.manual_seed(0)
+    n = 10007
+    p, g = torch.randn(n), torch.randn(n)
+    m, v = torch.zeros(n), torch.zeros(n)
+    ref = [t.clone() for t in (p, g, m, v)]
+    w16 = torch.empty(n, dtype=torch.bfloat16)
+    ops.adamw_(*ref, w16, 5000, 1e-3, 0.9, 0.95, 1e-8, 0.1, 1)
+    gp = [t.clone().to(DEV) for t in (p, g, m, v)]
+    gw = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    ops.adamw_(*gp, gw, 5000, 1e-3, 0.9, 0.95, 1e-8, 0.1, 1)
+    for a, b in zip(gp, ref):
+        close(a, b, atol=1e-5, rtol=1e-5)
+    close(gw, w16, atol=1e-2, rtol=1e-2)
+    ss = torch.zeros(1, device=DEV)
+    ops.sumsq(g.to(DEV), ss)
+    assert abs(ss.item() - (g.double() ** 2).sum().item()) / ss.item() < 1e-4

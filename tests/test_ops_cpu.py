@@ -1,0 +1,140 @@
+"""CPU reference ops (the numerics oracle for the HIP kernels) vs torch.nn.functional /
+autograd, including the explicit backward formulas."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+import mipipe  # noqa: F401
+from mipipe import ops
+
+
+def f32(*s):
+    return torch.randn(*s)
+
+
+@pytest.mark.parametrize("kind", ["layernorm", "rmsnorm"])
+def test_norm_matches_autograd(kind):
+    torch.manual_seed(0)
+    T, D = 16, 64
+    x, br, w, b = f32(T, D), f32(T, D), f32(D), f32(D)
+    dy, dres = f32(T, D), f32(T, D)
+    xa, bra, wa, ba = [t.clone().requires_grad_() for t in (x, br, w, b)]
+    s = xa + bra
+    if kind == "layernorm":
+        y = F.layer_norm(s, (D,), wa, ba, 1e-5)
+    else:
+        y = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + 1e-5) * wa
+    (y * dy).sum().backward()
+    yo, so, mean, rstd = ops.norm_fwd(x, w, b if kind == "layernorm" else None, br, kind=kind)
+    torch.testing.assert_close(yo, y.detach(), atol=1e-5, rtol=1e-5)
+    dw, db = torch.zeros(D), torch.zeros(D)
+    ds, _ = ops.norm_bwd(dy, so, w, mean, rstd, kind=kind, dres=None, dw=dw,
+                         dbias=db if kind == "layernorm" else None)
+    torch.testing.assert_close(ds, xa.grad, atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dw, wa.grad, atol=1e-4, rtol=1e-4)
+    if kind == "layernorm":
+        torch.testing.assert_close(db, ba.grad, atol=1e-4, rtol=1e-4)
+    ds2, _ = ops.norm_bwd(dy, so, w, mean, rstd, kind=kind, dres=dres, dw=torch.zeros(D))
+    torch.testing.assert_close(ds2, xa.grad + dres, atol=1e-4, rtol=1e-4)
+
+
+def test_xent_matches_torch():
+    torch.manual_seed(0)
+    T, V, Vp = 12, 50, 64
+    lg = f32(T, Vp)
+    tg = torch.randint(0, V, (T,))
+    la = lg[:, :V].clone().requires_grad_()
+    ref = F.cross_entropy(la, tg)
+    ref.backward()
+    g = lg.clone()
+    loss = ops.xent_fwd_bwd(g, tg, V, 1.0 / T)
+    torch.testing.assert_close(loss.mean(), ref.detach(), atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(g[:, :V], la.grad, atol=1e-6, rtol=1e-5)
+    assert torch.all(g[:, V:] == 0)
+
+
+@pytest.mark.parametrize("causal,Hkv", [(True, 4), (False, 4), (True, 2)])
+def test_attention_matches_sdpa(causal, Hkv):
+    torch.manual_seed(0)
+    B, S, H, D = 2, 16, 4, 8
+    T = B * S
+    qkv = f32(T, (H + 2 * Hkv) * D)
+    q, k, v = qkv[:, :H * D], qkv[:, H * D:(H + Hkv) * D], qkv[:, (H + Hkv) * D:]
+    o = torch.empty(T, H * D)
+    lse = torch.empty(B * H * S)
+    ops.attn_fwd(q, k, v, o, lse, B, S, S, H, Hkv, D, causal)
+    Q = q.reshape(B, S, H, D).transpose(1, 2).clone().requires_grad_()
+    K = k.reshape(B, S, Hkv, D).transpose(1, 2).clone().requires_grad_()
+    V = v.reshape(B, S, Hkv, D).transpose(1, 2).clone().requires_grad_()
+    rep = H // Hkv
+    ref = F.scaled_dot_product_attention(Q, K.repeat_interleave(rep, 1), V.repeat_interleave(rep, 1),
+                                         is_causal=causal)
+    torch.testing.assert_close(o, ref.transpose(1, 2).reshape(T, H * D).detach(), atol=1e-5, rtol=1e-5)
+    do = f32(T, H * D)
+    ref.backward(do.reshape(B, S, H, D).transpose(1, 2))
+    dq, dk, dv = torch.empty(T, H * D), torch.empty(T, Hkv * D), torch.empty(T, Hkv * D)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, S, H, Hkv, D, causal)
+    torch.testing.assert_close(dq, Q.grad.transpose(1, 2).reshape(T, -1), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dk, K.grad.transpose(1, 2).reshape(T, -1), atol=1e-4, rtol=1e-4)
+    torch.testing.assert_close(dv, V.grad.transpose(1, 2).reshape(T, -1), atol=1e-4, rtol=1e-4)
+
+
+def test_linear_family_matches_autograd():
+    torch.manual_seed(0)
+    T, K, N = 10, 16, 24
+    x, w, b, r = f32(T, K), f32(N, K), f32(N), f32(T, N)
+    xa, wa, ba = [t.clone().requires_grad_() for t in (x, w, b)]
+    pre = xa @ wa.t() + ba
+    y = F.gelu(pre, approximate="tanh")
+    dy = f32(T, N)
+    (y * dy).sum().backward()
+    yo, aux = ops.linear(x, w, b, act="gelu_tanh")
+    torch.testing.assert_close(yo, y.detach(), atol=1e-5, rtol=1e-5)
+    da = ops.act_bwd(dy, aux, "gelu_tanh", dbias=(db := torch.zeros(N)))
+    torch.testing.assert_close(db, ba.grad, atol=1e-4, rtol=1e-4)
+    dw = ops.linear_dw(da, x, torch.zeros(N, K))
+    torch.testing.assert_close(dw, wa.grad, atol=1e-4, rtol=1e-4)
+    dx = ops.linear_dx(da, w)
+    torch.testing.assert_close(dx, xa.grad, atol=1e-4, rtol=1e-4)
+    # fused dgelu in the dX GEMM of the *next* layer == act_bwd after plain dX
+    w2 = f32(5, N)
+    dz = f32(T, 5)
+    fused = ops.linear_dx(dz, w2, act_input=aux, act="gelu_tanh")
+    unf = ops.act_bwd(ops.linear_dx(dz, w2), aux, "gelu_tanh")
+    torch.testing.assert_close(fused, unf, atol=1e-5, rtol=1e-5)
+    yr, _ = ops.linear(x, w, b, residual=r)
+    torch.testing.assert_close(yr, x @ w.t() + b + r, atol=1e-5, rtol=1e-5)
+
+
+def test_swiglu_rope_embedding_adamw():
+    torch.manual_seed(0)
+    T, Fd = 6, 8
+    gu = f32(T, 2 * Fd).requires_grad_()
+    y = F.silu(gu[:, :Fd]) * gu[:, Fd:]
+    dy = f32(T, Fd)
+    (y * dy).sum().backward()
+    torch.testing.assert_close(ops.swiglu_fwd(gu.detach()), y.detach())
+    torch.testing.assert_close(ops.swiglu_bwd(gu.detach(), dy), gu.grad, atol=1e-5, rtol=1e-5)
+    S, H, Hkv, Dh = 5, 2, 1, 8
+    qkv = f32(S, (H + 2 * Hkv) * Dh)
+    cs, sn = ops.rope_tables(S, Dh, 10000.0, "cpu")
+    r = ops.rope_(qkv.clone(), cs, sn, S, H, Hkv, Dh)
+    back = ops.rope_(r.clone(), cs, sn, S, H, Hkv, Dh, inverse=True)
+    torch.testing.assert_close(back, qkv, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(r[:, (H + Hkv) * Dh:], qkv[:, (H + Hkv) * Dh:])  # v untouched
+    # embedding
+    wte, wpe = f32(20, 8), f32(4, 8)
+    idx = torch.randint(0, 20, (8,))
+    e = ops.embed_fwd(idx, wte, wpe, 4)
+    torch.testing.assert_close(e, wte[idx] + wpe[torch.arange(8) % 4])
+    # adamw vs torch.optim.AdamW
+    p = torch.nn.Parameter(f32(50))
+    p.grad = f32(50)
+    opt = torch.optim.AdamW([p], lr=1e-2, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1)
+    pf, gf = p.detach().clone(), p.grad.clone()
+    opt.step()
+    m, v = torch.zeros(50), torch.zeros(50)
+    ops.adamw_(pf, gf, m, v, None, 50, 1e-2, 0.9, 0.95, 1e-8, 0.1, 1)
+    torch.testing.assert_close(pf, p.detach(), atol=1e-6, rtol=1e-6)
