@@ -102,8 +102,9 @@ def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_siz
         for i in range(spw):
             stage_idx = rank + world_size * i
             if engine == "native":
-                from ..models.native import build_reference_stage
-                stages.append(build_reference_stage(args, stage_idx, num_stages, dev))
+                from ..models.stage import build_reference_stage
+                stages.append(build_reference_stage(args, stage_idx, num_stages, dev,
+                                                    mbs=batch_size // num_microbatches, seq_len=seq_length))
             else:
                 model = Transformer(args)
                 stages.append(manual_model_split(model, stage_idx, num_stages, dev))

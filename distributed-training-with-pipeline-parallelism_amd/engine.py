@@ -1,0 +1,148 @@
+"""High-level training engine: native model + pipeline schedule + DP + fused optimizer.
+
+    trainer = PipelineTrainer(NativeConfig.gpt2("small"), pp=4, schedule="1F1B",
+                              n_microbatches=8, mbs=8, seq_len=1024)
+    loss = trainer.train_step(tokens, targets)   # tokens on pp-rank 0, targets on the last
+
+One process per GPU (``torchrun``), RCCL over xGMI between pipeline ranks and between
+DP replicas.  A training step = the lowered pipeline program (fwd/bwd of all
+microbatches, p2p, per-stage DP all-reduce at REDUCE_GRAD) + tied-embedding sync +
+global grad-norm clip + one fused AdamW launch per stage arena.
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import ops
+from .models.config import NativeConfig
+from .models.native import NativeModel, ParamArena, balanced_layer_ranges
+from .models.stage import NativeStage
+from .parallel.comm import P2P
+from .parallel.mesh import Mesh, build_mesh
+from .parallel.runtime import PipelineRuntime
+from .parallel.schedules import SCHEDULES, canonical_name, rank_stages
+
+
+class FlatAdamW:
+    """AdamW over flat stage arenas (one fused kernel launch per arena).
+
+    Global grad-norm clipping sums the per-arena squared norms on device and, with PP,
+    across the pipeline group (a 4-byte all-reduce) -- no host synchronisation."""
+
+    def __init__(self, arenas: List[ParamArena], lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
+                 weight_decay: float = 0.1, max_grad_norm: float = 1.0, pp_group=None):
+        self.arenas = arenas
+        self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
+        self.max_norm = max_grad_norm
+        self.pp_group = pp_group
+        self.step_count = 0
+        self.m = [torch.zeros_like(a.master) for a in arenas]
+        self.v = [torch.zeros_like(a.master) for a in arenas]
+        dev = arenas[0].device if arenas else torch.device("cpu")
+        self.sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+
+    def step(self, lr: Optional[float] = None) -> None:
+        self.step_count += 1
+        lr = self.lr if lr is None else lr
+        use_clip = self.max_norm and self.max_norm > 0
+        if use_clip:
+            self.sumsq.zero_()
+            for a in self.arenas:
+                ops.sumsq(a.grad, self.sumsq)
+            if self.pp_group is not None and dist.get_world_size(self.pp_group) > 1:
+                dist.all_reduce(self.sumsq, group=self.pp_group)
+        for a, m, v in zip(self.arenas, self.m, self.v):
+            ops.adamw_(a.master, a.grad, m, v, a.w16, a.n_decay, lr, self.betas[0], self.betas[1], self.eps, self.wd,
+                       self.step_count, self.sumsq if use_clip else None, self.max_norm if use_clip else 0.0, 1.0,
+                       zero_grad=True)
+
+    def state_dict(self):
+        return {"step": self.step_count, "m": [t.clone() for t in self.m], "v": [t.clone() for t in self.v]}
+
+    def load_state_dict(self, sd):
+        self.step_count = sd["step"]
+        for dst, src in zip(self.m, sd["m"]):
+            dst.copy_(src)
+        for dst, src in zip(self.v, sd["v"]):
+            dst.copy_(src)
+
+
+class PipelineTrainer:
+    def __init__(self, cfg: NativeConfig, pp: int = 1, dp: int = 1, schedule: str = "1F1B",
+                 n_microbatches: int = 8, mbs: int = 8, seq_len: int = 1024, v: Optional[int] = None,
+                 device=None, lr: float = 3e-4, weight_decay: float = 0.1, max_grad_norm: float = 1.0,
+                 recompute: bool = False, profile: bool = False, seed: int = 0, style: str = "loop",
+                 mesh: Optional[Mesh] = None, layer_ranges=None, dtype=torch.bfloat16):
+        self.cfg = cfg
+        self.schedule = canonical_name(schedule)
+        if v is None:
+            v = SCHEDULES[self.schedule][1]
+        if not SCHEDULES[self.schedule][2]:
+            v = 1
+        self.v = v
+        self.m, self.mbs, self.S = n_microbatches, mbs, seq_len
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else \
+                torch.device("cpu")
+        self.device = torch.device(device)
+        self.mesh = mesh if mesh is not None else build_mesh(pp, dp, self.device)
+        num_stages = pp * v
+        if layer_ranges is None:
+            layer_ranges = balanced_layer_ranges(cfg, num_stages, seq_len)
+        self.layer_ranges = layer_ranges
+        my_stages = rank_stages(self.mesh.pp_rank, pp, v, style)
+        tied_pp = cfg.tie_embeddings and num_stages > 1
+        self.stages: List[NativeStage] = []
+        for s in my_stages:
+            model = NativeModel(cfg, s, num_stages, self.device, layer_range=layer_ranges[s], seed=seed,
+                                recompute=recompute, mbs=mbs, seq_len=seq_len, dtype=dtype)
+            egroup = self.mesh.embed_group if (tied_pp and (s == 0 or s == num_stages - 1)) else None
+            self.stages.append(NativeStage(model, mbs, seq_len, dp_group=self.mesh.dp_group, embed_group=egroup,
+                                           seed=seed + 1000 * self.mesh.dp_rank))
+        p2p = P2P(self.mesh.pp_group, self.mesh.pipe_ranks, self.device)
+        self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
+                                       scale_grads=True, style=style, profile=profile)
+        self.optimizer = FlatAdamW([st.arena for st in self.stages], lr=lr, weight_decay=weight_decay,
+                                   max_grad_norm=max_grad_norm, pp_group=self.mesh.pp_group if pp > 1 else None)
+        self.last_losses: List[torch.Tensor] = []
+
+    @property
+    def is_first(self) -> bool:
+        return any(st.is_first for st in self.stages)
+
+    @property
+    def is_last(self) -> bool:
+        return any(st.is_last for st in self.stages)
+
+    def num_params_local(self) -> int:
+        return sum(st.arena.numel for st in self.stages)
+
+    def train_step(self, tokens: Optional[torch.Tensor] = None, targets: Optional[torch.Tensor] = None,
+                   lr: Optional[float] = None) -> Optional[torch.Tensor]:
+        """tokens/targets: [m*mbs, S] int64 (tokens needed on the first stage's rank,
+        targets on the last).  Returns the mean loss tensor on the last-stage rank."""
+        inputs = None
+        if self.is_first:
+            inputs = [(c,) for c in torch.tensor_split(tokens, self.m, dim=0)]
+        tg = list(torch.tensor_split(targets, self.m, dim=0)) if self.is_last else None
+        losses: List[torch.Tensor] = []
+        self.runtime.step(inputs, tg, losses, return_outputs=False)
+        self.optimizer.step(lr)
+        self.last_losses = losses
+        if losses:
+            return torch.stack(losses).mean()
+        return None
+
+    def bubble(self) -> float:
+        return self.runtime.bubble()
+
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self):
+        sd = {}
+        for st in self.stages:
+            sd.update(st.arena.state_dict())
+        return sd

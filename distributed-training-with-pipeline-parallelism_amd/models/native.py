@@ -1,0 +1,607 @@
+"""Native transformer stages: explicit per-layer forward/backward on the HIP kernels.
+
+Why explicit instead of autograd:
+* every tensor a backward needs is stashed in a per-microbatch slot that the pipeline
+  schedule bounds (GPipe: m slots, 1F1B: <= P - s), and nothing else is kept alive;
+* the fused epilogues (bias+GELU with saved pre-activation, residual adds, GELU' in the
+  dX GEMM, f32 dW accumulation into the flat grad arena) cross what would be separate
+  autograd nodes;
+* the backward splits into an input-grad part (I) and a weight-grad part (W) for
+  zero-bubble schedules, and supports full activation recompute (Llama-3 8B config).
+
+Parameters of a stage live in one :class:`ParamArena` (flat f32 master + flat bf16 working
+copy + flat f32 grad).  Names are global FQNs (``layers.7.attn.wqkv.weight``;
+the reference architecture uses the reference's own nn.TransformerDecoderLayer names),
+so checkpoints are per-stage shards that re-split to any PP degree.
+"""
+from __future__ import annotations
+
+import hashlib
+import math
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import ops
+from .config import NativeConfig
+
+# ======================================================================================
+# parameter arena
+# ======================================================================================
+
+
+@dataclass
+class ParamSpec:
+    name: str
+    shape: Tuple[int, ...]
+    init: str          # normal | zeros | ones | normal_scaled
+    decay: bool
+    std: float = 0.02
+
+
+def _name_seed(seed: int, name: str) -> int:
+    h = hashlib.blake2b(f"{seed}:{name}".encode(), digest_size=8).digest()
+    return int.from_bytes(h, "little") & 0x7FFFFFFFFFFFFFFF
+
+
+class ParamArena:
+    """Flat storage for one stage's parameters: f32 master, bf16 copy, f32 grads.
+
+    Decayed tensors come first so weight decay is a prefix ``[0, n_decay)`` of the
+    flat buffer (one AdamW launch for the whole stage)."""
+
+    def __init__(self, specs: Sequence[ParamSpec], device, dtype=torch.bfloat16, seed: int = 0,
+                 init: bool = True):
+        specs = sorted(specs, key=lambda s: (not s.decay,))
+        self.specs = {s.name: s for s in specs}
+        self.order = [s.name for s in specs]
+        self.offsets: Dict[str, int] = {}
+        off = 0
+        for s in specs:
+            n = int(math.prod(s.shape))
+            # keep every tensor 16-byte aligned in the bf16 copy (8 elements)
+            off = (off + 7) // 8 * 8
+            self.offsets[s.name] = off
+            off += n
+        self.numel = (off + 7) // 8 * 8
+        self.n_decay = 0
+        for s in specs:
+            if s.decay:
+                self.n_decay = self.offsets[s.name] + int(math.prod(s.shape))
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        self.w16 = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        if init:
+            self.init_params(seed)
+
+    def init_params(self, seed: int = 0) -> None:
+        for name in self.order:
+            s = self.specs[name]
+            v = self.master_view(name)
+            if s.init == "zeros":
+                v.zero_()
+            elif s.init == "ones":
+                v.fill_(1.0)
+            else:
+                gdev = "cuda" if self.device.type == "cuda" else "cpu"
+                g = torch.Generator(device=gdev).manual_seed(_name_seed(seed, name))
+                v.copy_(torch.randn(s.shape, generator=g, device=gdev, dtype=torch.float32) * s.std)
+        self.sync_w16()
+
+    def sync_w16(self) -> None:
+        ops.cast_f32_bf16(self.master, self.w16)
+
+    def _view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
+        s = self.specs[name]
+        o = self.offsets[name]
+        return buf[o: o + int(math.prod(s.shape))].view(s.shape)
+
+    def w(self, name: str) -> torch.Tensor:
+        return self._view(self.w16, name)
+
+    def g(self, name: str) -> torch.Tensor:
+        return self._view(self.grad, name)
+
+    def master_view(self, name: str) -> torch.Tensor:
+        return self._view(self.master, name)
+
+    def has(self, name: str) -> bool:
+        return name in self.specs
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        return {n: self.master_view(n).detach().clone() for n in self.order}
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
+        missing = [n for n in self.order if n not in sd]
+        if strict and missing:
+            raise KeyError(f"missing keys: {missing[:5]}...")
+        for n in self.order:
+            if n in sd:
+                self.master_view(n).copy_(sd[n].to(self.device, torch.float32).reshape(self.specs[n].shape))
+        self.sync_w16()
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+
+# ======================================================================================
+# per-microbatch context
+# ======================================================================================
+
+
+class MBContext:
+    """Activation stash of one microbatch on one stage (a dict per layer)."""
+
+    def __init__(self, mb: int, seed: int):
+        self.mb = mb
+        self.seed = seed
+        self.layers: Dict[int, dict] = {}
+        self.misc: dict = {}
+
+
+def _seed(base: int, *parts: int) -> int:
+    x = base & 0xFFFFFFFFFFFF
+    for p in parts:
+        x = (x * 0x100000001B3 + (p + 0x9E37)) & 0x7FFFFFFFFFFFFFFF
+    return x
+
+
+# ======================================================================================
+# blocks
+# ======================================================================================
+
+
+def block_param_specs(cfg: NativeConfig, i: int) -> List[ParamSpec]:
+    d, f = cfg.d_model, cfg.d_ff
+    std, rstd = cfg.init_std, cfg.init_std / math.sqrt(2 * cfg.n_layers)
+    nb = "ones"
+    out: List[ParamSpec] = []
+    P = f"layers.{i}."
+    if cfg.cross_attn:  # reference nn.TransformerDecoderLayer names
+        for att in ("self_attn", "multihead_attn"):
+            out += [ParamSpec(P + f"{att}.in_proj_weight", (3 * d, d), "normal", True, std),
+                    ParamSpec(P + f"{att}.in_proj_bias", (3 * d,), "zeros", False),
+                    ParamSpec(P + f"{att}.out_proj.weight", (d, d), "normal", True, std),
+                    ParamSpec(P + f"{att}.out_proj.bias", (d,), "zeros", False)]
+        out += [ParamSpec(P + "linear1.weight", (f, d), "normal", True, std),
+                ParamSpec(P + "linear1.bias", (f,), "zeros", False),
+                ParamSpec(P + "linear2.weight", (d, f), "normal", True, std),
+                ParamSpec(P + "linear2.bias", (d,), "zeros", False)]
+        for k in (1, 2, 3):
+            out += [ParamSpec(P + f"norm{k}.weight", (d,), nb, False), ParamSpec(P + f"norm{k}.bias", (d,), "zeros", False)]
+        return out
+    out += [ParamSpec(P + "attn_norm.weight", (d,), nb, False)]
+    if cfg.norm == "layernorm":
+        out += [ParamSpec(P + "attn_norm.bias", (d,), "zeros", False)]
+    out += [ParamSpec(P + "attn.wqkv.weight", (cfg.qkv_dim, d), "normal", True, std),
+            ParamSpec(P + "attn.wo.weight", (d, d), "normal", True, rstd)]
+    if cfg.bias:
+        out += [ParamSpec(P + "attn.wqkv.bias", (cfg.qkv_dim,), "zeros", False),
+                ParamSpec(P + "attn.wo.bias", (d,), "zeros", False)]
+    out += [ParamSpec(P + "ffn_norm.weight", (d,), nb, False)]
+    if cfg.norm == "layernorm":
+        out += [ParamSpec(P + "ffn_norm.bias", (d,), "zeros", False)]
+    if cfg.activation == "swiglu":
+        out += [ParamSpec(P + "ffn.w13.weight", (2 * f, d), "normal", True, std),
+                ParamSpec(P + "ffn.w2.weight", (d, f), "normal", True, rstd)]
+    else:
+        out += [ParamSpec(P + "ffn.w1.weight", (f, d), "normal", True, std),
+                ParamSpec(P + "ffn.w2.weight", (d, f), "normal", True, rstd)]
+        if cfg.bias:
+            out += [ParamSpec(P + "ffn.w1.bias", (f,), "zeros", False),
+                    ParamSpec(P + "ffn.w2.bias", (d,), "zeros", False)]
+    return out
+
+
+class Block:
+    """One transformer layer with explicit forward / backward (pre-norm GPT-2/Llama or
+    the reference post-norm self+cross-attention block)."""
+
+    def __init__(self, cfg: NativeConfig, idx: int, arena: ParamArena, rope=None):
+        self.cfg = cfg
+        self.i = idx
+        self.A = arena
+        self.P = f"layers.{idx}."
+        self.rope = rope  # (cos, sin) tables
+
+    def w(self, n):
+        return self.A.w(self.P + n)
+
+    def g(self, n):
+        return self.A.g(self.P + n)
+
+    def wb(self, n):
+        return self.A.w(self.P + n) if self.A.has(self.P + n) else None
+
+    def gb(self, n):
+        return self.A.g(self.P + n) if self.A.has(self.P + n) else None
+
+    # ------------------------------------------------------------------ pre-norm
+    def _attn_fwd(self, h, B, S, st, seed):
+        cfg = self.cfg
+        H, KV, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+        qkv, _ = ops.linear(h, self.w("attn.wqkv.weight"), self.wb("attn.wqkv.bias"))
+        if cfg.pos == "rope":
+            ops.rope_(qkv, self.rope[0], self.rope[1], S, H, KV, Dh)
+        q, k, v = qkv[:, : H * Dh], qkv[:, H * Dh:(H + KV) * Dh], qkv[:, (H + KV) * Dh:]
+        o = torch.empty(h.shape[0], H * Dh, device=h.device, dtype=h.dtype)
+        lse = torch.empty(B * H * S, device=h.device, dtype=torch.float32)
+        ops.attn_fwd(q, k, v, o, lse, B, S, S, H, KV, Dh, cfg.causal, p_drop=cfg.dropout, seed=seed)
+        st["qkv"], st["o"], st["lse"] = qkv, o, lse
+        return o
+
+    def forward(self, x: torch.Tensor, B: int, S: int, ctx: MBContext, recompute: bool = False):
+        cfg = self.cfg
+        st: dict = {}
+        sd = _seed(ctx.seed, self.i)
+        if cfg.cross_attn:
+            y = self._ref_forward(x, B, S, st, sd)
+        else:
+            kind = cfg.norm
+            h1, _, mu1, rs1 = ops.norm_fwd(x, self.w("attn_norm.weight"), self.wb("attn_norm.bias"), kind=kind,
+                                           eps=cfg.norm_eps)
+            o = self._attn_fwd(h1, B, S, st, _seed(sd, 1))
+            x2, _ = ops.linear(o, self.w("attn.wo.weight"), self.wb("attn.wo.bias"), residual=x)
+            h2, _, mu2, rs2 = ops.norm_fwd(x2, self.w("ffn_norm.weight"), self.wb("ffn_norm.bias"), kind=kind,
+                                           eps=cfg.norm_eps)
+            if cfg.activation == "swiglu":
+                gu, _ = ops.linear(h2, self.w("ffn.w13.weight"))
+                gact = ops.swiglu_fwd(gu)
+                y, _ = ops.linear(gact, self.w("ffn.w2.weight"), residual=x2)
+                st.update(gu=gu, g=gact)
+            else:
+                gact, a = ops.linear(h2, self.w("ffn.w1.weight"), self.wb("ffn.w1.bias"), act=cfg.activation)
+                y, _ = ops.linear(gact, self.w("ffn.w2.weight"), self.wb("ffn.w2.bias"), residual=x2)
+                st.update(a=a, g=gact)
+            st.update(x=x, h1=h1, mu1=mu1, rs1=rs1, x2=x2, h2=h2, mu2=mu2, rs2=rs2)
+        if recompute:
+            st = {"x": x}  # full recompute: keep only the layer input
+        ctx.layers[self.i] = st
+        return y
+
+    def _ensure(self, B, S, ctx):
+        st = ctx.layers[self.i]
+        if len(st) == 1 and "x" in st:  # recompute the stash
+            tmp = MBContext(ctx.mb, ctx.seed)
+            self.forward(st["x"], B, S, tmp, recompute=False)
+            ctx.layers[self.i] = tmp.layers[self.i]
+        return ctx.layers[self.i]
+
+    def backward(self, dy: torch.Tensor, B: int, S: int, ctx: MBContext, weight_grads: bool = True,
+                 defer: Optional[list] = None):
+        """Returns dx.  If ``weight_grads`` is False the dW GEMMs are appended to ``defer``
+        (zero-bubble split: I now, W later)."""
+        st = self._ensure(B, S, ctx)
+        cfg = self.cfg
+        sd = _seed(ctx.seed, self.i)
+        wjobs: List[Callable[[], None]] = []
+        if cfg.cross_attn:
+            dx = self._ref_backward(dy, B, S, st, sd, wjobs)
+        else:
+            kind = cfg.norm
+            H, KV, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
+            # ---------------- FFN
+            if cfg.activation == "swiglu":
+                dgact = ops.linear_dx(dy, self.w("ffn.w2.weight"))
+                gact, h2, gu = st["g"], st["h2"], st["gu"]
+                wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
+                dgu = ops.swiglu_bwd(gu, dgact)
+                wjobs.append(lambda dgu=dgu, h2=h2: ops.linear_dw(dgu, h2, self.g("ffn.w13.weight")))
+                dh2 = ops.linear_dx(dgu, self.w("ffn.w13.weight"))
+            else:
+                gact, a, h2 = st["g"], st["a"], st["h2"]
+                da = ops.linear_dx(dy, self.w("ffn.w2.weight"), act_input=a, act=cfg.activation)
+                wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
+                if cfg.bias:
+                    wjobs.append(lambda dy=dy: ops.colsum(dy, self.g("ffn.w2.bias")))
+                    wjobs.append(lambda da=da: ops.colsum(da, self.g("ffn.w1.bias")))
+                wjobs.append(lambda da=da, h2=h2: ops.linear_dw(da, h2, self.g("ffn.w1.weight")))
+                dh2 = ops.linear_dx(da, self.w("ffn.w1.weight"))
+            dx2, _ = ops.norm_bwd(dh2, st["x2"], self.w("ffn_norm.weight"), st["mu2"], st["rs2"], kind=kind,
+                                  dres=dy, dw=self.g("ffn_norm.weight"), dbias=self.gb("ffn_norm.bias"))
+            # ---------------- attention
+            o = st["o"]
+            do = ops.linear_dx(dx2, self.w("attn.wo.weight"))
+            wjobs.append(lambda dx2=dx2, o=o: ops.linear_dw(dx2, o, self.g("attn.wo.weight")))
+            if cfg.bias:
+                wjobs.append(lambda dx2=dx2: ops.colsum(dx2, self.g("attn.wo.bias")))
+            qkv = st["qkv"]
+            q, k, v = qkv[:, : H * Dh], qkv[:, H * Dh:(H + KV) * Dh], qkv[:, (H + KV) * Dh:]
+            dqkv = torch.empty_like(qkv)
+            dq, dk, dv = dqkv[:, : H * Dh], dqkv[:, H * Dh:(H + KV) * Dh], dqkv[:, (H + KV) * Dh:]
+            ops.attn_bwd(q, k, v, o, do, st["lse"], dq, dk, dv, B, S, S, H, KV, Dh, cfg.causal,
+                         p_drop=cfg.dropout, seed=_seed(sd, 1))
+            if cfg.pos == "rope":
+                ops.rope_(dqkv, self.rope[0], self.rope[1], S, H, KV, Dh, inverse=True)
+            h1 = st["h1"]
+            wjobs.append(lambda dqkv=dqkv, h1=h1: ops.linear_dw(dqkv, h1, self.g("attn.wqkv.weight")))
+            if cfg.bias:
+                wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, self.g("attn.wqkv.bias")))
+            dh1 = ops.linear_dx(dqkv, self.w("attn.wqkv.weight"))
+            dx, _ = ops.norm_bwd(dh1, st["x"], self.w("attn_norm.weight"), st["mu1"], st["rs1"], kind=kind,
+                                 dres=dx2, dw=self.g("attn_norm.weight"), dbias=self.gb("attn_norm.bias"))
+        if weight_grads:
+            for j in wjobs:
+                j()
+        else:
+            defer.extend(wjobs)
+        del ctx.layers[self.i]
+        return dx
+
+    # ------------------------------------------------------------------ reference post-norm block
+    def _mha(self, prefix, xq, xkv, B, S, seed, st, key, self_attn: bool):
+        cfg = self.cfg
+        H, Dh, d = cfg.n_heads, cfg.head_dim, cfg.d_model
+        W, b = self.w(prefix + ".in_proj_weight"), self.w(prefix + ".in_proj_bias")
+        if self_attn:
+            qkv, _ = ops.linear(xq, W, b)
+            q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+            st[key + "qkv"] = qkv
+        else:
+            q, _ = ops.linear(xq, W[:d], b[:d])
+            kv, _ = ops.linear(xkv, W[d:], b[d:])
+            k, v = kv[:, :d], kv[:, d:]
+            st[key + "q"], st[key + "kv"] = q, kv
+        o = torch.empty(xq.shape[0], d, device=xq.device, dtype=xq.dtype)
+        lse = torch.empty(B * H * S, device=xq.device, dtype=torch.float32)
+        ops.attn_fwd(q, k, v, o, lse, B, S, S, H, H, Dh, False, p_drop=cfg.dropout, seed=seed)
+        st[key + "o"], st[key + "lse"] = o, lse
+        out, _ = ops.linear(o, self.w(prefix + ".out_proj.weight"), self.w(prefix + ".out_proj.bias"))
+        return out
+
+    def _ref_forward(self, h, B, S, st, sd):
+        cfg = self.cfg
+        p = cfg.dropout
+        sa = self._mha("self_attn", h, h, B, S, _seed(sd, 1), st, "sa_", True)
+        x1, s1, mu1, rs1 = ops.norm_fwd(h, self.w("norm1.weight"), self.w("norm1.bias"), branch=sa, eps=cfg.norm_eps,
+                                        p_drop=p, seed=_seed(sd, 2))
+        ca = self._mha("multihead_attn", x1, h, B, S, _seed(sd, 3), st, "ca_", False)
+        x2, s2, mu2, rs2 = ops.norm_fwd(x1, self.w("norm2.weight"), self.w("norm2.bias"), branch=ca,
+                                        eps=cfg.norm_eps, p_drop=p, seed=_seed(sd, 4))
+        a, _ = ops.linear(x2, self.w("linear1.weight"), self.w("linear1.bias"))
+        gact = ops.act_fwd(a, "relu", p_drop=p, seed=_seed(sd, 5))
+        f, _ = ops.linear(gact, self.w("linear2.weight"), self.w("linear2.bias"))
+        y, s3, mu3, rs3 = ops.norm_fwd(x2, self.w("norm3.weight"), self.w("norm3.bias"), branch=f, eps=cfg.norm_eps,
+                                       p_drop=p, seed=_seed(sd, 6))
+        st.update(x=h, x1=x1, s1=s1, mu1=mu1, rs1=rs1, x2=x2, s2=s2, mu2=mu2, rs2=rs2, a=a, g=gact, s3=s3, mu3=mu3,
+                  rs3=rs3)
+        return y
+
+    def _mha_bwd(self, prefix, dout, xq, xkv, B, S, seed, st, key, self_attn, wjobs, dres_q, dres_kv):
+        """Returns (dxq, dxkv) with the residual grads folded in."""
+        cfg = self.cfg
+        H, Dh, d = cfg.n_heads, cfg.head_dim, cfg.d_model
+        W = self.w(prefix + ".in_proj_weight")
+        gW, gb = self.g(prefix + ".in_proj_weight"), self.g(prefix + ".in_proj_bias")
+        o = st[key + "o"]
+        wjobs.append(lambda dout=dout, o=o: ops.linear_dw(dout, o, self.g(prefix + ".out_proj.weight")))
+        wjobs.append(lambda dout=dout: ops.colsum(dout, self.g(prefix + ".out_proj.bias")))
+        do = ops.linear_dx(dout, self.w(prefix + ".out_proj.weight"))
+        if self_attn:
+            qkv = st[key + "qkv"]
+            q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
+            dqkv = torch.empty_like(qkv)
+            dq, dk, dv = dqkv[:, :d], dqkv[:, d:2 * d], dqkv[:, 2 * d:]
+        else:
+            q, kv = st[key + "q"], st[key + "kv"]
+            k, v = kv[:, :d], kv[:, d:]
+            dq = torch.empty_like(q)
+            dkv = torch.empty_like(kv)
+            dk, dv = dkv[:, :d], dkv[:, d:]
+        ops.attn_bwd(q, k, v, o, do, st[key + "lse"], dq, dk, dv, B, S, S, H, H, Dh, False, p_drop=cfg.dropout,
+                     seed=seed)
+        if self_attn:
+            wjobs.append(lambda dqkv=dqkv, xq=xq: ops.linear_dw(dqkv, xq, gW))
+            wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, gb))
+            dx = ops.linear_dx(dqkv, W, residual=dres_q)
+            return dx, None
+        wjobs.append(lambda dq=dq, xq=xq: ops.linear_dw(dq, xq, gW[:d]))
+        wjobs.append(lambda dq=dq: ops.colsum(dq, gb[:d]))
+        wjobs.append(lambda dkv=dkv, xkv=xkv: ops.linear_dw(dkv, xkv, gW[d:]))
+        wjobs.append(lambda dkv=dkv: ops.colsum(dkv, gb[d:]))
+        dxq = ops.linear_dx(dq, W[:d], residual=dres_q)
+        dxkv = ops.linear_dx(dkv, W[d:], residual=dres_kv)
+        return dxq, dxkv
+
+    def _ref_backward(self, dy, B, S, st, sd, wjobs):
+        cfg = self.cfg
+        p = cfg.dropout
+        # norm3(x2 + drop(f))
+        ds3, df = ops.norm_bwd(dy, st["s3"], self.w("norm3.weight"), st["mu3"], st["rs3"], dw=self.g("norm3.weight"),
+                               dbias=self.g("norm3.bias"), p_drop=p, seed=_seed(sd, 6), want_branch=True)
+        gact, a, x2 = st["g"], st["a"], st["x2"]
+        wjobs.append(lambda df=df, gact=gact: ops.linear_dw(df, gact, self.g("linear2.weight")))
+        wjobs.append(lambda df=df: ops.colsum(df, self.g("linear2.bias")))
+        dg = ops.linear_dx(df, self.w("linear2.weight"))
+        da = ops.act_bwd(dg, a, "relu", dbias=None, p_drop=p, seed=_seed(sd, 5))
+        wjobs.append(lambda da=da: ops.colsum(da, self.g("linear1.bias")))
+        wjobs.append(lambda da=da, x2=x2: ops.linear_dw(da, x2, self.g("linear1.weight")))
+        dx2 = ops.linear_dx(da, self.w("linear1.weight"), residual=ds3)
+        # norm2(x1 + drop(ca))
+        ds2, dca = ops.norm_bwd(dx2, st["s2"], self.w("norm2.weight"), st["mu2"], st["rs2"], dw=self.g("norm2.weight"),
+                                dbias=self.g("norm2.bias"), p_drop=p, seed=_seed(sd, 4), want_branch=True)
+        h, x1 = st["x"], st["x1"]
+        dx1, dh_mem = self._mha_bwd("multihead_attn", dca, x1, h, B, S, _seed(sd, 3), st, "ca_", False, wjobs,
+                                    dres_q=ds2, dres_kv=None)
+        # norm1(h + drop(sa))
+        ds1, dsa = ops.norm_bwd(dx1, st["s1"], self.w("norm1.weight"), st["mu1"], st["rs1"], dw=self.g("norm1.weight"),
+                                dbias=self.g("norm1.bias"), p_drop=p, seed=_seed(sd, 2), want_branch=True)
+        dres = ds1 + dh_mem
+        dh, _ = self._mha_bwd("self_attn", dsa, h, h, B, S, _seed(sd, 1), st, "sa_", True, wjobs, dres_q=dres,
+                              dres_kv=None)
+        return dh
+
+
+# ======================================================================================
+# stage model
+# ======================================================================================
+
+
+def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 1024,
+                          reference_rule: bool = False) -> List[Tuple[int, int]]:
+    """Layer ranges per stage.
+
+    ``reference_rule``: ``L // num_stages`` per stage, remainder on the last stage
+    (reference helper:70-75).  Otherwise a cost-balanced split: the embedding and the
+    LM head (+ loss) are priced in layer-equivalents from their FLOPs and the layers are
+    distributed so the max stage cost is minimal (the head of a 50k-vocab GPT-2 costs
+    ~4.5 layers; leaving it out of the balance is what makes naive PP=8 splits slow)."""
+    L = cfg.n_layers
+    if reference_rule or num_stages == 1:
+        per = L // num_stages
+        return [(s * per, (s + 1) * per if s < num_stages - 1 else L) for s in range(num_stages)]
+    d = cfg.d_model
+    layer_cost = (cfg.flops_per_token(seq_len) / 3.0 - 2 * d * cfg.vocab_size) / L
+    head_cost = (2 * d * cfg.vocab_padded) / layer_cost + 0.3  # + CE / final norm, in layer units
+    emb_cost = 0.1
+    P = num_stages
+    best = None
+    for k_last in range(0, L + 1):
+        rest = L - k_last
+        base, extra = divmod(rest, P - 1)
+        # give the remainder to the later non-head stages (stage 0 also holds the embedding)
+        counts = [base + (1 if s >= P - 1 - extra else 0) for s in range(P - 1)] + [k_last]
+        costs = [c + (emb_cost if s == 0 else 0.0) + (head_cost if s == P - 1 else 0.0)
+                 for s, c in enumerate(counts)]
+        key = (round(max(costs), 6), -min(counts[:-1]) if P > 1 else 0)
+        if best is None or key < best[0]:
+            best = (key, counts)
+    out, start = [], 0
+    for k in best[1]:
+        out.append((start, start + k))
+        start += k
+    return out
+
+
+class NativeModel:
+    """The part of a model that one pipeline stage owns (embedding on stage 0, head +
+    loss on the last stage), with explicit fwd/bwd per microbatch."""
+
+    def __init__(self, cfg: NativeConfig, stage_index: int, num_stages: int, device, layer_range=None,
+                 seed: int = 0, recompute: bool = False, mbs: int = 1, seq_len: int = 1024, init: bool = True,
+                 dtype=torch.bfloat16):
+        self.cfg = cfg
+        self.stage_index = stage_index
+        self.num_stages = num_stages
+        self.first = stage_index == 0
+        self.last = stage_index == num_stages - 1
+        self.device = torch.device(device)
+        self.recompute = recompute
+        if layer_range is None:
+            layer_range = balanced_layer_ranges(cfg, num_stages, seq_len)[stage_index]
+        self.layer_range = layer_range
+        specs: List[ParamSpec] = []
+        d = cfg.d_model
+        if self.first:
+            specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False, cfg.init_std))
+            if cfg.pos == "learned":
+                specs.append(ParamSpec("pos_embeddings.weight", (cfg.max_seq_len, d), "normal", False, 0.01))
+        for i in range(*layer_range):
+            specs += block_param_specs(cfg, i)
+        if self.last:
+            if cfg.final_norm:
+                specs.append(ParamSpec("norm.weight", (d,), "ones", False))
+                if cfg.norm == "layernorm":
+                    specs.append(ParamSpec("norm.bias", (d,), "zeros", False))
+            if cfg.tie_embeddings:
+                if not self.first:  # tied copy on the last stage, kept in sync by the embed group
+                    specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False,
+                                           cfg.init_std))
+            else:
+                specs.append(ParamSpec("output.weight", (cfg.vocab_padded, d), "normal", True, cfg.init_std))
+                if cfg.bias and cfg.cross_attn:
+                    specs.append(ParamSpec("output.bias", (cfg.vocab_padded,), "zeros", False))
+        self.arena = ParamArena(specs, self.device, dtype=dtype, seed=seed, init=init)
+        rope = None
+        if cfg.pos == "rope":
+            rope = ops.rope_tables(cfg.max_seq_len, cfg.head_dim, cfg.rope_theta, self.device)
+        self.blocks = [Block(cfg, i, self.arena, rope) for i in range(*layer_range)]
+        self.defer_w: Dict[int, list] = {}
+
+    # ------------------------------------------------------------------ helpers
+    def head_weight(self):
+        return self.arena.w("tok_embeddings.weight" if self.cfg.tie_embeddings else "output.weight")
+
+    def head_grad(self):
+        return self.arena.g("tok_embeddings.weight" if self.cfg.tie_embeddings else "output.weight")
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, x: torch.Tensor, ctx: MBContext, B: int, S: int, target: Optional[torch.Tensor] = None,
+                loss_scale: float = 1.0):
+        """x: tokens [B,S] (stage 0) or hidden [B*S, D].  Last stage: returns the mean
+        loss (f32 scalar tensor) and keeps dlogits for the backward."""
+        cfg = self.cfg
+        if self.first:
+            tokens = x.reshape(-1)
+            h = ops.embed_fwd(tokens, self.arena.w("tok_embeddings.weight"),
+                              self.arena.w("pos_embeddings.weight") if cfg.pos == "learned" else None, S)
+            ctx.misc["tokens"] = tokens
+        else:
+            h = x
+        for blk in self.blocks:
+            h = blk.forward(h, B, S, ctx, recompute=self.recompute)
+        if not self.last:
+            return h
+        # final norm + head + fused CE (grad computed now, consumed by the backward)
+        if cfg.final_norm:
+            hn, _, mu, rs = ops.norm_fwd(h, self.arena.w("norm.weight"),
+                                         self.arena.w("norm.bias") if self.arena.has("norm.bias") else None,
+                                         kind=cfg.norm, eps=cfg.norm_eps)
+            ctx.misc.update(hpre=h, mu=mu, rs=rs)
+        else:
+            hn = h
+        hb = self.arena.w("output.bias") if self.arena.has("output.bias") else None
+        logits, _ = ops.linear(hn, self.head_weight(), hb)
+        T = hn.shape[0]
+        if target is None:
+            ctx.misc.update(hn=hn, logits=logits)
+            return logits
+        row_loss = ops.xent_fwd_bwd(logits, target.reshape(-1), cfg.vocab_size, grad_scale=loss_scale / T)
+        ctx.misc.update(hn=hn, dlogits=logits)
+        return row_loss.mean()
+
+    # ------------------------------------------------------------------ backward
+    def backward(self, dy: Optional[torch.Tensor], ctx: MBContext, B: int, S: int, weight_grads: bool = True):
+        cfg = self.cfg
+        defer: List = []
+        if self.last:
+            dl = ctx.misc.pop("dlogits")
+            hn = ctx.misc.pop("hn")
+            W = self.head_weight()
+            dhn = ops.linear_dx(dl, W)
+            jobs = [lambda dl=dl, hn=hn: ops.linear_dw(dl, hn, self.head_grad())]
+            if self.arena.has("output.bias"):
+                jobs.append(lambda dl=dl: ops.colsum(dl, self.arena.g("output.bias")))
+            if weight_grads:
+                for j in jobs:
+                    j()
+            else:
+                defer.extend(jobs)
+            if cfg.final_norm:
+                dy, _ = ops.norm_bwd(dhn, ctx.misc.pop("hpre"), self.arena.w("norm.weight"), ctx.misc.pop("mu"),
+                                     ctx.misc.pop("rs"), kind=cfg.norm, dw=self.arena.g("norm.weight"),
+                                     dbias=self.arena.g("norm.bias") if self.arena.has("norm.bias") else None)
+            else:
+                dy = dhn
+        for blk in reversed(self.blocks):
+            dy = blk.backward(dy, B, S, ctx, weight_grads=weight_grads, defer=defer)
+        if self.first:
+            tokens = ctx.misc.pop("tokens")
+            jobs = [lambda dy=dy, tokens=tokens: ops.embed_bwd(
+                tokens, dy, self.arena.g("tok_embeddings.weight"),
+                self.arena.g("pos_embeddings.weight") if cfg.pos == "learned" else None, S)]
+            if weight_grads:
+                jobs[0]()
+            else:
+                defer.extend(jobs)
+            dy = None
+        if not weight_grads:
+            self.defer_w[ctx.mb] = defer
+        return dy
+
+    def backward_weight(self, mb: int):
+        for j in self.defer_w.pop(mb, []):
+            j()

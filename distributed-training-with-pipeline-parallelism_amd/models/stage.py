@@ -1,0 +1,105 @@
+"""Adapter between :class:`~mipipe.models.native.NativeModel` and the pipeline runtime."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..parallel.dp import allreduce_flat
+from ..parallel.stage import StageBase
+from .config import NativeConfig
+from .native import MBContext, NativeModel, _seed
+
+
+class NativeStage(StageBase):
+    """One virtual pipeline stage of a native model.
+
+    Static shapes (no runtime shape inference): stage 0 receives ``[mbs, S]`` int64
+    tokens, every other stage ``[mbs*S, d_model]`` bf16 activations; the last stage
+    emits the microbatch loss.  Gradients are already scaled by ``1/m`` through the loss
+    scale; ``reduce_grad`` issues the async DP all-reduce on the flat grad arena and
+    ``post_step`` sums tied-embedding grads between the first and last stage.
+    """
+
+    def __init__(self, model: NativeModel, mbs: int, seq_len: int, dp_group=None, embed_group=None,
+                 seed: int = 1234):
+        self.model = model
+        self.cfg: NativeConfig = model.cfg
+        self.stage_index = model.stage_index
+        self.num_stages = model.num_stages
+        self.device = model.device
+        self.mbs, self.S = mbs, seq_len
+        self.dp_group = dp_group
+        self.embed_group = embed_group
+        self.seed = seed
+        self.step_id = 0
+        T = mbs * seq_len
+        D = self.cfg.d_model
+        if self.is_first:
+            self.input_specs = [((mbs, seq_len), torch.int64)]
+        else:
+            self.input_specs = [((T, D), model.arena.dtype)]
+        self.output_specs = [((T, D), model.arena.dtype)] if not self.is_last else [((), torch.float32)]
+        self._ctx = {}
+
+    @property
+    def arena(self):
+        return self.model.arena
+
+    def clear_runtime_states(self):
+        self._ctx.clear()
+        self.step_id += 1
+
+    def forward_mb(self, mb, args, target, loss_fn, loss_scale):
+        ctx = MBContext(mb, _seed(self.seed, self.step_id, mb))
+        x = args[0]
+        out = self.model.forward(x, ctx, self.mbs, self.S, target=target if self.is_last else None,
+                                 loss_scale=loss_scale)
+        self._ctx[mb] = ctx
+        if self.is_last:
+            if target is None:
+                return (out,), None
+            return (out.detach(),), out
+        return (out,), None
+
+    def backward_mb(self, mb, grad_outputs):
+        ctx = self._ctx.pop(mb)
+        dy = None if (self.is_last or not grad_outputs) else grad_outputs[0]
+        dx = self.model.backward(dy, ctx, self.mbs, self.S, weight_grads=True)
+        return (dx,) if dx is not None else ()
+
+    def backward_input_mb(self, mb, grad_outputs):
+        ctx = self._ctx.pop(mb)
+        dy = None if (self.is_last or not grad_outputs) else grad_outputs[0]
+        dx = self.model.backward(dy, ctx, self.mbs, self.S, weight_grads=False)
+        return (dx,) if dx is not None else ()
+
+    def backward_weight_mb(self, mb):
+        self.model.backward_weight(mb)
+
+    def infer_output_specs(self, args):
+        return self.output_specs
+
+    def reduce_grad(self, n_microbatches, scaled_in_loss):
+        if not scaled_in_loss:
+            self.arena.grad.div_(n_microbatches)
+        if self.dp_group is not None and dist.get_world_size(self.dp_group) > 1:
+            return allreduce_flat(self.arena.grad, self.dp_group)
+        return None
+
+    def post_step(self):
+        if self.embed_group is not None and self.cfg.tie_embeddings and self.arena.has("tok_embeddings.weight"):
+            dist.all_reduce(self.arena.g("tok_embeddings.weight"), group=self.embed_group)
+
+
+def build_reference_stage(args, stage_index: int, num_stages: int, device, mbs: int = 8, seq_len: int = 128,
+                          seed: int = 0) -> NativeStage:
+    """Reference architecture (helper:23-55) on the HIP path with the reference split rule."""
+    cfg = NativeConfig.reference(n_layers=args.n_layers, n_heads=args.n_heads, dim=args.dim,
+                                 vocab_size=args.vocab_size, dropout=getattr(args, "dropout", 0.1),
+                                 dim_feedforward=getattr(args, "dim_feedforward", 2048))
+    from .native import balanced_layer_ranges
+    rng = balanced_layer_ranges(cfg, num_stages, reference_rule=True)[stage_index]
+    model = NativeModel(cfg, stage_index, num_stages, device, layer_range=rng, seed=seed)
+    return NativeStage(model, mbs, seq_len)

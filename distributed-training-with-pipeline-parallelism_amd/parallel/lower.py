@@ -137,9 +137,15 @@ def lower(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1, st
             for i, e in enumerate(program[r]):
                 if isinstance(e, Action) and e.op in (Op.B, Op.W):
                     last_bwd[e.stage] = i
-            # insert after the last backward, in descending index order
+            # insert after the last backward and the comm groups that directly follow it
+            # (its sends), in descending index order, so a blocking grad reduction can
+            # never hold back the send its peer is waiting for
             for st, i in sorted(last_bwd.items(), key=lambda kv: -kv[1]):
-                program[r].insert(i + 1, Action(st, Op.REDUCE_GRAD))
+                j = i + 1
+                while j < len(program[r]) and isinstance(program[r][j], CommGroup) and \
+                        all(op.action.op.is_send for op in program[r][j].ops):
+                    j += 1
+                program[r].insert(j, Action(st, Op.REDUCE_GRAD))
     if check:
         check_lowered(program, S)
     return program

@@ -270,6 +270,8 @@ class PipelineRuntime:
                 w.wait()
         for w in reduce_works:
             w.wait()
+        for st in self.stages.values():
+            st.post_step()
         if self.profile:
             self.last_timeline, self.last_step_ms = self.timer.finish()
         if losses is not None and mb_losses:

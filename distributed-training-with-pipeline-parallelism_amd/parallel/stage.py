@@ -77,6 +77,11 @@ class StageBase:
     def clear_runtime_states(self) -> None:
         pass
 
+    def post_step(self) -> None:
+        """Called once after every microbatch and reduction of a step completed (e.g. tied
+        embedding grad sync between the first and the last stage)."""
+        return None
+
 
 class PipelineStage(StageBase):
     """Autograd-driven stage around a user ``nn.Module`` (reference frontend).
