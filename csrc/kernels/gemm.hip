@@ -146,17 +146,20 @@ __global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = {};
 
-  const int nk = K / BK;
-  loadA(0);
-  loadB(0);
+  // split-K: blockIdx.y selects a contiguous K range (f32 accumulate path only)
+  const int nsplit = gridDim.y;
+  const int nk = K / BK / nsplit;
+  const int kbase = (int)blockIdx.y * nk * BK;
+  loadA(kbase);
+  loadB(kbase);
   sa.store(abuf(0));
   sb.store(bbuf(0));
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) {
-      loadA((kt + 1) * BK);
-      loadB((kt + 1) * BK);
+      loadA(kbase + (kt + 1) * BK);
+      loadB(kbase + (kt + 1) * BK);
     }
     const char* ai = abuf(cur);
     const char* bi = bbuf(cur);
@@ -192,6 +195,18 @@ __global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__
         ct[row * CPITCH + col] = acc[i][j][r];
       }
   __syncthreads();
+  if constexpr (ACC) {
+    if (nsplit > 1) {
+      // lane-consecutive columns: each f32 atomic wave-instruction covers 256 contiguous bytes
+      float* C = reinterpret_cast<float*>(Cv);
+      for (int idx = threadIdx.x; idx < BM * BN; idx += 256) {
+        const int row = idx >> 7, col = idx & 127;
+        const int gr = m0 + row, gc = n0 + col;
+        if (gr < M && gc < N) atomicAdd(C + (int64_t)gr * ldc + gc, alpha * ct[row * CPITCH + col]);
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int it = 0; it < (BM * BN / 8) / 256; ++it) {
     const int idx = threadIdx.x + 256 * it;
@@ -262,7 +277,15 @@ static int launch(const void* A, const void* B, void* C, const void* bias, const
     attr_set = true;
   }
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
-  kern<<<nwg, 256, lds, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (const bf16_t*)R,
+  int split = 1;
+  if (ACC) {
+    // enough workgroups to fill 256 CUs twice, each K slice >= 512 deep and a divisor of K/BK
+    const int ktiles = K / BK;
+    int want = (512 + nwg - 1) / nwg;
+    for (int s = want > 16 ? 16 : want; s > 1; --s)
+      if (ktiles % s == 0 && ktiles / s >= 8) { split = s; break; }
+  }
+  kern<<<dim3(nwg, split), 256, lds, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (const bf16_t*)R,
                               (bf16_t*)X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
   return (int)hipGetLastError();
 }
