@@ -37,7 +37,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--schedule", default="1F1B")
-    ap.add_argument("--mbs", type=int, default=8)
+    ap.add_argument("--mbs", type=int, default=16)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--dp", type=int, default=1)

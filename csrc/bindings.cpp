@@ -9,8 +9,8 @@ extern "C" {
 int mp_norm_fwd(int rms, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
                 float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed, hipStream_t st);
 int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
-                const void* dres, void* ds, void* dbranch, float* dw, float* dbias, int rows, int D, float p,
-                uint64_t seed, hipStream_t st);
+                const void* dres, void* ds, void* dbranch, float* dw, float* dbias, float* cs_res, float* cs_ds,
+                int rows, int D, float p, uint64_t seed, hipStream_t st);
 int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss, int T, int V, int Vp, float grad_scale,
                     int64_t ignore_index, int write_grad, hipStream_t st);
 int mp_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int T, int S, int D, int pos_offset,
@@ -38,6 +38,10 @@ int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, cons
                 int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride, int64_t dq_stride,
                 int64_t dk_stride, int64_t dv_stride, int causal, float scale, float p_drop, uint64_t seed,
                 hipStream_t st);
+int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st);
+int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
+             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
+             int epilogue, int c_f32_accum, float alpha, int force_cfg, hipStream_t st);
 int mp_gemm(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
             int epilogue, int c_f32_accum, float alpha, hipStream_t st);
@@ -78,7 +82,7 @@ void norm_fwd(bool rms, torch::Tensor a, c10::optional<torch::Tensor> b, torch::
 void norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c10::optional<torch::Tensor> mean,
               torch::Tensor rstd, c10::optional<torch::Tensor> dres, torch::Tensor ds,
               c10::optional<torch::Tensor> dbranch, torch::Tensor dw, c10::optional<torch::Tensor> dbias, double p,
-              int64_t seed) {
+              int64_t seed, c10::optional<torch::Tensor> cs_res, c10::optional<torch::Tensor> cs_ds) {
   req(dy, torch::kBFloat16, "dy");
   req(s, torch::kBFloat16, "s");
   req(ds, torch::kBFloat16, "ds");
@@ -89,7 +93,9 @@ void norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c10:
   check(mp_norm_bwd(rms, dy.data_ptr(), s.data_ptr(), w.data_ptr(),
                     mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), ptr_or_null(dres),
                     ds.data_ptr(), mptr_or_null(dbranch), dw.data_ptr<float>(),
-                    dbias.has_value() ? dbias->data_ptr<float>() : nullptr, rows, D, (float)p, (uint64_t)seed,
+                    dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
+                    cs_res.has_value() ? cs_res->data_ptr<float>() : nullptr,
+                    cs_ds.has_value() ? cs_ds->data_ptr<float>() : nullptr, rows, D, (float)p, (uint64_t)seed,
                     cur_stream()),
         "norm_bwd");
 }
@@ -235,6 +241,34 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch
         "gemm");
 }
 
+// v2 engine (8 waves, glds staging).  Returns false if the combination is not provided
+// by v2 (the caller then uses gemm()).
+bool gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> bias,
+           c10::optional<torch::Tensor> residual, c10::optional<torch::Tensor> aux, bool transA, bool transB,
+           int64_t epilogue, bool accum, double alpha, int64_t force_cfg) {
+  const int M = C.size(0), N = C.size(1);
+  const int K = transA ? A.size(0) : A.size(1);
+  TORCH_CHECK((transA ? A.size(1) : A.size(0)) == M, "gemm2: A/M mismatch");
+  TORCH_CHECK((transB ? B.size(0) : B.size(1)) == K && (transB ? B.size(1) : B.size(0)) == N, "gemm2: B mismatch");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm2: inner dims must be contiguous");
+  TORCH_CHECK(!accum || C.scalar_type() == torch::kFloat32, "gemm2: accumulate needs f32 C");
+  const int rc = mp_gemm2(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual),
+                          mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),
+                          residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
+                          transA, transB, epilogue, accum, (float)alpha, (int)force_cfg, cur_stream());
+  if (rc == -2 || rc == -1) return false;
+  check(rc, "gemm2");
+  return true;
+}
+
+void transpose(torch::Tensor in, torch::Tensor out) {
+  TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && in.stride(1) == 1 && out.stride(1) == 1, "transpose: 2-D rows");
+  TORCH_CHECK(out.size(0) == in.size(1) && out.size(1) == in.size(0), "transpose: shape");
+  check(mp_transpose(in.data_ptr(), out.data_ptr(), in.size(0), in.size(1), in.stride(0), out.stride(0),
+                     cur_stream()),
+        "transpose");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -256,4 +290,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
+  m.def("gemm2", &gemm2);
+  m.def("transpose", &transpose);
 }

@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 // backward dK / dV: workgroup = 128 keys (4 waves x 32) of one (b, kv head)
 // ==========================================================================================
 template <int DP, bool CAUSAL, bool DROP>
-__global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(
+__global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs,
@@ -462,7 +462,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkdv_kernel(
 template <int DP, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
-    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
+    float* __restrict__ DELTA,
     bf16_t* __restrict__ dQ, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
     int64_t os, int64_t dqs, float scale, float p_drop, uint64_t seed) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -490,7 +491,20 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(
   }
   const int64_t sidx = (int64_t)bh * Sq + qrow;
   const float lse = qvalid ? LSE[sidx] : INFINITY;
-  const float dlt = qvalid ? DELTA[sidx] : 0.f;
+  // delta = rowsum(dO * O), fused here (each lane holds half of the row's d range)
+  float dlt = 0.f;
+  {
+    const bf16_t* Orow = O + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) {
+      const u16x8 ov = gload8(Orow, 16 * s + 8 * hl, D, qvalid);
+      const bf16x8 g = gf[s];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt += bf2f(ov[j]) * (float)g[j];
+    }
+    dlt += __shfl_xor(dlt, 32, 64);
+    if (qvalid && hl == 0) DELTA[sidx] = dlt;
+  }
   const float c = scale * LOG2E;
   f32x16 dq[DP / 32];
 #pragma unroll
@@ -606,9 +620,13 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
                       int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs, int64_t dks, int64_t dvs,
                       float scale, float p, uint64_t seed, hipStream_t st) {
   {
-    const int64_t items = (int64_t)B * Sq * H;
-    attn_delta_kernel<<<(int)((items + 3) / 4), 256, 0, st>>>((const bf16_t*)o, (const bf16_t*)dout, delta, B, Sq, H,
-                                                              D, os);
+    const size_t lds = 4 * 64 * DP * 2;
+    auto kern = attn_bwd_dq_kernel<DP, CAUSAL, DROP>;
+    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    dim3 grid((Sq + 127) / 128, B * H);
+    kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
+                                 (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os,
+                                 dqs, scale, p, seed);
   }
   {
     const size_t lds = 4 * 64 * DP * 2 + 4 * 128 * sizeof(float);
@@ -618,14 +636,6 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
     kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse,
                                  delta, (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, dks, dvs,
                                  scale, p, seed);
-  }
-  {
-    const size_t lds = 4 * 64 * DP * 2;
-    auto kern = attn_bwd_dq_kernel<DP, CAUSAL, DROP>;
-    if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    dim3 grid((Sq + 127) / 128, B * H);
-    kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse,
-                                 delta, (bf16_t*)dq, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, dqs, scale, p, seed);
   }
   return (int)hipGetLastError();
 }

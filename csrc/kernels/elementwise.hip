@@ -155,6 +155,23 @@ __global__ void __launch_bounds__(256) rope_kernel(bf16_t* __restrict__ qkv, con
   }
 }
 
+// out[C][R] = in[R][C] (bf16), 64x64 tiles through LDS (+1 pad); in/out row strides given.
+__global__ void __launch_bounds__(256) transpose_kernel(const bf16_t* __restrict__ in, bf16_t* __restrict__ out,
+                                                        int R, int C, int64_t ldi, int64_t ldo) {
+  __shared__ bf16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? in[(int64_t)r * ldi + c] : (bf16_t)0;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) out[(int64_t)c * ldo + r] = tile[tx][i];
+  }
+}
+
 static int grid_n8(int64_t n) {
   int64_t b = (n / 8 + 255) / 256;
   return (int)(b < 4096 ? (b < 1 ? 1 : b) : 4096);
@@ -214,5 +231,11 @@ extern "C" int mp_rope(void* qkv, const float* cs, const float* sn, int T, int S
   int64_t b = (total + 255) / 256;
   rope_kernel<<<(int)(b < 4096 ? b : 4096), 256, 0, st>>>((bf16_t*)qkv, cs, sn, T, S, H, Hkv, Dh, pos_offset,
                                                           inverse ? -1.f : 1.f);
+  return (int)hipGetLastError();
+}
+
+extern "C" int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st) {
+  dim3 grid((C + 63) / 64, (R + 63) / 64);
+  transpose_kernel<<<grid, 256, 0, st>>>((const bf16_t*)in, (bf16_t*)out, R, C, ldi, ldo);
   return (int)hipGetLastError();
 }

@@ -1,0 +1,406 @@
+// v2 bf16 MFMA GEMM: 8 waves, large tiles, direct-to-LDS staging (global_load_lds_dwordx4).
+//
+//   C[M,N] (+)= alpha * op(A) op(B) (+ fused epilogue); same contract as gemm.hip
+//   (TA/TB layouts, epilogues, f32 split-K accumulate), different engine:
+//
+// * Tiles BMxBN (256x256, 256x192, 256x128, 128x128) chosen per problem by the host so
+//   the tile count fills whole "waves" of 256 CUs (GPT-2: N = 768 / 2304 / 3072 divide
+//   by 192/256 -> zero quantisation loss at T = 16384 tokens).
+// * Staging: every 1 KiB piece of a tile is one wave-instruction of global_load_lds
+//   (no VGPR round trip, no ds_write).  The LDS destination is lane-linear, so the
+//   bank-conflict swizzle of the image is applied on the *source* address (cdna guide
+//   §5.4 rule 21): lane l fetches the logical chunk that belongs at its physical slot.
+// * Pipeline: 2 LDS stages; tile t+1 is in flight while tile t is consumed; counted
+//   `s_waitcnt vmcnt(P)` (P = pieces per wave per tile) + raw s_barrier, never
+//   __syncthreads() (which would drain the in-flight DMA).
+// * MFMA 32x32x16 bf16, per wave (BM/WM)x(BN/WN); fragments by ds_read_b128 (K-contiguous
+//   images) or two ds_read_b64_tr_b16 (outer-contiguous images).
+// * Epilogue staged through LDS one wave-row group at a time -> coalesced 16-byte bias /
+//   residual / activation / store, or lane-consecutive f32 atomics for split-K.
+#include "mp_common.h"
+
+using namespace mp;
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+namespace g2 {
+
+enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RELU = 3, EPI_BIAS_RES = 4, EPI_RES = 5,
+           EPI_DGELU = 6, EPI_DRELU = 7 };
+
+constexpr int BK = 64;
+constexpr int NT = 512;
+
+__device__ __forceinline__ int swz8(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
+__device__ __forceinline__ int swz16(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// K-contiguous image [rows][64 k]: 128-byte rows, 8 chunks
+__device__ __forceinline__ int offK(int row, int chunk) { return row * 128 + 16 * (chunk ^ swz8(row)); }
+// outer-contiguous image [64 k][COLS]: 2*COLS-byte rows; swizzle the low 4 chunk bits
+template <int COLS>
+__device__ __forceinline__ int offO(int row, int chunk) {
+  return row * (COLS * 2) + 16 * ((chunk & ~15) | ((chunk & 15) ^ swz16(row)));
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+template <bool OUTER, int COLS>
+__device__ __forceinline__ bf16x8 frag(const char* img, int rc, int s, int hl) {
+  if constexpr (!OUTER) {
+    return *reinterpret_cast<const bf16x8*>(img + offK(rc, 2 * s + hl));
+  } else {
+    const int i = threadIdx.x & 15, q = i >> 2, p = i & 3;
+    const int col = (rc & ~15) + 4 * p;
+    const int r0 = 16 * s + 8 * hl;
+    const char* a0 = img + offO<COLS>(r0 + q, col >> 3) + ((col & 7) << 1);
+    const char* a1 = img + offO<COLS>(r0 + 4 + q, col >> 3) + ((col & 7) << 1);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  }
+}
+
+// global source (bf16 element pointer) of the 16 bytes that land at byte `pos` of an image
+template <bool OUTER, int ROWS>
+__device__ __forceinline__ const bf16_t* src_of(const bf16_t* base, int64_t ld, int pos, int outer0, int outer_lim,
+                                                int k0) {
+  if constexpr (!OUTER) {  // [ROWS][64k]
+    const int row = pos >> 7, phys = (pos >> 4) & 7;
+    const int chunk = phys ^ swz8(row);
+    int o = outer0 + row;
+    o = o < outer_lim ? o : outer_lim - 1;  // clamp: rows past the edge only feed masked outputs
+    return base + (int64_t)o * ld + k0 + chunk * 8;
+  } else {  // [64k][ROWS cols]
+    constexpr int PITCH = ROWS * 2;
+    const int row = pos / PITCH, phys = (pos % PITCH) >> 4;
+    const int chunk = (phys & ~15) | ((phys & 15) ^ swz16(row));
+    int o = outer0 + chunk * 8;
+    o = o < outer_lim ? o : outer_lim - 8;
+    return base + (int64_t)(k0 + row) * ld + o;
+  }
+}
+
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  // s_waitcnt simm16 for gfx9: vmcnt[3:0] | expcnt[6:4]=7 | lgkmcnt[11:8]=15 | vmcnt_hi[15:14]
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | (((N >> 4) & 3) << 14));
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
+__global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm2_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                      void* __restrict__ Cv, const bf16_t* __restrict__ bias,
+                                                      const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX, int M,
+                                                      int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                                      int64_t ldr, int64_t ldx, float alpha) {
+  static_assert(WM * WN == 8, "8 waves");
+  constexpr int WTM = BM / WM / 32, WTN = BN / WN / 32;
+  static_assert(WTM * 32 * WM == BM && WTN * 32 * WN == BN, "tile/wave mismatch");
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int PIECES = STAGE / 1024, PW = PIECES / 8;
+  static_assert(PW * 8 == PIECES, "pieces must split over 8 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int wg = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int group = wg / (GROUP * gn);
+  const int first_m = group * GROUP;
+  const int gsz = min(gm - first_m, GROUP);
+  const int tm = first_m + (wg % (GROUP * gn)) % gsz;
+  const int tn = (wg % (GROUP * gn)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int wm = wr * (BM / WM), wn = wc * (BN / WN);
+
+  const int nsplit = gridDim.y;
+  const int nk = K / BK / nsplit;
+  const int kbase = (int)blockIdx.y * nk * BK;
+
+  // per-lane source pointers of every piece this wave stages, at k = kbase; a later
+  // k-tile only adds a wave-uniform offset (k0 elements for K-contiguous images,
+  // k0 rows for outer-contiguous ones)
+  const bf16_t* psrc[PW];
+  bool pisA[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int p = wave + 8 * i;            // wave-uniform piece index
+    const int pos = p * 1024 + lane * 16;  // this lane's byte in the stage
+    pisA[i] = p * 1024 < A_BYTES;
+    if (pisA[i]) psrc[i] = src_of<TA, BM>(A, lda, pos, m0, M, kbase);
+    else psrc[i] = src_of<TB, BN>(B, ldb, pos - A_BYTES, n0, N, kbase);
+  }
+  auto issue = [&](int stage, int kt) {
+    char* sb = smem + stage * STAGE;
+    const int64_t dA = TA ? (int64_t)kt * BK * lda : (int64_t)kt * BK;
+    const int64_t dB = TB ? (int64_t)kt * BK * ldb : (int64_t)kt * BK;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int p = wave + 8 * i;
+      const bf16_t* src = psrc[i] + (pisA[i] ? dA : dB);
+      __builtin_amdgcn_global_load_lds((const void*)src, (__attribute__((address_space(3))) void*)(sb + p * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  f32x16 acc[WTM][WTN];
+#pragma unroll
+  for (int i = 0; i < WTM; ++i)
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) acc[i][j] = {};
+
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    wait_vmcnt<PW>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nk; ++t) {
+    const char* sa = smem + (t & 1) * STAGE;
+    const char* sbB = sa + A_BYTES;
+    // fragments double-buffered in registers: k-substep s+1 is read from LDS while the
+    // MFMAs of substep s issue (the loop is fully unrolled, so [s & 1] is static)
+    bf16x8 af[2][WTM], bfr[2][WTN];
+#pragma unroll
+    for (int i = 0; i < WTM; ++i) af[0][i] = frag<TA, BM>(sa, wm + 32 * i + l32, 0, hl);
+#pragma unroll
+    for (int j = 0; j < WTN; ++j) bfr[0][j] = frag<TB, BN>(sbB, wn + 32 * j + l32, 0, hl);
+#pragma unroll
+    for (int s = 0; s < BK / 16; ++s) {
+      const int c = s & 1;
+      if (s + 1 < BK / 16) {
+#pragma unroll
+        for (int i = 0; i < WTM; ++i) af[c ^ 1][i] = frag<TA, BM>(sa, wm + 32 * i + l32, s + 1, hl);
+#pragma unroll
+        for (int j = 0; j < WTN; ++j) bfr[c ^ 1][j] = frag<TB, BN>(sbB, wn + 32 * j + l32, s + 1, hl);
+      }
+      // pin the order: substep s+1's LDS reads are in flight under substep s's MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j) acc[i][j] = mfma32(af[c][i], bfr[c][j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // everyone finished reading this stage before it is refilled
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) {
+      issue(t & 1, t + 2);
+      wait_vmcnt<PW>();  // tile t+1 landed, tile t+2 still in flight
+    } else {
+      wait_vmcnt<0>();
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // ---- epilogue: one wave-row group at a time through LDS
+  constexpr int RG = BM / WM;      // rows per group
+  constexpr int CP = BN + 4;       // f32 pitch
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll 1
+  for (int pass = 0; pass < WM; ++pass) {
+    if (wr == pass) {
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            const int col = wn + 32 * j + l32;
+            ct[row * CP + col] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    const int rbase = m0 + pass * RG;
+    if constexpr (ACC) {
+      if (nsplit > 1) {
+        float* C = reinterpret_cast<float*>(Cv);
+        for (int idx = threadIdx.x; idx < RG * BN; idx += NT) {
+          const int row = idx / BN, col = idx % BN;
+          const int gr = rbase + row, gc = n0 + col;
+          if (gr < M && gc < N) atomicAdd(C + (int64_t)gr * ldc + gc, alpha * ct[row * CP + col]);
+        }
+        __syncthreads();
+        continue;
+      }
+    }
+    for (int idx = threadIdx.x; idx < RG * BN / 8; idx += NT) {
+      const int row = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
+      const int gr = rbase + row, gc = n0 + c8;
+      if (gr >= M || gc >= N) continue;
+      float v[8];
+      const float4 lo = *reinterpret_cast<const float4*>(ct + row * CP + c8);
+      const float4 hi = *reinterpret_cast<const float4*>(ct + row * CP + c8 + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= alpha;
+      if constexpr (ACC) {
+        float* cp = reinterpret_cast<float*>(Cv) + (int64_t)gr * ldc + gc;
+        float4 c0 = *reinterpret_cast<float4*>(cp), c1 = *reinterpret_cast<float4*>(cp + 4);
+        c0.x += v[0]; c0.y += v[1]; c0.z += v[2]; c0.w += v[3];
+        c1.x += v[4]; c1.y += v[5]; c1.z += v[6]; c1.w += v[7];
+        *reinterpret_cast<float4*>(cp) = c0;
+        *reinterpret_cast<float4*>(cp + 4) = c1;
+      } else {
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RES) {
+          u16x8 bv = *reinterpret_cast<const u16x8*>(bias + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[e]);
+        }
+        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
+          u16x8 pre;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            pre[e] = f2bf(v[e]);
+            const float x = bf2f(pre[e]);
+            v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
+          }
+          *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
+        }
+        if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
+          u16x8 rv = *reinterpret_cast<const u16x8*>(R + (int64_t)gr * ldr + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bf2f(rv[e]);
+        }
+        if constexpr (EPI == EPI_DGELU || EPI == EPI_DRELU) {
+          u16x8 xv = *reinterpret_cast<const u16x8*>(AUX + (int64_t)gr * ldx + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = bf2f(xv[e]);
+            v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
+          }
+        }
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(Cv) + (int64_t)gr * ldc + gc) = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
+static int launch(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M, int N, int K,
+                  int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
+                  hipStream_t st) {
+  constexpr int STAGE = (BM + BN) * BK * 2;
+  constexpr int EPI_BYTES = (BM / WM) * (BN + 4) * 4;
+  constexpr int LDS = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
+  auto kern = gemm2_kernel<BM, BN, WM, WN, TA, TB, EPI, ACC>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
+                                          (const bf16_t*)R, (bf16_t*)X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
+  return (int)hipGetLastError();
+}
+
+// tile configurations: 0: 256x256 (2x4 waves), 1: 256x192 (4x2), 2: 256x128 (4x2), 3: 128x128 (2x4)
+struct Cfg {
+  int bm, bn;
+  float eff;  // relative efficiency of the tile shape (bigger tiles reuse more)
+};
+static const Cfg CFGS[4] = {{256, 256, 1.00f}, {256, 192, 0.96f}, {256, 128, 0.90f}, {128, 128, 0.72f}};
+
+static int choose(int M, int N, int K, bool acc, int* split_out) {
+  int best = 3, best_split = 1;
+  float best_score = -1.f;
+  for (int c = 0; c < 4; ++c) {
+    const int cus = c == 3 ? 512 : 256;  // 128x128 tiles fit two workgroups per CU
+    if (acc && CFGS[c].bn == 192) continue;  // outer-contig images need power-of-two widths
+    const int tiles = ((M + CFGS[c].bm - 1) / CFGS[c].bm) * ((N + CFGS[c].bn - 1) / CFGS[c].bn);
+    int split = 1;
+    if (acc) {
+      const int kt = K / BK;
+      const int want = (cus + tiles - 1) / tiles;
+      for (int s = want > 16 ? 16 : want; s > 1; --s)
+        if (kt % s == 0 && kt / s >= 8) { split = s; break; }
+    }
+    const int work = tiles * split;
+    const int waves = (work + cus - 1) / cus;
+    // useful fraction of the occupied CU-time, x tile efficiency, minus padding waste
+    const float fill = (float)work / (waves * cus);
+    const float pad = (float)M * N / ((float)((M + CFGS[c].bm - 1) / CFGS[c].bm * CFGS[c].bm) *
+                                      ((N + CFGS[c].bn - 1) / CFGS[c].bn * CFGS[c].bn));
+    const float score = fill * CFGS[c].eff * pad * (split > 1 ? 0.93f : 1.f);
+    if (score > best_score + 1e-4f) {
+      best_score = score;
+      best = c;
+      best_split = split;
+    }
+  }
+  *split_out = best_split;
+  return best;
+}
+
+}  // namespace g2
+
+using namespace g2;
+
+template <bool TA, bool TB, int EPI, bool ACC>
+static int dispatch(int cfg, const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M,
+                    int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
+                    int split, hipStream_t st) {
+  switch (cfg) {
+    case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    case 1: return launch<256, 192, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    case 2: return launch<256, 128, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    default: return launch<128, 128, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+  }
+}
+
+// returns -2 if the (layout, epilogue) combination is not instantiated here (caller falls back to v1)
+extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux,
+                        int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux,
+                        int transA, int transB, int epilogue, int c_f32_accum, float alpha, int force_cfg,
+                        hipStream_t st) {
+  if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
+  int split = 1;
+  int cfg = choose(M, N, K, c_f32_accum != 0, &split);
+  if (force_cfg >= 0 && force_cfg < 4) cfg = force_cfg;
+  if ((transA || transB) && cfg == 1) cfg = 2;
+  if (!c_f32_accum) split = 1;
+#define MP_G(TA_, TB_, E_, ACC_)                                                                                  \
+  if ((bool)transA == TA_ && (bool)transB == TB_ && epilogue == E_ && (bool)c_f32_accum == ACC_)                 \
+    return dispatch<TA_, TB_, E_, ACC_>(cfg, A, B, C, bias, residual, aux, M, N, K, lda, ldb, ldc, ld_res, ld_aux, \
+                                        alpha, split, st);
+  MP_G(false, false, EPI_NONE, false)
+  MP_G(false, false, EPI_BIAS, false)
+  MP_G(false, false, EPI_BIAS_GELU, false)
+  MP_G(false, false, EPI_BIAS_RELU, false)
+  MP_G(false, false, EPI_BIAS_RES, false)
+  MP_G(false, false, EPI_RES, false)
+  MP_G(false, false, EPI_DGELU, false)
+  MP_G(false, false, EPI_DRELU, false)
+  MP_G(true, true, EPI_NONE, true)
+#undef MP_G
+  return -2;
+}

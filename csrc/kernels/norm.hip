@@ -93,17 +93,27 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(
 }
 
 // Backward.  grid.x blocks, each handling a contiguous slab of rows (4 waves, wave-strided).
-template <int MAXJ, bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BRANCH_GRAD>
+// COLS: also accumulate column sums of dres and of ds (the bias grads of the two
+// projections that feed / consume this residual point: GPT-2's FFN-out and attn-out biases)
+template <int MAXJ, bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BRANCH_GRAD, bool COLS>
 __global__ void __launch_bounds__(256) norm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
     bf16_t* __restrict__ ds_out, bf16_t* __restrict__ dbranch, float* __restrict__ dw, float* __restrict__ dbias,
-    int rows, int D, int rows_per_block, float p_drop, uint64_t seed) {
+    float* __restrict__ cs_res, float* __restrict__ cs_ds, int rows, int D, int rows_per_block, float p_drop,
+    uint64_t seed) {
   __shared__ float red[4][2][MAXJ * 64 * 8 > 1024 ? 1024 : MAXJ * 64 * 8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nchunk = D >> 3;
   float acc_w[MAXJ][8], acc_b[MAXJ][8];
+  float acc_r[COLS ? MAXJ : 1][8], acc_s[COLS ? MAXJ : 1][8];
   float wreg[MAXJ][8];
+  if constexpr (COLS) {
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc_r[j][e] = acc_s[j][e] = 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < MAXJ; ++j) {
     const int c = lane + 64 * j;
@@ -161,6 +171,10 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
           float v = rstd * (g[j][e] - s1 - xh[j][e] * s2);
           if (HAS_DRES) v += bf2f(rv[e]);
           out[e] = f2bf(v);
+          if constexpr (COLS) {
+            acc_r[j][e] += bf2f(rv[e]);
+            acc_s[j][e] += bf2f(out[e]);
+          }
           if (BRANCH_GRAD) bout[e] = f2bf(v * dropout_scale(seed, base + c * 8 + e, p_drop));
         }
         *reinterpret_cast<u16x8*>(ds_out + base + c * 8) = out;
@@ -171,30 +185,33 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
   // reduce per-column partials over the 4 waves, then one atomic per column
   constexpr int CAP = MAXJ * 64 * 8 > 1024 ? 1024 : MAXJ * 64 * 8;
 #pragma unroll
-  for (int j0 = 0; j0 < MAXJ; j0 += CAP / 512) {
-    __syncthreads();
+  for (int q = 0; q < (COLS ? 2 : 1); ++q) {
+    float (*x0)[8] = q == 0 ? acc_w : acc_r;
+    float (*x1)[8] = q == 0 ? acc_b : acc_s;
+    float* o0 = q == 0 ? dw : cs_res;
+    float* o1 = q == 0 ? (HAS_BIAS ? dbias : nullptr) : cs_ds;
 #pragma unroll
-    for (int jj = 0; jj < CAP / 512; ++jj) {
-      const int j = j0 + jj;
-      if (j < MAXJ) {
+    for (int j0 = 0; j0 < MAXJ; j0 += CAP / 512) {
+      __syncthreads();
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          red[wv][0][(jj * 64 + lane) * 8 + e] = acc_w[j][e];
-          red[wv][1][(jj * 64 + lane) * 8 + e] = acc_b[j][e];
+      for (int jj = 0; jj < CAP / 512; ++jj) {
+        const int j = j0 + jj;
+        if (j < MAXJ) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            red[wv][0][(jj * 64 + lane) * 8 + e] = x0[j][e];
+            red[wv][1][(jj * 64 + lane) * 8 + e] = x1[j][e];
+          }
         }
       }
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < CAP; i += 256) {
-      const int jj = i / 512, rem = i % 512, ln = rem / 8, e = rem % 8;
-      const int j = j0 + jj;
-      const int c = ln + 64 * j;
-      if (j < MAXJ && c < nchunk) {
-        float sw = red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i];
-        atomicAdd(dw + c * 8 + e, sw);
-        if (HAS_BIAS) {
-          float sb = red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i];
-          atomicAdd(dbias + c * 8 + e, sb);
+      __syncthreads();
+      for (int i = threadIdx.x; i < CAP; i += 256) {
+        const int jj = i / 512, rem = i % 512, ln = rem / 8, e = rem % 8;
+        const int j = j0 + jj;
+        const int c = ln + 64 * j;
+        if (j < MAXJ && c < nchunk) {
+          atomicAdd(o0 + c * 8 + e, red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i]);
+          if (o1 != nullptr) atomicAdd(o1 + c * 8 + e, red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i]);
         }
       }
     }
@@ -246,18 +263,18 @@ extern "C" int mp_norm_fwd(int rms, const void* a, const void* b, const void* w,
   return (int)hipGetLastError();
 }
 
-template <bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG>
+template <bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG, bool COLS>
 static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
-                       const void* dres, void* ds, void* dbr, float* dw, float* db, int rows, int D, float p,
-                       uint64_t seed, hipStream_t st) {
+                       const void* dres, void* ds, void* dbr, float* dw, float* db, float* csr, float* css, int rows,
+                       int D, float p, uint64_t seed, hipStream_t st) {
   const int nblk = rows < 512 ? (rows + 3) / 4 : 512;
   const int rpb = (rows + nblk - 1) / nblk;
   dim3 grid((rows + rpb - 1) / rpb), block(256);
 #define MP_BWD(J)                                                                                                   \
   case J:                                                                                                           \
-    norm_bwd_kernel<J, RMS, HAS_DRES, HAS_BIAS, BG><<<grid, block, 0, st>>>(                                        \
+    norm_bwd_kernel<J, RMS, HAS_DRES, HAS_BIAS, BG, COLS><<<grid, block, 0, st>>>(                                  \
         (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)ds,        \
-        (bf16_t*)dbr, dw, db, rows, D, rpb, p, seed);                                                               \
+        (bf16_t*)dbr, dw, db, csr, css, rows, D, rpb, p, seed);                                                     \
     break;
   switch (maxj) { MP_BWD(1) MP_BWD(2) MP_BWD(4) MP_BWD(8) MP_BWD(10) MP_BWD(16) }
 #undef MP_BWD
@@ -265,14 +282,24 @@ static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, c
 
 extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean,
                            const float* rstd, const void* dres, void* ds, void* dbranch, float* dw, float* dbias,
-                           int rows, int D, float p, uint64_t seed, hipStream_t st) {
+                           float* cs_res, float* cs_ds, int rows, int D, float p, uint64_t seed, hipStream_t st) {
   if (D % 8 != 0 || D > 16 * 512) return -1;
   const int J = pick_j(D);
   const bool hd = dres != nullptr, hb = dbias != nullptr, bg = dbranch != nullptr;
-#define MP_B(R, HD, HB, BG_)                                                                                  \
-  if (rms == R && hd == HD && hb == HB && bg == BG_) {                                                         \
-    launch_bwd<R, HD, HB, BG_>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, rows, D, p, seed, st); \
-    return (int)hipGetLastError();                                                                           \
+  if (cs_res != nullptr || cs_ds != nullptr) {
+    // column sums of dres and ds (bias grads of the adjacent projections): LN, dres, no branch
+    if (rms || !hd || bg || cs_res == nullptr || cs_ds == nullptr || J > 4) return -3;
+    if (hb) launch_bwd<false, true, true, false, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res,
+                                                       cs_ds, rows, D, p, seed, st);
+    else launch_bwd<false, true, false, false, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res,
+                                                     cs_ds, rows, D, p, seed, st);
+    return (int)hipGetLastError();
+  }
+#define MP_B(R, HD, HB, BG_)                                                                                   \
+  if (rms == R && hd == HD && hb == HB && bg == BG_) {                                                          \
+    launch_bwd<R, HD, HB, BG_, false>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, nullptr, nullptr, \
+                                      rows, D, p, seed, st);                                                   \
+    return (int)hipGetLastError();                                                                            \
   }
   MP_B(0, 0, 0, 0) MP_B(0, 0, 0, 1) MP_B(0, 0, 1, 0) MP_B(0, 0, 1, 1)
   MP_B(0, 1, 0, 0) MP_B(0, 1, 0, 1) MP_B(0, 1, 1, 0) MP_B(0, 1, 1, 1)

@@ -296,17 +296,21 @@ class Block:
                 da = ops.linear_dx(dy, self.w("ffn.w2.weight"), act_input=a, act=cfg.activation)
                 wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
                 if cfg.bias:
-                    wjobs.append(lambda dy=dy: ops.colsum(dy, self.g("ffn.w2.bias")))
                     wjobs.append(lambda da=da: ops.colsum(da, self.g("ffn.w1.bias")))
                 wjobs.append(lambda da=da, h2=h2: ops.linear_dw(da, h2, self.g("ffn.w1.weight")))
                 dh2 = ops.linear_dx(da, self.w("ffn.w1.weight"))
+            fuse_cs = cfg.bias and kind == "layernorm"
             dx2, _ = ops.norm_bwd(dh2, st["x2"], self.w("ffn_norm.weight"), st["mu2"], st["rs2"], kind=kind,
-                                  dres=dy, dw=self.g("ffn_norm.weight"), dbias=self.gb("ffn_norm.bias"))
+                                  dres=dy, dw=self.g("ffn_norm.weight"), dbias=self.gb("ffn_norm.bias"),
+                                  colsum_dres=self.g("ffn.w2.bias") if fuse_cs else None,
+                                  colsum_ds=self.g("attn.wo.bias") if fuse_cs else None)
+            if cfg.bias and not fuse_cs:
+                wjobs.append(lambda dy=dy: ops.colsum(dy, self.g("ffn.w2.bias")))
             # ---------------- attention
             o = st["o"]
             do = ops.linear_dx(dx2, self.w("attn.wo.weight"))
             wjobs.append(lambda dx2=dx2, o=o: ops.linear_dw(dx2, o, self.g("attn.wo.weight")))
-            if cfg.bias:
+            if cfg.bias and not fuse_cs:
                 wjobs.append(lambda dx2=dx2: ops.colsum(dx2, self.g("attn.wo.bias")))
             qkv = st["qkv"]
             q, k, v = qkv[:, : H * Dh], qkv[:, H * Dh:(H + KV) * Dh], qkv[:, (H + KV) * Dh:]

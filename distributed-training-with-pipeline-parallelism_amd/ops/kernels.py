@@ -19,6 +19,9 @@ LOG2E = 1.4426950408889634
 # GEMM backend for plain (epilogue-free) GEMMs on GPU: "hip" (our MFMA kernel) or "blas"
 # (hipBLASLt through torch).  Fused-epilogue GEMMs always use the HIP kernel.
 GEMM_BACKEND = os.environ.get("MIPIPE_GEMM", "hip")
+# GEMM engine: 2 = 8-wave glds engine (gemm2.hip) with fallback to 1 (gemm.hip) for
+# combinations v2 does not instantiate; 1 = always gemm.hip.
+GEMM_V = int(os.environ.get("MIPIPE_GEMM_V", "2"))
 
 
 def load_ext():
@@ -107,8 +110,11 @@ def norm_fwd(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = No
 def norm_bwd(dy: torch.Tensor, s: torch.Tensor, w: torch.Tensor, mean, rstd, kind: str = "layernorm",
              dres: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
              dbias: Optional[torch.Tensor] = None, p_drop: float = 0.0, seed: int = 0, ds=None, dbranch=None,
-             want_branch: bool = False):
-    """ds = d(norm input) (+ dres); dw/dbias (f32) accumulate.  Returns (ds, dbranch)."""
+             want_branch: bool = False, colsum_dres: Optional[torch.Tensor] = None,
+             colsum_ds: Optional[torch.Tensor] = None):
+    """ds = d(norm input) (+ dres); dw/dbias (f32) accumulate.  Optionally also accumulates
+    the column sums of ``dres`` and of ``ds`` (f32) -- the bias grads of the projections
+    around this residual point -- in the same pass.  Returns (ds, dbranch)."""
     rms = kind == "rmsnorm"
     D = dy.shape[-1]
     rows = dy.numel() // D
@@ -119,7 +125,7 @@ def norm_bwd(dy: torch.Tensor, s: torch.Tensor, w: torch.Tensor, mean, rstd, kin
         dbranch = torch.empty_like(dy)
     if _gpu(dy):
         _ext().norm_bwd(rms, dy, s, w, mean, rstd, dres, ds, dbranch if need_branch else None, dw, dbias,
-                        float(p_drop), int(seed))
+                        float(p_drop), int(seed), colsum_dres, colsum_ds)
         return ds, (dbranch if need_branch else (ds if want_branch else None))
     d = dy.float().reshape(rows, D)
     x = s.float().reshape(rows, D)
@@ -132,6 +138,10 @@ def norm_bwd(dy: torch.Tensor, s: torch.Tensor, w: torch.Tensor, mean, rstd, kin
     if dres is not None:
         v = v + dres.float().reshape(rows, D)
     ds.copy_(v.reshape(dy.shape).to(ds.dtype))
+    if colsum_dres is not None:
+        colsum_dres += dres.float().reshape(rows, D).sum(0)
+    if colsum_ds is not None:
+        colsum_ds += ds.float().reshape(rows, D).sum(0)
     if dw is not None:
         dw += (d * xh).sum(0)
     if dbias is not None:
@@ -211,9 +221,24 @@ def embed_bwd(idx: torch.Tensor, dout: torch.Tensor, dwte: torch.Tensor, dwpe: O
 # GEMMs (linear layers)
 # ======================================================================================
 def _gemm(A, B, C, bias=None, residual=None, aux=None, transA=False, transB=False, epi=EPI_NONE, accum=False,
-          alpha=1.0):
-    _ext().gemm(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum), float(alpha))
+          alpha=1.0, cfg: int = -1):
+    e = _ext()
+    if GEMM_V >= 2 and e.gemm2(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum),
+                               float(alpha), int(cfg)):
+        return C
+    e.gemm(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum), float(alpha))
     return C
+
+
+def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """out = x^T for a 2-D bf16 matrix (row-contiguous views allowed)."""
+    if out is None:
+        out = torch.empty(x.shape[1], x.shape[0], device=x.device, dtype=x.dtype)
+    if _gpu(x):
+        _ext().transpose(x, out)
+    else:
+        out.copy_(x.t())
+    return out
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
@@ -274,13 +299,23 @@ def _act_grad_cpu(x, act):
 
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tensor] = None, act: str = "none",
-              out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None):
+              out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
+              wt: Optional[torch.Tensor] = None):
     """dx = dy @ w  (w [N,K]), optionally times act'(act_input) (the previous layer's
-    pre-activation) and plus ``residual``."""
+    pre-activation) and plus ``residual``.  With ``wt`` (= w^T, [K,N], kept by the param
+    arena) the GEMM runs in the both-K-contiguous form on the v2 engine."""
     T, N = dy.shape
     K = w.shape[1]
     if out is None:
         out = torch.empty(T, K, device=dy.device, dtype=dy.dtype)
+    if _gpu(dy) and wt is not None and GEMM_BACKEND != "blas":
+        if act != "none":
+            _gemm(dy, wt, out, aux=act_input, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU)
+        elif residual is not None:
+            _gemm(dy, wt, out, residual=residual, epi=EPI_RES)
+        else:
+            _gemm(dy, wt, out)
+        return out
     if _gpu(dy):
         if act != "none":
             _gemm(dy, w, out, aux=act_input, transB=True, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU)

@@ -229,3 +229,72 @@ def test_adamw():
     ss = torch.zeros(1, device=DEV)
     ops.sumsq(g.to(DEV), ss)
     assert abs(ss.item() - (g.double() ** 2).sum().item()) / ss.item() < 1e-4
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, "bias_gelu"), (1000, 2304, 256, "bias"), (256, 384, 128, "res"),
+                                       (520, 136, 64, "none"), (512, 768, 3072, "dgelu")])
+def test_gemm2_configs(cfg, M, N, K, epi):
+    from mipipe.ops import kernels as _k
+    torch.manual_seed(0)
+    x, w, b, r = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1), rnd(M, N)
+    xg, wg, bg, rg = (t.to(DEV) for t in (x, w, b, r))
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    aux = rnd(M, N).to(DEV)
+    epi_id = dict(none=0, bias=1, bias_gelu=2, res=5, dgelu=6)[epi]
+    _k._gemm(xg, wg, y, bias=bg if "bias" in epi else None, residual=rg if epi == "res" else None,
+             aux=aux if "gelu" in epi else None, epi=epi_id, cfg=cfg)
+    ref = x.float() @ w.float().t()
+    if "bias" in epi:
+        ref = ref + b.float()
+    if epi == "bias_gelu":
+        close(aux, ref.to(torch.bfloat16))
+        ref = torch.nn.functional.gelu(ref.to(torch.bfloat16).float(), approximate="tanh")
+    if epi == "res":
+        ref = ref + r.float()
+    if epi == "dgelu":
+        a = aux.float().cpu()
+        k0, k1 = 0.7978845608028654, 0.044715
+        t = torch.tanh(k0 * (a + k1 * a ** 3))
+        ref = ref * (0.5 * (1 + t) + 0.5 * a * (1 - t * t) * k0 * (1 + 3 * k1 * a * a))
+    close(y, ref)
+
+
+@pytest.mark.parametrize("cfg", [0, 2, 3])
+@pytest.mark.parametrize("M,N,K", [(768, 768, 8192), (2304, 768, 1024), (136, 200, 512), (3072, 768, 2048)])
+def test_gemm2_dw_splitk(cfg, M, N, K):
+    from mipipe.ops import kernels as _k
+    torch.manual_seed(0)
+    dy, x = rnd(K, M, scale=0.1), rnd(K, N)
+    base = torch.randn(M, N)
+    g = base.clone().to(DEV)
+    _k._gemm(dy.to(DEV), x.to(DEV), g, transA=True, transB=True, accum=True, cfg=cfg)
+    close(g, base + dy.float().t() @ x.float(), atol=3e-2, rtol=1e-2)
+
+
+def test_linear_dx_with_transposed_weight():
+    torch.manual_seed(0)
+    dy, w, a = rnd(1024, 2304), rnd(2304, 768, scale=0.02), rnd(1024, 768)
+    wt = ops.transpose(w.to(DEV))
+    close(wt, w.t().contiguous(), atol=0, rtol=0)
+    ref = ops.linear_dx(dy, w, act_input=a, act="gelu_tanh")
+    got = ops.linear_dx(dy.to(DEV), w.to(DEV), act_input=a.to(DEV), act="gelu_tanh", wt=wt)
+    close(got, ref)
+
+
+def test_norm_bwd_fused_colsums():
+    torch.manual_seed(0)
+    T, D = 300, 768
+    x, w, b = rnd(T, D), rnd(D, scale=0.5) + 1, rnd(D, scale=0.1)
+    dy, dres = rnd(T, D), rnd(T, D)
+    outs = []
+    for dev in ("cpu", DEV):
+        mv = lambda t: t.to(dev)
+        y, s, mean, rstd = ops.norm_fwd(mv(x), mv(w), mv(b))
+        dw, db = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        c1, c2 = torch.zeros(D, device=dev), torch.zeros(D, device=dev)
+        ds, _ = ops.norm_bwd(mv(dy), s, mv(w), mean, rstd, dres=mv(dres), dw=dw, dbias=db, colsum_dres=c1,
+                             colsum_ds=c2)
+        outs.append((ds, dw, db, c1, c2))
+    for a, g in zip(*outs):
+        close(g, a, atol=5e-2, rtol=2e-2)

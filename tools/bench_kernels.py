@@ -33,7 +33,7 @@ def timeit(fn, iters=20, warm=5):
     return s.elapsed_time(e) / iters * 1e-3
 
 
-def gemm_cases(T=8192):
+def gemm_cases(T=16384):
     d, f, V = 768, 3072, 50304
     out = []
     for name, N, K in [("qkv", 3 * d, d), ("wo", d, d), ("fc1", f, d), ("fc2", d, f), ("head", V, d)]:
@@ -68,7 +68,8 @@ def main():
             dy = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             w = torch.randn(K, N, device=dev, dtype=torch.bfloat16) * K ** -0.5
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            ours = lambda: _k._gemm(dy, w, y, transB=True)
+            wt = w.t().contiguous()   # the arena keeps W^T: dX runs as an NT GEMM
+            ours = lambda: _k._gemm(dy, wt, y)
             lib = lambda: torch.mm(dy, w, out=y)
         else:               # dw[M,N] += dy[K,M]^T x[K,N]  (f32 accumulate)
             dy = torch.randn(K, M, device=dev, dtype=torch.bfloat16)
