@@ -88,18 +88,25 @@ __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, floa
   return hash_u32(seed, idx) >= thr ? 1.0f / (1.0f - p) : 0.0f;
 }
 
+// tanh-GELU through one v_exp_f32 + one v_rcp_f32 (0.5(1+tanh u) = sigmoid(2u));
+// libm tanhf is a long branchy sequence and dominated the GEMM epilogues.
+__device__ __forceinline__ float sigmoid_fast(float z) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * z));
+}
+
 __device__ __forceinline__ float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float u = k0 * (x + k1 * x * x * x);
-  return 0.5f * x * (1.0f + tanhf(u));
+  const float u = k0 * (x + k1 * x * x * x);
+  return x * sigmoid_fast(2.0f * u);
 }
 
 __device__ __forceinline__ float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float u = k0 * (x + k1 * x2 * x);
-  float t = tanhf(u);
-  return 0.5f * (1.0f + t) + 0.5f * x * (1.0f - t * t) * k0 * (1.0f + 3.0f * k1 * x2);
+  const float x2 = x * x;
+  const float u = k0 * (x + k1 * x2 * x);
+  const float sg = sigmoid_fast(2.0f * u);  // = 0.5(1 + tanh u)
+  // d/dx [x sg(2u)] = sg + x * 2 sg (1 - sg) * u'
+  return sg + 2.0f * x * sg * (1.0f - sg) * k0 * (1.0f + 3.0f * k1 * x2);
 }
 
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }

@@ -125,9 +125,13 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
   const int wr = wave / WN, wc = wave % WN;
   const int wm = wr * (BM / WM), wn = wc * (BN / WN);
 
+  // split-K: split y owns k-tiles [y*KT/S, (y+1)*KT/S) (uneven splits allowed, so the
+  // split count can be chosen for CU fill rather than divisibility)
   const int nsplit = gridDim.y;
-  const int nk = K / BK / nsplit;
-  const int kbase = (int)blockIdx.y * nk * BK;
+  const int ktiles = K / BK;
+  const int kt0 = (int)blockIdx.y * ktiles / nsplit;
+  const int nk = ((int)blockIdx.y + 1) * ktiles / nsplit - kt0;
+  const int kbase = kt0 * BK;
 
   // per-lane source pointers of every piece this wave stages, at k = kbase; a later
   // k-tile only adds a wave-uniform offset (k0 elements for K-contiguous images,
@@ -331,30 +335,28 @@ struct Cfg {
 static const Cfg CFGS[4] = {{256, 256, 1.00f}, {256, 192, 0.96f}, {256, 128, 0.90f}, {128, 128, 0.72f}};
 
 static int choose(int M, int N, int K, bool acc, int* split_out) {
+  // minimise modelled time = (#rounds of CU slots) x (per-item k-loop + epilogue) / tile efficiency;
+  // padded tiles are charged like real ones, so quantisation and padding waste both count
   int best = 3, best_split = 1;
-  float best_score = -1.f;
+  float best_t = 3.0e38f;
+  const int kt = K / BK;
   for (int c = 0; c < 4; ++c) {
-    const int cus = c == 3 ? 512 : 256;  // 128x128 tiles fit two workgroups per CU
+    const int slots = c == 3 ? 512 : 256;  // 128x128 tiles fit two workgroups per CU
     if (acc && CFGS[c].bn == 192) continue;  // outer-contig images need power-of-two widths
     const int tiles = ((M + CFGS[c].bm - 1) / CFGS[c].bm) * ((N + CFGS[c].bn - 1) / CFGS[c].bn);
-    int split = 1;
-    if (acc) {
-      const int kt = K / BK;
-      const int want = (cus + tiles - 1) / tiles;
-      for (int s = want > 16 ? 16 : want; s > 1; --s)
-        if (kt % s == 0 && kt / s >= 8) { split = s; break; }
-    }
-    const int work = tiles * split;
-    const int waves = (work + cus - 1) / cus;
-    // useful fraction of the occupied CU-time, x tile efficiency, minus padding waste
-    const float fill = (float)work / (waves * cus);
-    const float pad = (float)M * N / ((float)((M + CFGS[c].bm - 1) / CFGS[c].bm * CFGS[c].bm) *
-                                      ((N + CFGS[c].bn - 1) / CFGS[c].bn * CFGS[c].bn));
-    const float score = fill * CFGS[c].eff * pad * (split > 1 ? 0.93f : 1.f);
-    if (score > best_score + 1e-4f) {
-      best_score = score;
-      best = c;
-      best_split = split;
+    const float area = (float)(CFGS[c].bm * CFGS[c].bn) / (256.f * 256.f) * (c == 3 ? 2.f : 1.f);
+    const int max_split = acc ? (kt / 4 < 32 ? kt / 4 : 32) : 1;
+    for (int s = 1; s <= (max_split > 1 ? max_split : 1); ++s) {
+      const int work = tiles * s;
+      const int rounds = (work + slots - 1) / slots;
+      const int kper = (kt + s - 1) / s;
+      const float epi = s > 1 ? 6.f : 2.f;  // f32 atomics vs a bf16/f32 store, in k-tile units
+      const float t = rounds * (kper + epi + 2.f) * area / CFGS[c].eff;  // +2: prologue fill
+      if (t < best_t * 0.999f) {
+        best_t = t;
+        best = c;
+        best_split = s;
+      }
     }
   }
   *split_out = best_split;

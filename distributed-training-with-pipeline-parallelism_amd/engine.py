@@ -59,6 +59,7 @@ class FlatAdamW:
             ops.adamw_(a.master, a.grad, m, v, a.w16, a.n_decay, lr, self.betas[0], self.betas[1], self.eps, self.wd,
                        self.step_count, self.sumsq if use_clip else None, self.max_norm if use_clip else 0.0, 1.0,
                        zero_grad=True)
+            a.refresh_transposes()
 
     def state_dict(self):
         return {"step": self.step_count, "m": [t.clone() for t in self.m], "v": [t.clone() for t in self.v]}

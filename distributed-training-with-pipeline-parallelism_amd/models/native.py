@@ -38,6 +38,7 @@ class ParamSpec:
     init: str          # normal | zeros | ones | normal_scaled
     decay: bool
     std: float = 0.02
+    transpose: bool = False  # keep a bf16 W^T copy (dX GEMMs run both-K-contiguous)
 
 
 def _name_seed(seed: int, name: str) -> int:
@@ -74,6 +75,15 @@ class ParamArena:
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.w16 = torch.zeros(self.numel, dtype=dtype, device=self.device)
+        # transposed bf16 copies of the matrices used as B in dX = dY W (GPU only)
+        self.t_offsets: Dict[str, int] = {}
+        toff = 0
+        if self.device.type == "cuda":
+            for s in specs:
+                if s.transpose and len(s.shape) == 2:
+                    self.t_offsets[s.name] = toff
+                    toff += (int(math.prod(s.shape)) + 7) // 8 * 8
+        self.wt16 = torch.zeros(max(toff, 1), dtype=dtype, device=self.device)
         if init:
             self.init_params(seed)
 
@@ -93,6 +103,19 @@ class ParamArena:
 
     def sync_w16(self) -> None:
         ops.cast_f32_bf16(self.master, self.w16)
+        self.refresh_transposes()
+
+    def refresh_transposes(self) -> None:
+        for name in self.t_offsets:
+            ops.transpose(self.w(name), self.wt(name))
+
+    def wt(self, name: str) -> Optional[torch.Tensor]:
+        """W^T ([in, out]) view of a 2-D weight, or None if no copy is kept."""
+        o = self.t_offsets.get(name)
+        if o is None:
+            return None
+        r, c = self.specs[name].shape
+        return self.wt16[o: o + r * c].view(c, r)
 
     def _view(self, buf: torch.Tensor, name: str) -> torch.Tensor:
         s = self.specs[name]
@@ -162,13 +185,13 @@ def block_param_specs(cfg: NativeConfig, i: int) -> List[ParamSpec]:
     P = f"layers.{i}."
     if cfg.cross_attn:  # reference nn.TransformerDecoderLayer names
         for att in ("self_attn", "multihead_attn"):
-            out += [ParamSpec(P + f"{att}.in_proj_weight", (3 * d, d), "normal", True, std),
+            out += [ParamSpec(P + f"{att}.in_proj_weight", (3 * d, d), "normal", True, std, True),
                     ParamSpec(P + f"{att}.in_proj_bias", (3 * d,), "zeros", False),
-                    ParamSpec(P + f"{att}.out_proj.weight", (d, d), "normal", True, std),
+                    ParamSpec(P + f"{att}.out_proj.weight", (d, d), "normal", True, std, True),
                     ParamSpec(P + f"{att}.out_proj.bias", (d,), "zeros", False)]
-        out += [ParamSpec(P + "linear1.weight", (f, d), "normal", True, std),
+        out += [ParamSpec(P + "linear1.weight", (f, d), "normal", True, std, True),
                 ParamSpec(P + "linear1.bias", (f,), "zeros", False),
-                ParamSpec(P + "linear2.weight", (d, f), "normal", True, std),
+                ParamSpec(P + "linear2.weight", (d, f), "normal", True, std, True),
                 ParamSpec(P + "linear2.bias", (d,), "zeros", False)]
         for k in (1, 2, 3):
             out += [ParamSpec(P + f"norm{k}.weight", (d,), nb, False), ParamSpec(P + f"norm{k}.bias", (d,), "zeros", False)]
@@ -176,8 +199,8 @@ def block_param_specs(cfg: NativeConfig, i: int) -> List[ParamSpec]:
     out += [ParamSpec(P + "attn_norm.weight", (d,), nb, False)]
     if cfg.norm == "layernorm":
         out += [ParamSpec(P + "attn_norm.bias", (d,), "zeros", False)]
-    out += [ParamSpec(P + "attn.wqkv.weight", (cfg.qkv_dim, d), "normal", True, std),
-            ParamSpec(P + "attn.wo.weight", (d, d), "normal", True, rstd)]
+    out += [ParamSpec(P + "attn.wqkv.weight", (cfg.qkv_dim, d), "normal", True, std, True),
+            ParamSpec(P + "attn.wo.weight", (d, d), "normal", True, rstd, True)]
     if cfg.bias:
         out += [ParamSpec(P + "attn.wqkv.bias", (cfg.qkv_dim,), "zeros", False),
                 ParamSpec(P + "attn.wo.bias", (d,), "zeros", False)]
@@ -185,11 +208,11 @@ def block_param_specs(cfg: NativeConfig, i: int) -> List[ParamSpec]:
     if cfg.norm == "layernorm":
         out += [ParamSpec(P + "ffn_norm.bias", (d,), "zeros", False)]
     if cfg.activation == "swiglu":
-        out += [ParamSpec(P + "ffn.w13.weight", (2 * f, d), "normal", True, std),
-                ParamSpec(P + "ffn.w2.weight", (d, f), "normal", True, rstd)]
+        out += [ParamSpec(P + "ffn.w13.weight", (2 * f, d), "normal", True, std, True),
+                ParamSpec(P + "ffn.w2.weight", (d, f), "normal", True, rstd, True)]
     else:
-        out += [ParamSpec(P + "ffn.w1.weight", (f, d), "normal", True, std),
-                ParamSpec(P + "ffn.w2.weight", (d, f), "normal", True, rstd)]
+        out += [ParamSpec(P + "ffn.w1.weight", (f, d), "normal", True, std, True),
+                ParamSpec(P + "ffn.w2.weight", (d, f), "normal", True, rstd, True)]
         if cfg.bias:
             out += [ParamSpec(P + "ffn.w1.bias", (f,), "zeros", False),
                     ParamSpec(P + "ffn.w2.bias", (d,), "zeros", False)]
@@ -215,6 +238,9 @@ class Block:
 
     def wb(self, n):
         return self.A.w(self.P + n) if self.A.has(self.P + n) else None
+
+    def wt(self, n):
+        return self.A.wt(self.P + n)
 
     def gb(self, n):
         return self.A.g(self.P + n) if self.A.has(self.P + n) else None
@@ -285,20 +311,21 @@ class Block:
             H, KV, Dh = cfg.n_heads, cfg.n_kv_heads, cfg.head_dim
             # ---------------- FFN
             if cfg.activation == "swiglu":
-                dgact = ops.linear_dx(dy, self.w("ffn.w2.weight"))
+                dgact = ops.linear_dx(dy, self.w("ffn.w2.weight"), wt=self.wt("ffn.w2.weight"))
                 gact, h2, gu = st["g"], st["h2"], st["gu"]
                 wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
                 dgu = ops.swiglu_bwd(gu, dgact)
                 wjobs.append(lambda dgu=dgu, h2=h2: ops.linear_dw(dgu, h2, self.g("ffn.w13.weight")))
-                dh2 = ops.linear_dx(dgu, self.w("ffn.w13.weight"))
+                dh2 = ops.linear_dx(dgu, self.w("ffn.w13.weight"), wt=self.wt("ffn.w13.weight"))
             else:
                 gact, a, h2 = st["g"], st["a"], st["h2"]
-                da = ops.linear_dx(dy, self.w("ffn.w2.weight"), act_input=a, act=cfg.activation)
+                da = ops.linear_dx(dy, self.w("ffn.w2.weight"), act_input=a, act=cfg.activation,
+                                   wt=self.wt("ffn.w2.weight"))
                 wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
                 if cfg.bias:
                     wjobs.append(lambda da=da: ops.colsum(da, self.g("ffn.w1.bias")))
                 wjobs.append(lambda da=da, h2=h2: ops.linear_dw(da, h2, self.g("ffn.w1.weight")))
-                dh2 = ops.linear_dx(da, self.w("ffn.w1.weight"))
+                dh2 = ops.linear_dx(da, self.w("ffn.w1.weight"), wt=self.wt("ffn.w1.weight"))
             fuse_cs = cfg.bias and kind == "layernorm"
             dx2, _ = ops.norm_bwd(dh2, st["x2"], self.w("ffn_norm.weight"), st["mu2"], st["rs2"], kind=kind,
                                   dres=dy, dw=self.g("ffn_norm.weight"), dbias=self.gb("ffn_norm.bias"),
@@ -308,7 +335,7 @@ class Block:
                 wjobs.append(lambda dy=dy: ops.colsum(dy, self.g("ffn.w2.bias")))
             # ---------------- attention
             o = st["o"]
-            do = ops.linear_dx(dx2, self.w("attn.wo.weight"))
+            do = ops.linear_dx(dx2, self.w("attn.wo.weight"), wt=self.wt("attn.wo.weight"))
             wjobs.append(lambda dx2=dx2, o=o: ops.linear_dw(dx2, o, self.g("attn.wo.weight")))
             if cfg.bias and not fuse_cs:
                 wjobs.append(lambda dx2=dx2: ops.colsum(dx2, self.g("attn.wo.bias")))
@@ -324,7 +351,7 @@ class Block:
             wjobs.append(lambda dqkv=dqkv, h1=h1: ops.linear_dw(dqkv, h1, self.g("attn.wqkv.weight")))
             if cfg.bias:
                 wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, self.g("attn.wqkv.bias")))
-            dh1 = ops.linear_dx(dqkv, self.w("attn.wqkv.weight"))
+            dh1 = ops.linear_dx(dqkv, self.w("attn.wqkv.weight"), wt=self.wt("attn.wqkv.weight"))
             dx, _ = ops.norm_bwd(dh1, st["x"], self.w("attn_norm.weight"), st["mu1"], st["rs1"], kind=kind,
                                  dres=dx2, dw=self.g("attn_norm.weight"), dbias=self.gb("attn_norm.bias"))
         if weight_grads:
@@ -383,7 +410,7 @@ class Block:
         o = st[key + "o"]
         wjobs.append(lambda dout=dout, o=o: ops.linear_dw(dout, o, self.g(prefix + ".out_proj.weight")))
         wjobs.append(lambda dout=dout: ops.colsum(dout, self.g(prefix + ".out_proj.bias")))
-        do = ops.linear_dx(dout, self.w(prefix + ".out_proj.weight"))
+        do = ops.linear_dx(dout, self.w(prefix + ".out_proj.weight"), wt=self.wt(prefix + ".out_proj.weight"))
         if self_attn:
             qkv = st[key + "qkv"]
             q, k, v = qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:]
@@ -400,14 +427,15 @@ class Block:
         if self_attn:
             wjobs.append(lambda dqkv=dqkv, xq=xq: ops.linear_dw(dqkv, xq, gW))
             wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, gb))
-            dx = ops.linear_dx(dqkv, W, residual=dres_q)
+            dx = ops.linear_dx(dqkv, W, residual=dres_q, wt=self.wt(prefix + ".in_proj_weight"))
             return dx, None
         wjobs.append(lambda dq=dq, xq=xq: ops.linear_dw(dq, xq, gW[:d]))
         wjobs.append(lambda dq=dq: ops.colsum(dq, gb[:d]))
         wjobs.append(lambda dkv=dkv, xkv=xkv: ops.linear_dw(dkv, xkv, gW[d:]))
         wjobs.append(lambda dkv=dkv: ops.colsum(dkv, gb[d:]))
-        dxq = ops.linear_dx(dq, W[:d], residual=dres_q)
-        dxkv = ops.linear_dx(dkv, W[d:], residual=dres_kv)
+        WT = self.wt(prefix + ".in_proj_weight")
+        dxq = ops.linear_dx(dq, W[:d], residual=dres_q, wt=None if WT is None else WT[:, :d])
+        dxkv = ops.linear_dx(dkv, W[d:], residual=dres_kv, wt=None if WT is None else WT[:, d:])
         return dxq, dxkv
 
     def _ref_backward(self, dy, B, S, st, sd, wjobs):
@@ -419,11 +447,11 @@ class Block:
         gact, a, x2 = st["g"], st["a"], st["x2"]
         wjobs.append(lambda df=df, gact=gact: ops.linear_dw(df, gact, self.g("linear2.weight")))
         wjobs.append(lambda df=df: ops.colsum(df, self.g("linear2.bias")))
-        dg = ops.linear_dx(df, self.w("linear2.weight"))
+        dg = ops.linear_dx(df, self.w("linear2.weight"), wt=self.wt("linear2.weight"))
         da = ops.act_bwd(dg, a, "relu", dbias=None, p_drop=p, seed=_seed(sd, 5))
         wjobs.append(lambda da=da: ops.colsum(da, self.g("linear1.bias")))
         wjobs.append(lambda da=da, x2=x2: ops.linear_dw(da, x2, self.g("linear1.weight")))
-        dx2 = ops.linear_dx(da, self.w("linear1.weight"), residual=ds3)
+        dx2 = ops.linear_dx(da, self.w("linear1.weight"), residual=ds3, wt=self.wt("linear1.weight"))
         # norm2(x1 + drop(ca))
         ds2, dca = ops.norm_bwd(dx2, st["s2"], self.w("norm2.weight"), st["mu2"], st["rs2"], dw=self.g("norm2.weight"),
                                 dbias=self.g("norm2.bias"), p_drop=p, seed=_seed(sd, 4), want_branch=True)
@@ -500,7 +528,8 @@ class NativeModel:
         specs: List[ParamSpec] = []
         d = cfg.d_model
         if self.first:
-            specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False, cfg.init_std))
+            specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False, cfg.init_std,
+                                   cfg.tie_embeddings and self.last))
             if cfg.pos == "learned":
                 specs.append(ParamSpec("pos_embeddings.weight", (cfg.max_seq_len, d), "normal", False, 0.01))
         for i in range(*layer_range):
@@ -513,9 +542,9 @@ class NativeModel:
             if cfg.tie_embeddings:
                 if not self.first:  # tied copy on the last stage, kept in sync by the embed group
                     specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False,
-                                           cfg.init_std))
+                                           cfg.init_std, True))
             else:
-                specs.append(ParamSpec("output.weight", (cfg.vocab_padded, d), "normal", True, cfg.init_std))
+                specs.append(ParamSpec("output.weight", (cfg.vocab_padded, d), "normal", True, cfg.init_std, True))
                 if cfg.bias and cfg.cross_attn:
                     specs.append(ParamSpec("output.bias", (cfg.vocab_padded,), "zeros", False))
         self.arena = ParamArena(specs, self.device, dtype=dtype, seed=seed, init=init)
@@ -528,6 +557,9 @@ class NativeModel:
     # ------------------------------------------------------------------ helpers
     def head_weight(self):
         return self.arena.w("tok_embeddings.weight" if self.cfg.tie_embeddings else "output.weight")
+
+    def head_weight_t(self):
+        return self.arena.wt("tok_embeddings.weight" if self.cfg.tie_embeddings else "output.weight")
 
     def head_grad(self):
         return self.arena.g("tok_embeddings.weight" if self.cfg.tie_embeddings else "output.weight")
@@ -575,7 +607,7 @@ class NativeModel:
             dl = ctx.misc.pop("dlogits")
             hn = ctx.misc.pop("hn")
             W = self.head_weight()
-            dhn = ops.linear_dx(dl, W)
+            dhn = ops.linear_dx(dl, W, wt=self.head_weight_t())
             jobs = [lambda dl=dl, hn=hn: ops.linear_dw(dl, hn, self.head_grad())]
             if self.arena.has("output.bias"):
                 jobs.append(lambda dl=dl: ops.colsum(dl, self.arena.g("output.bias")))

@@ -40,6 +40,8 @@ def gemm_cases(T=16384):
         out.append((f"fwd_{name}", "fwd", T, N, K))
         out.append((f"dx_{name}", "dx", T, K, N))
         out.append((f"dw_{name}", "dw", N, K, T))
+    out.append(("fwdgelu_fc1", "fwdgelu", T, f, d))
+    out.append(("dxdgelu_fc2", "dxdgelu", T, f, d))
     for name, N, K in [("l_qkv", 6144, 4096), ("l_w13", 28672, 4096), ("l_w2", 4096, 14336)]:
         out.append((f"fwd_{name}", "fwd", T, N, K))
         out.append((f"dw_{name}", "dw", N, K, T))
@@ -64,6 +66,21 @@ def main():
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             ours = lambda: _k._gemm(x, w, y)
             lib = lambda: torch.mm(x, w.t(), out=y)
+        elif kind == "fwdgelu":  # a = x w^T + b; y = gelu(a)   (fused epilogue vs addmm + gelu)
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * K ** -0.5
+            b = torch.randn(N, device=dev, dtype=torch.bfloat16)
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            aux = torch.empty_like(y)
+            ours = lambda: _k._gemm(x, w, y, bias=b, aux=aux, epi=_k.EPI_BIAS_GELU)
+            lib = lambda: F.gelu(torch.addmm(b, x, w.t(), out=aux), approximate="tanh")
+        elif kind == "dxdgelu":  # da = (dy W) * gelu'(a)
+            dy = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
+            wt = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * K ** -0.5
+            aux = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            ours = lambda: _k._gemm(dy, wt, y, aux=aux, epi=_k.EPI_DGELU)
+            lib = lambda: torch.mm(dy, wt.t(), out=y).mul_(aux)
         elif kind == "dx":  # dx[M,N] = dy[M,K] w[K,N]
             dy = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             w = torch.randn(K, N, device=dev, dtype=torch.bfloat16) * K ** -0.5
