@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--dp", type=int, default=1)
     ap.add_argument("--v", type=int, default=None, help="virtual stages per rank (interleaved)")
     ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--no-split-head", action="store_true",
+                    help="keep the LM head on the last stage (default with PP>1: distributed head)")
     ap.add_argument("--no-bubble", action="store_true", help="skip the profiled bubble-measurement step")
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the profiled step (per rank)")
     return ap.parse_args()
@@ -75,7 +77,8 @@ def main():
     m = a.microbatches if a.microbatches is not None else max(2, 2 * pp)
     cfg = NativeConfig.by_name(a.model)
     trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m,
-                              mbs=a.mbs, seq_len=a.seq, v=a.v, device=device, recompute=a.recompute, seed=0)
+                              mbs=a.mbs, seq_len=a.seq, v=a.v, device=device, recompute=a.recompute, seed=0,
+                              split_head=False if a.no_split_head else None)
     gb = dp * m * a.mbs
     g = torch.Generator(device=device).manual_seed(1234 + trainer.mesh.dp_rank)
     tokens = torch.randint(0, cfg.vocab_size, (m * a.mbs, a.seq), device=device, generator=g)
@@ -140,7 +143,9 @@ def main():
         "config": {"model": a.model, "params": cfg.n_params(), "global_batch": gb, "seq_len": a.seq,
                    "micro_batch": a.mbs, "microbatches": m, "schedule": trainer.schedule, "v": trainer.v,
                    "parallelism": f"pp{pp}" + (f"_dp{dp}" if dp > 1 else ""),
-                   "layer_split": trainer.layer_ranges, "optimizer": "AdamW(fused, clip 1.0)"},
+                   "layer_split": trainer.layer_ranges, "optimizer": "AdamW(fused, clip 1.0)",
+                   "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
+                   else "last stage"},
     }
     if loss_val is not None:
         out["last_loss"] = round(loss_val, 4)

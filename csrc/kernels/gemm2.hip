@@ -334,7 +334,7 @@ struct Cfg {
 };
 static const Cfg CFGS[4] = {{256, 256, 1.00f}, {256, 192, 0.96f}, {256, 128, 0.90f}, {128, 128, 0.72f}};
 
-static int choose(int M, int N, int K, bool acc, int* split_out) {
+static int choose(int M, int N, int K, bool acc, bool outer, int* split_out) {
   // minimise modelled time = (#rounds of CU slots) x (per-item k-loop + epilogue) / tile efficiency;
   // padded tiles are charged like real ones, so quantisation and padding waste both count
   int best = 3, best_split = 1;
@@ -342,7 +342,7 @@ static int choose(int M, int N, int K, bool acc, int* split_out) {
   const int kt = K / BK;
   for (int c = 0; c < 4; ++c) {
     const int slots = c == 3 ? 512 : 256;  // 128x128 tiles fit two workgroups per CU
-    if (acc && CFGS[c].bn == 192) continue;  // outer-contig images need power-of-two widths
+    if (outer && CFGS[c].bn == 192) continue;  // outer-contig images need power-of-two widths
     const int tiles = ((M + CFGS[c].bm - 1) / CFGS[c].bm) * ((N + CFGS[c].bn - 1) / CFGS[c].bn);
     const float area = (float)(CFGS[c].bm * CFGS[c].bn) / (256.f * 256.f) * (c == 3 ? 2.f : 1.f);
     const int max_split = acc ? (kt / 4 < 32 ? kt / 4 : 32) : 1;
@@ -386,7 +386,7 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
                         hipStream_t st) {
   if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
   int split = 1;
-  int cfg = choose(M, N, K, c_f32_accum != 0, &split);
+  int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
   if (force_cfg >= 0 && force_cfg < 4) cfg = force_cfg;
   if ((transA || transB) && cfg == 1) cfg = 2;
   if (!c_f32_accum) split = 1;
@@ -403,6 +403,7 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   MP_G(false, false, EPI_DGELU, false)
   MP_G(false, false, EPI_DRELU, false)
   MP_G(true, true, EPI_NONE, true)
+  MP_G(false, false, EPI_NONE, true)
 #undef MP_G
   return -2;
 }

@@ -19,12 +19,13 @@ import torch.distributed as dist
 
 from . import ops
 from .models.config import NativeConfig
-from .models.native import NativeModel, ParamArena, balanced_layer_ranges
+from .models.native import HeadShard, NativeModel, ParamArena, balanced_layer_ranges, stage_cost_model
 from .models.stage import NativeStage
 from .parallel.comm import P2P
+from .parallel.headsplit import HeadPlan, head_token_split, plan_head_schedule
 from .parallel.mesh import Mesh, build_mesh
 from .parallel.runtime import PipelineRuntime
-from .parallel.schedules import SCHEDULES, canonical_name, rank_stages
+from .parallel.schedules import SCHEDULES, canonical_name, generate, rank_stages, stage_to_rank
 
 
 class FlatAdamW:
@@ -34,8 +35,11 @@ class FlatAdamW:
     across the pipeline group (a 4-byte all-reduce) -- no host synchronisation."""
 
     def __init__(self, arenas: List[ParamArena], lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
-                 weight_decay: float = 0.1, max_grad_norm: float = 1.0, pp_group=None):
+                 weight_decay: float = 0.1, max_grad_norm: float = 1.0, pp_group=None, norm_skip=()):
         self.arenas = arenas
+        # arenas replicated across the pipeline group (distributed head) count in the
+        # global grad norm on one rank only
+        self.norm_skip = set(norm_skip)
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_norm = max_grad_norm
         self.pp_group = pp_group
@@ -51,8 +55,9 @@ class FlatAdamW:
         use_clip = self.max_norm and self.max_norm > 0
         if use_clip:
             self.sumsq.zero_()
-            for a in self.arenas:
-                ops.sumsq(a.grad, self.sumsq)
+            for i, a in enumerate(self.arenas):
+                if i not in self.norm_skip:
+                    ops.sumsq(a.grad, self.sumsq)
             if self.pp_group is not None and dist.get_world_size(self.pp_group) > 1:
                 dist.all_reduce(self.sumsq, group=self.pp_group)
         for a, m, v in zip(self.arenas, self.m, self.v):
@@ -77,7 +82,8 @@ class PipelineTrainer:
                  n_microbatches: int = 8, mbs: int = 8, seq_len: int = 1024, v: Optional[int] = None,
                  device=None, lr: float = 3e-4, weight_decay: float = 0.1, max_grad_norm: float = 1.0,
                  recompute: bool = False, profile: bool = False, seed: int = 0, style: str = "loop",
-                 mesh: Optional[Mesh] = None, layer_ranges=None, dtype=torch.bfloat16):
+                 mesh: Optional[Mesh] = None, layer_ranges=None, dtype=torch.bfloat16,
+                 split_head: Optional[bool] = None, head_align: Optional[int] = None):
         self.cfg = cfg
         self.schedule = canonical_name(schedule)
         if v is None:
@@ -92,23 +98,51 @@ class PipelineTrainer:
         self.device = torch.device(device)
         self.mesh = mesh if mesh is not None else build_mesh(pp, dp, self.device)
         num_stages = pp * v
+        # distributed LM head (parallel/headsplit.py): default on whenever there is a pipeline
+        self.split_head = pp > 1 if split_head is None else (bool(split_head) and pp > 1)
         if layer_ranges is None:
-            layer_ranges = balanced_layer_ranges(cfg, num_stages, seq_len)
+            layer_ranges = balanced_layer_ranges(cfg, num_stages, seq_len, head_on_last=not self.split_head)
         self.layer_ranges = layer_ranges
         my_stages = rank_stages(self.mesh.pp_rank, pp, v, style)
-        tied_pp = cfg.tie_embeddings and num_stages > 1
+        tied_pp = cfg.tie_embeddings and num_stages > 1 and not self.split_head
+        self.head: Optional[HeadShard] = None
+        orders = head_plan = head_costs = stage_costs = None
+        self.head_chunks = None
+        if self.split_head:
+            self.head = HeadShard(cfg, self.device, seed=seed, dtype=dtype)
+            lc, head_units, ec = stage_cost_model(cfg, seq_len)
+            stage_costs = [(r1 - r0) * lc + (ec if s == 0 else 0.0) + (0.1 if s == num_stages - 1 else 0.0)
+                           for s, (r0, r1) in enumerate(layer_ranges)]
+            rank_load = [sum(stage_costs[s] for s in range(num_stages) if stage_to_rank(s, pp, style) == r)
+                         for r in range(pp)]
+            T = mbs * seq_len
+            align = head_align or next(a for a in (256, 128, 64, 32, 16, 8, 1) if T % a == 0)
+            chunks = head_token_split(T, rank_load, head_units, align=align)
+            head_costs = {r: 3.0 * head_units * chunks[r] / T for r in range(pp) if chunks[r] > 0}
+            base = generate(self.schedule, pp, n_microbatches, v, style)
+            orders, self.head_lag, self.planned_makespan = plan_head_schedule(base, pp, v, style, head_costs,
+                                                                              stage_costs)
+            head_plan = HeadPlan(chunks, cfg.d_model, runner=self.head.run, dtype=dtype)
+            self.head_chunks = chunks
         self.stages: List[NativeStage] = []
         for s in my_stages:
             model = NativeModel(cfg, s, num_stages, self.device, layer_range=layer_ranges[s], seed=seed,
-                                recompute=recompute, mbs=mbs, seq_len=seq_len, dtype=dtype)
+                                recompute=recompute, mbs=mbs, seq_len=seq_len, dtype=dtype, head=self.head)
             egroup = self.mesh.embed_group if (tied_pp and (s == 0 or s == num_stages - 1)) else None
             self.stages.append(NativeStage(model, mbs, seq_len, dp_group=self.mesh.dp_group, embed_group=egroup,
                                            seed=seed + 1000 * self.mesh.dp_rank))
         p2p = P2P(self.mesh.pp_group, self.mesh.pipe_ranks, self.device)
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
-                                       scale_grads=True, style=style, profile=profile)
-        self.optimizer = FlatAdamW([st.arena for st in self.stages], lr=lr, weight_decay=weight_decay,
-                                   max_grad_norm=max_grad_norm, pp_group=self.mesh.pp_group if pp > 1 else None)
+                                       scale_grads=True, style=style, profile=profile, orders=orders,
+                                       head=head_plan, head_costs=head_costs, stage_costs=stage_costs)
+        arenas = [st.arena for st in self.stages]
+        norm_skip = []
+        if self.head is not None:
+            arenas.append(self.head.arena)
+            if self.mesh.pp_rank != 0:
+                norm_skip.append(len(arenas) - 1)
+        self.optimizer = FlatAdamW(arenas, lr=lr, weight_decay=weight_decay, max_grad_norm=max_grad_norm,
+                                   pp_group=self.mesh.pp_group if pp > 1 else None, norm_skip=norm_skip)
         self.last_losses: List[torch.Tensor] = []
 
     @property
@@ -117,7 +151,8 @@ class PipelineTrainer:
 
     @property
     def is_last(self) -> bool:
-        return any(st.is_last for st in self.stages)
+        """Holds the loss (every rank with a distributed head)."""
+        return self.head is not None or any(st.is_last for st in self.stages)
 
     def num_params_local(self) -> int:
         return sum(st.arena.numel for st in self.stages)
@@ -132,6 +167,15 @@ class PipelineTrainer:
         tg = list(torch.tensor_split(targets, self.m, dim=0)) if self.is_last else None
         losses: List[torch.Tensor] = []
         self.runtime.step(inputs, tg, losses, return_outputs=False)
+        if self.head is not None:
+            # replicated head: one gradient all-reduce over every rank (pipeline x DP)
+            if dist.is_initialized() and dist.get_world_size() > 1:
+                dist.all_reduce(self.head.arena.grad)
+            parts = torch.stack([self.runtime.head_losses.get(i, torch.zeros((), device=self.device))
+                                 for i in range(self.m)]).float()
+            if self.mesh.pp_group is not None and dist.get_world_size(self.mesh.pp_group) > 1:
+                dist.all_reduce(parts, group=self.mesh.pp_group)
+            losses = list(parts / (self.mbs * self.S))
         self.optimizer.step(lr)
         self.last_losses = losses
         if losses:
@@ -146,4 +190,6 @@ class PipelineTrainer:
         sd = {}
         for st in self.stages:
             sd.update(st.arena.state_dict())
+        if self.head is not None:
+            sd.update(self.head.arena.state_dict())
         return sd

@@ -472,8 +472,17 @@ class Block:
 # ======================================================================================
 
 
+def stage_cost_model(cfg: NativeConfig, seq_len: int = 1024) -> Tuple[float, float, float]:
+    """(layer, head, embedding) costs in layer units (forward FLOPs; the head includes
+    its CE / final-norm overhead)."""
+    d = cfg.d_model
+    layer_cost = (cfg.flops_per_token(seq_len) / 3.0 - 2 * d * cfg.vocab_size) / cfg.n_layers
+    head_cost = (2 * d * cfg.vocab_padded) / layer_cost + 0.3
+    return 1.0, head_cost, 0.1
+
+
 def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 1024,
-                          reference_rule: bool = False) -> List[Tuple[int, int]]:
+                          reference_rule: bool = False, head_on_last: bool = True) -> List[Tuple[int, int]]:
     """Layer ranges per stage.
 
     ``reference_rule``: ``L // num_stages`` per stage, remainder on the last stage
@@ -485,10 +494,9 @@ def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 102
     if reference_rule or num_stages == 1:
         per = L // num_stages
         return [(s * per, (s + 1) * per if s < num_stages - 1 else L) for s in range(num_stages)]
-    d = cfg.d_model
-    layer_cost = (cfg.flops_per_token(seq_len) / 3.0 - 2 * d * cfg.vocab_size) / L
-    head_cost = (2 * d * cfg.vocab_padded) / layer_cost + 0.3  # + CE / final norm, in layer units
-    emb_cost = 0.1
+    _, head_cost, emb_cost = stage_cost_model(cfg, seq_len)
+    if not head_on_last:  # distributed head (parallel/headsplit.py): only the final norm stays
+        head_cost = 0.1
     P = num_stages
     best = None
     for k_last in range(0, L + 1):
@@ -508,18 +516,63 @@ def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 102
     return out
 
 
+def head_param_specs(cfg: NativeConfig) -> List[ParamSpec]:
+    d = cfg.d_model
+    if cfg.tie_embeddings:
+        return [ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False, cfg.init_std, True)]
+    out = [ParamSpec("output.weight", (cfg.vocab_padded, d), "normal", True, cfg.init_std, True)]
+    if cfg.bias and cfg.cross_attn:
+        out.append(ParamSpec("output.bias", (cfg.vocab_padded,), "zeros", False))
+    return out
+
+
+class HeadShard:
+    """LM head + loss replicated on every pipeline rank (distributed head,
+    parallel/headsplit.py).  Runs one token chunk of a microbatch: logits, fused
+    softmax-CE fwd+bwd, input grad (returned to the last stage) and weight grad
+    (accumulated locally, all-reduced once per step).  With tied embeddings the
+    first stage's embedding reads/updates this same arena."""
+
+    def __init__(self, cfg: NativeConfig, device, seed: int = 0, dtype=torch.bfloat16, init: bool = True):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.arena = ParamArena(head_param_specs(cfg), self.device, dtype=dtype, seed=seed, init=init)
+        self.wname = "tok_embeddings.weight" if cfg.tie_embeddings else "output.weight"
+
+    def weight(self):
+        return self.arena.w(self.wname)
+
+    def run(self, h: torch.Tensor, target: torch.Tensor, dh_out: torch.Tensor, grad_scale: float) -> torch.Tensor:
+        """h [Tc, D] final-norm output rows, target [Tc] ids; writes dL/dh into
+        ``dh_out`` and returns the chunk's summed token loss (f32 scalar tensor)."""
+        A = self.arena
+        W = self.weight()
+        hb = A.w("output.bias") if A.has("output.bias") else None
+        logits, _ = ops.linear(h, W, hb)
+        row_loss = ops.xent_fwd_bwd(logits, target.reshape(-1), self.cfg.vocab_size, grad_scale=grad_scale)
+        ops.linear_dx(logits, W, out=dh_out, wt=A.wt(self.wname))
+        ops.linear_dw(logits, h, A.g(self.wname))
+        if hb is not None:
+            ops.colsum(logits, A.g("output.bias"))
+        return row_loss.sum()
+
+
 class NativeModel:
     """The part of a model that one pipeline stage owns (embedding on stage 0, head +
     loss on the last stage), with explicit fwd/bwd per microbatch."""
 
     def __init__(self, cfg: NativeConfig, stage_index: int, num_stages: int, device, layer_range=None,
                  seed: int = 0, recompute: bool = False, mbs: int = 1, seq_len: int = 1024, init: bool = True,
-                 dtype=torch.bfloat16):
+                 dtype=torch.bfloat16, head: Optional[HeadShard] = None):
         self.cfg = cfg
         self.stage_index = stage_index
         self.num_stages = num_stages
         self.first = stage_index == 0
         self.last = stage_index == num_stages - 1
+        # distributed head: the last stage stops at the final norm, the (tied) vocab
+        # matrix lives in the shared HeadShard arena
+        self.head = head
+        self.split_head = head is not None
         self.device = torch.device(device)
         self.recompute = recompute
         if layer_range is None:
@@ -528,8 +581,9 @@ class NativeModel:
         specs: List[ParamSpec] = []
         d = cfg.d_model
         if self.first:
-            specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False, cfg.init_std,
-                                   cfg.tie_embeddings and self.last))
+            if not (self.split_head and cfg.tie_embeddings):
+                specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False,
+                                       cfg.init_std, cfg.tie_embeddings and self.last))
             if cfg.pos == "learned":
                 specs.append(ParamSpec("pos_embeddings.weight", (cfg.max_seq_len, d), "normal", False, 0.01))
         for i in range(*layer_range):
@@ -539,7 +593,9 @@ class NativeModel:
                 specs.append(ParamSpec("norm.weight", (d,), "ones", False))
                 if cfg.norm == "layernorm":
                     specs.append(ParamSpec("norm.bias", (d,), "zeros", False))
-            if cfg.tie_embeddings:
+            if self.split_head:
+                pass
+            elif cfg.tie_embeddings:
                 if not self.first:  # tied copy on the last stage, kept in sync by the embed group
                     specs.append(ParamSpec("tok_embeddings.weight", (cfg.vocab_padded, d), "normal", False,
                                            cfg.init_std, True))
@@ -555,6 +611,11 @@ class NativeModel:
         self.defer_w: Dict[int, list] = {}
 
     # ------------------------------------------------------------------ helpers
+    def _emb_arena(self) -> ParamArena:
+        if self.split_head and self.cfg.tie_embeddings:
+            return self.head.arena
+        return self.arena
+
     def head_weight(self):
         return self.arena.w("tok_embeddings.weight" if self.cfg.tie_embeddings else "output.weight")
 
@@ -572,7 +633,7 @@ class NativeModel:
         cfg = self.cfg
         if self.first:
             tokens = x.reshape(-1)
-            h = ops.embed_fwd(tokens, self.arena.w("tok_embeddings.weight"),
+            h = ops.embed_fwd(tokens, self._emb_arena().w("tok_embeddings.weight"),
                               self.arena.w("pos_embeddings.weight") if cfg.pos == "learned" else None, S)
             ctx.misc["tokens"] = tokens
         else:
@@ -589,6 +650,8 @@ class NativeModel:
             ctx.misc.update(hpre=h, mu=mu, rs=rs)
         else:
             hn = h
+        if self.split_head:  # the head runs as distributed chunks (HeadShard.run)
+            return hn
         hb = self.arena.w("output.bias") if self.arena.has("output.bias") else None
         logits, _ = ops.linear(hn, self.head_weight(), hb)
         T = hn.shape[0]
@@ -603,7 +666,13 @@ class NativeModel:
     def backward(self, dy: Optional[torch.Tensor], ctx: MBContext, B: int, S: int, weight_grads: bool = True):
         cfg = self.cfg
         defer: List = []
-        if self.last:
+        if self.last and self.split_head:
+            # dy = dL/d(final-norm output), gathered from the head chunks
+            if cfg.final_norm:
+                dy, _ = ops.norm_bwd(dy, ctx.misc.pop("hpre"), self.arena.w("norm.weight"), ctx.misc.pop("mu"),
+                                     ctx.misc.pop("rs"), kind=cfg.norm, dw=self.arena.g("norm.weight"),
+                                     dbias=self.arena.g("norm.bias") if self.arena.has("norm.bias") else None)
+        elif self.last:
             dl = ctx.misc.pop("dlogits")
             hn = ctx.misc.pop("hn")
             W = self.head_weight()
@@ -626,8 +695,9 @@ class NativeModel:
             dy = blk.backward(dy, B, S, ctx, weight_grads=weight_grads, defer=defer)
         if self.first:
             tokens = ctx.misc.pop("tokens")
+            ea = self._emb_arena()
             jobs = [lambda dy=dy, tokens=tokens: ops.embed_bwd(
-                tokens, dy, self.arena.g("tok_embeddings.weight"),
+                tokens, dy, ea.g("tok_embeddings.weight"),
                 self.arena.g("pos_embeddings.weight") if cfg.pos == "learned" else None, S)]
             if weight_grads:
                 jobs[0]()

@@ -40,7 +40,11 @@ class NativeStage(StageBase):
             self.input_specs = [((mbs, seq_len), torch.int64)]
         else:
             self.input_specs = [((T, D), model.arena.dtype)]
-        self.output_specs = [((T, D), model.arena.dtype)] if not self.is_last else [((), torch.float32)]
+        self.split_head = model.split_head
+        if self.is_last and not self.split_head:
+            self.output_specs = [((), torch.float32)]
+        else:  # hidden states (the last stage's final-norm output with a distributed head)
+            self.output_specs = [((T, D), model.arena.dtype)]
         self._ctx = {}
 
     @property
@@ -57,21 +61,26 @@ class NativeStage(StageBase):
         out = self.model.forward(x, ctx, self.mbs, self.S, target=target if self.is_last else None,
                                  loss_scale=loss_scale)
         self._ctx[mb] = ctx
-        if self.is_last:
+        if self.is_last and not self.split_head:
             if target is None:
                 return (out,), None
             return (out.detach(),), out
         return (out,), None
 
+    def _dy(self, grad_outputs):
+        if (self.is_last and not self.split_head) or not grad_outputs:
+            return None
+        return grad_outputs[0]
+
     def backward_mb(self, mb, grad_outputs):
         ctx = self._ctx.pop(mb)
-        dy = None if (self.is_last or not grad_outputs) else grad_outputs[0]
+        dy = self._dy(grad_outputs)
         dx = self.model.backward(dy, ctx, self.mbs, self.S, weight_grads=True)
         return (dx,) if dx is not None else ()
 
     def backward_input_mb(self, mb, grad_outputs):
         ctx = self._ctx.pop(mb)
-        dy = None if (self.is_last or not grad_outputs) else grad_outputs[0]
+        dy = self._dy(grad_outputs)
         dx = self.model.backward(dy, ctx, self.mbs, self.S, weight_grads=False)
         return (dx,) if dx is not None else ()
 

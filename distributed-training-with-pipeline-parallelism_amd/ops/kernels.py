@@ -309,6 +309,13 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
     if out is None:
         out = torch.empty(T, K, device=dy.device, dtype=dy.dtype)
     if _gpu(dy) and wt is not None and GEMM_BACKEND != "blas":
+        if act == "none" and residual is None and (T // 256) * (K // 192) < 128 and N >= 4096:
+            # few output tiles, long reduction (a distributed-head chunk: [Tc, D] = dl[Tc, V] W):
+            # split-K into an f32 buffer fills the chip; one cast pass at the end
+            acc = torch.zeros(T, K, device=dy.device, dtype=torch.float32)
+            _gemm(dy, wt, acc, accum=True)
+            out.copy_(acc)
+            return out
         if act != "none":
             _gemm(dy, wt, out, aux=act_input, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU)
         elif residual is not None:

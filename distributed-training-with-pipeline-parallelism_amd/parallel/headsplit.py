@@ -1,0 +1,207 @@
+"""Distributed LM head: spread the vocabulary projection + loss over every pipeline rank.
+
+With a 50k vocabulary the head of GPT-2 small costs as much as ~5 transformer layers,
+so at PP=8 the last stage alone would bound the pipeline to ~40 % of ideal
+(12 layers + head cannot be split evenly when the head is one indivisible block).
+The reference has no answer to this (its last stage simply owns the head,
+helper:23-55 / helper:70-75); here the head becomes a set of ``H`` actions:
+
+* the last stage's forward stops at the final norm; its output rows (tokens) are cut
+  into per-rank chunks and sent to every rank (``SEND_H``);
+* rank r runs ``rH m`` on its chunk: logits = h W^T, fused softmax-CE forward+backward,
+  dh = dlogits W, dW += dlogits^T h, and sends dh back (``SEND_D``); softmax is over the
+  full vocabulary, so chunks need no cross-rank statistics;
+* the last stage's backward starts from the gathered dh.
+
+Every rank holds the (tied) head weight; its gradient is all-reduced once per step and
+the replicated AdamW update keeps the copies bit-identical.  Chunk sizes are chosen by
+water-filling so that (stage layers + head chunk) is level across ranks, and the ``H``
+actions are placed into each rank's compute order by a list-scheduling simulation
+(``insert_head_ops``), after which the normal lowering/deadlock check applies.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
+
+from .ir import Action, Op
+from .schedules import stage_to_rank
+from .simulate import DEFAULT_COSTS, action_rank, in_messages, simulate, uses_split_backward
+
+
+def head_token_split(T: int, rank_load: Sequence[float], head_load: float, align: int = 128) -> List[int]:
+    """Token chunk per rank so that ``rank_load[r] + head_load * tokens_r / T`` is as
+    level as possible (water-filling), in multiples of ``align`` tokens, summing to T."""
+    P = len(rank_load)
+    units = T // align
+    if units * align != T:
+        raise ValueError(f"{T} tokens are not a multiple of the chunk alignment {align}")
+    per_unit = head_load / units
+    # water level L: sum_r max(0, L - load_r) = head_load
+    loads = sorted(rank_load)
+    level = loads[0]
+    rem = head_load
+    for i in range(P):
+        nxt = loads[i + 1] if i + 1 < P else float("inf")
+        cap = (nxt - loads[i]) * (i + 1)
+        if rem <= cap:
+            level = loads[i] + rem / (i + 1)
+            break
+        rem -= cap
+    share = [max(0.0, level - x) / per_unit for x in rank_load]
+    cnt = [int(s) for s in share]
+    # largest remainders get the leftover units
+    left = units - sum(cnt)
+    order = sorted(range(P), key=lambda r: -(share[r] - cnt[r]))
+    for r in order[:left]:
+        cnt[r] += 1
+    return [c * align for c in cnt]
+
+
+def _lag_last_stage(order: List[Action], last: int, lag: int) -> List[Action]:
+    """Delay the last stage's backward (B/I/W) of microbatch i until after its forward
+    of i+lag (the slack that lets the other ranks fit their head chunks in).  A stable
+    re-sort: relative orders of forwards and of backwards are unchanged."""
+    if lag <= 0:
+        return list(order)
+    fpos = {a.mb: i for i, a in enumerate(order) if a.stage == last and a.op == Op.F}
+    if not fpos:
+        return list(order)
+    flast = max(fpos.values())
+    keys = []
+    for i, a in enumerate(order):
+        k = float(i)
+        if a.stage == last and a.op in (Op.B, Op.I, Op.W):
+            k = max(k, fpos.get(a.mb + lag, flast) + 0.5)
+        keys.append(k)
+    return [a for _, a in sorted(zip(keys, order), key=lambda t: t[0])]
+
+
+def insert_head_ops(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int, style: str,
+                    head_costs: Dict[int, float], stage_costs: Optional[Sequence[float]] = None,
+                    lag: int = 1, comm: float = 0.05, costs: Optional[Dict[Op, float]] = None,
+                    policy: str = "head_first") -> Dict[int, List[Action]]:
+    """Insert ``rH m`` actions (ranks with a non-zero ``head_costs[r]``) into per-rank
+    compute orders by list scheduling: whenever a rank is free it runs whichever is
+    startable first -- its next scheduled action or its next head chunk (ties go to
+    the head chunk, which the last stage is waiting for)."""
+    costs = dict(DEFAULT_COSTS, **(costs or {}))
+    S = pp * v
+    s2r = [stage_to_rank(s, pp, style) for s in range(S)]
+    base = {r: [a for a in orders.get(r, []) if a is not None and a.op.is_compute] for r in range(pp)}
+    split = uses_split_backward(base)
+    last_rank = s2r[S - 1]
+    if v == 1 and lag > 0:
+        # every stage gets `lag` more warmup forwards (delaying only the last stage's
+        # backwards would starve the upstream ranks' steady state)
+        for r in range(pp):
+            base[r] = _lag_last_stage(base[r], r, lag)
+    head = tuple(r for r in range(pp) if head_costs.get(r, 0.0) > 0.0)
+    mbs = sorted({a.mb for a in base[last_rank] if a.op == Op.F and a.stage == S - 1})
+
+    def cost(a: Action) -> float:
+        if a.op == Op.H:
+            return costs[Op.H] * head_costs[a.stage]
+        return costs[a.op] * (stage_costs[a.stage] if stage_costs is not None else 1.0)
+
+    ptr = {r: 0 for r in range(pp)}
+    hptr = {r: 0 for r in range(pp)}
+    avail = {r: 0.0 for r in range(pp)}
+    end: Dict[Action, float] = {}
+    out: Dict[int, List[Action]] = {r: [] for r in range(pp)}
+    total = sum(len(b) for b in base.values()) + len(head) * len(mbs)
+
+    def ready_time(a: Action, r: int) -> Optional[float]:
+        t = avail[r]
+        for d, _ in in_messages(a, S, split, head):
+            if d not in end:
+                return None
+            lat = comm if action_rank(d, s2r) != r else 0.0
+            t = max(t, end[d] + lat)
+        return t
+
+    done = 0
+    while done < total:
+        best = None  # (start, tie, rank, action, is_head)
+        for r in range(pp):
+            cands = []
+            if r in head and hptr[r] < len(mbs):
+                h = Action(r, Op.H, mbs[hptr[r]])
+                t = ready_time(h, r)
+                if t is not None:
+                    cands.append((t, 0, r, h, True))
+            if ptr[r] < len(base[r]):
+                a = base[r][ptr[r]]
+                t = ready_time(a, r)
+                if t is not None:
+                    cands.append((t, 1, r, a, False))
+            if policy == "fill" and len(cands) == 2 and cands[1][0] <= avail[r] + 1e-9:
+                cands = cands[1:]   # the scheduled action can start now: head chunks only fill gaps
+            elif policy == "fill" and len(cands) == 2:
+                cands = [cands[0]] if cands[0][0] <= cands[1][0] else [cands[1]]
+            for c in cands:
+                if best is None or (c[0], c[1], c[2]) < (best[0], best[1], best[2]):
+                    best = c
+        if best is None:
+            stuck = {r: str(base[r][ptr[r]]) for r in range(pp) if ptr[r] < len(base[r])}
+            raise RuntimeError(f"head placement deadlocks; stuck at {stuck}")
+        t, _, r, a, is_head = best
+        end[a] = t + cost(a)
+        avail[r] = end[a]
+        out[r].append(a)
+        if is_head:
+            hptr[r] += 1
+        else:
+            ptr[r] += 1
+        done += 1
+    return out
+
+
+def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int, style: str,
+                       head_costs: Dict[int, float], stage_costs: Optional[Sequence[float]] = None,
+                       comm: float = 0.05, lags: Sequence[int] = (0, 1, 2),
+                       policies: Sequence[str] = ("head_first", "fill")
+                       ) -> Tuple[Dict[int, List[Action]], int, float]:
+    """Best of ``insert_head_ops`` over the candidate last-stage lags (simulated
+    makespan).  Returns (orders, lag, makespan)."""
+    best = None
+    for pol in policies:
+        for lag in lags:
+            try:
+                o = insert_head_ops(orders, pp, v, style, head_costs, stage_costs, lag=lag, comm=comm, policy=pol)
+                res = simulate(o, pp, v, style, comm_latency=comm, stage_costs=stage_costs, head_costs=head_costs)
+            except RuntimeError:
+                continue
+            if best is None or res.makespan < best[2] - 1e-9:
+                best = (o, lag, res.makespan)
+    if best is None:
+        raise RuntimeError("no feasible head placement")
+    return best
+
+
+@dataclass
+class HeadPlan:
+    """Runtime description of a distributed head.
+
+    ``chunks[r]``: tokens of every microbatch that rank r processes (rows
+    ``offsets[r] : offsets[r] + chunks[r]`` of the last stage's [T, D] output);
+    ``runner(h, target, dh_out, grad_scale) -> loss_sum`` runs this rank's chunk."""
+    chunks: List[int]
+    d_model: int
+    runner: Optional[Callable] = None
+    dtype: object = None
+    offsets: List[int] = field(default_factory=list)
+
+    def __post_init__(self):
+        self.offsets = [sum(self.chunks[:r]) for r in range(len(self.chunks))]
+
+    @property
+    def tokens(self) -> int:
+        return sum(self.chunks)
+
+    @property
+    def ranks(self) -> Tuple[int, ...]:
+        return tuple(r for r, c in enumerate(self.chunks) if c > 0)
+
+    def rows(self, r: int) -> slice:
+        return slice(self.offsets[r], self.offsets[r] + self.chunks[r])

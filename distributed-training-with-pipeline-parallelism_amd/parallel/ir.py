@@ -31,25 +31,37 @@ class Op(enum.Enum):
     SEND_B = "SEND_B"
     RECV_B = "RECV_B"
     REDUCE_GRAD = "REDUCE_GRAD"
+    # distributed LM head (see :mod:`.headsplit`): ``rH m`` = rank r's token chunk of
+    # microbatch m through the head + loss (fwd and bwd fused); the last stage sends the
+    # chunk's final hidden states (SEND_H) and receives its input gradient (RECV_D)
+    H = "H"
+    SEND_H = "SEND_H"
+    RECV_H = "RECV_H"
+    SEND_D = "SEND_D"
+    RECV_D = "RECV_D"
 
     @property
     def is_compute(self) -> bool:
-        return self in (Op.F, Op.B, Op.I, Op.W)
+        return self in (Op.F, Op.B, Op.I, Op.W, Op.H)
 
     @property
     def is_comm(self) -> bool:
-        return self in (Op.SEND_F, Op.RECV_F, Op.SEND_B, Op.RECV_B)
+        return self.is_send or self.is_recv
 
     @property
     def is_send(self) -> bool:
-        return self in (Op.SEND_F, Op.SEND_B)
+        return self in (Op.SEND_F, Op.SEND_B, Op.SEND_H, Op.SEND_D)
 
     @property
     def is_recv(self) -> bool:
-        return self in (Op.RECV_F, Op.RECV_B)
+        return self in (Op.RECV_F, Op.RECV_B, Op.RECV_H, Op.RECV_D)
 
 
-_ACTION_RE = re.compile(r"^(\d+)(F|B|I|W|SEND_F|RECV_F|SEND_B|RECV_B|REDUCE_GRAD)(\d*)$")
+# message kind -> (send op, recv op)
+MSG_OPS = {"F": (Op.SEND_F, Op.RECV_F), "B": (Op.SEND_B, Op.RECV_B), "H": (Op.SEND_H, Op.RECV_H),
+           "D": (Op.SEND_D, Op.RECV_D)}
+
+_ACTION_RE = re.compile(r"^(\d+)(SEND_F|RECV_F|SEND_B|RECV_B|SEND_H|RECV_H|SEND_D|RECV_D|REDUCE_GRAD|F|B|I|W|H)(\d*)$")
 
 
 @dataclass(frozen=True)

@@ -27,50 +27,49 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Sequence, Tuple
 
-from .ir import Action, CommGroup, CommOp, Entry, Op
+from .ir import MSG_OPS, Action, CommGroup, CommOp, Entry, Op
 from .schedules import stage_to_rank
-from .simulate import check_lowered, simulate, uses_split_backward
+from .simulate import action_rank, check_lowered, head_ranks_of, in_messages, simulate, uses_split_backward
 
 
 @dataclass
 class Message:
-    key: tuple            # (kind 'F'|'B', dst_stage, mb)
+    key: tuple            # (kind 'F'|'B'|'H'|'D', dst stage (or head rank), mb)
     src: int
     dst: int
     t: float
     producer: Action
-    consumer_stage: int
+    consumer: Action
 
     def order_key(self):
         kind, stage, mb = self.key
         return (self.t, self.src, self.dst, kind, stage, mb)
 
 
-def _producers(a: Action, S: int, split: bool):
-    """Messages (kind, dst_stage) produced by a compute action."""
-    if a.op == Op.F and a.stage < S - 1:
-        return [("F", a.stage + 1)]
-    if a.op == (Op.I if split else Op.B) and a.stage > 0:
-        return [("B", a.stage - 1)]
-    return []
-
-
 def lower(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1, style: str = "loop",
-          comm: float = 0.05, add_reduce_grad: bool = True, check: bool = True) -> Dict[int, List[Entry]]:
+          comm: float = 0.05, add_reduce_grad: bool = True, check: bool = True,
+          costs: Optional[Dict[Op, float]] = None, head_costs: Optional[Dict[int, float]] = None,
+          stage_costs: Optional[Sequence[float]] = None) -> Dict[int, List[Entry]]:
     S = pp * v
     s2r = [stage_to_rank(s, pp, style) for s in range(S)]
     seq = {r: [a for a in orders.get(r, []) if a is not None and a.op.is_compute] for r in range(pp)}
     split = uses_split_backward(seq)
-    sim = simulate(seq, pp, v, style, comm_latency=comm)
+    head = head_ranks_of(seq)
+    sim = simulate(seq, pp, v, style, comm_latency=comm, costs=costs, head_costs=head_costs,
+                   stage_costs=stage_costs)
 
+    # every cross-rank input of every compute is one message (same-rank inputs are
+    # hand-offs); stamped with the producer's simulated end time
     msgs: List[Message] = []
     for r in range(pp):
         for a in seq[r]:
-            for kind, dst_stage in _producers(a, S, split):
-                dst = s2r[dst_stage]
-                if dst == r:
-                    continue  # same-rank hand-off, no comm
-                msgs.append(Message((kind, dst_stage, a.mb), r, dst, sim.end[a], a, dst_stage))
+            for prod, key in in_messages(a, S, split, head):
+                if key is None:
+                    continue
+                src = action_rank(prod, s2r)
+                if src == r:
+                    continue
+                msgs.append(Message(key, src, r, sim.end[prod], prod, a))
     msgs.sort(key=Message.order_key)
 
     program: Dict[int, List[Entry]] = {}
@@ -79,20 +78,16 @@ def lower(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1, st
         # index of consumer compute for each recv / producer compute for each send
         pos = {a: i for i, a in enumerate(seq[r])}
 
-        def consumer_idx(mm: Message) -> int:
-            kind, st, mb = mm.key
-            op = Op.F if kind == "F" else (Op.I if split else Op.B)
-            return pos[Action(st, op, mb)]
-
         ops_ordered: List[Tuple[CommOp, int, bool]] = []  # (op, anchor compute idx, is_send)
         for mm in mine:
             kind, st, mb = mm.key
+            send_op, recv_op = MSG_OPS[kind]
             if mm.src == r:
-                act = Action(mm.producer.stage, Op.SEND_F if kind == "F" else Op.SEND_B, mb)
+                act = Action(mm.producer.stage, send_op, mb)
                 ops_ordered.append((CommOp(act, mm.dst, mm.key), pos[mm.producer], True))
             else:
-                act = Action(st, Op.RECV_F if kind == "F" else Op.RECV_B, mb)
-                ops_ordered.append((CommOp(act, mm.src, mm.key), consumer_idx(mm), False))
+                act = Action(st, recv_op, mb)
+                ops_ordered.append((CommOp(act, mm.src, mm.key), pos[mm.consumer], False))
 
         # slot p = "posted right before compute p".  Walk the global order; each op goes
         # at max(previous op's slot, earliest allowed): sends after their producer,

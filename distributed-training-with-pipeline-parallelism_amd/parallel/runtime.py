@@ -13,6 +13,10 @@ torch schedules.py:2037-2284, and the single-stage loops schedules.py:727-994):
 * ``B`` / ``I`` / ``W`` -> backward (full or split).
 * ``REDUCE_GRAD`` -> the stage's grad finalisation + async DP all-reduce, issued
   right after its last backward so it overlaps the rest of the flush.
+* ``H``          -> (distributed head, :mod:`.headsplit`) this rank's token chunk of a
+  microbatch through the LM head + loss; the last stage scatters its final-norm
+  rows (``H`` messages) and its backward consumes the gathered chunk gradients
+  (``D`` messages, received straight into one [T, D] buffer per microbatch).
 
 Same-rank stage hand-offs (several virtual stages on one rank) bypass the
 transport.  With ``profile=True`` every compute action is bracketed by timing
@@ -29,6 +33,7 @@ import torch
 import torch.distributed as dist
 
 from .comm import P2P
+from .headsplit import HeadPlan
 from .ir import Action, CommGroup, Entry, Op, format_compute_grid
 from .lower import lower
 from .schedules import canonical_name, generate, stage_to_rank
@@ -79,7 +84,9 @@ class _Timer:
 class PipelineRuntime:
     def __init__(self, stages: Sequence[StageBase], schedule: str, n_microbatches: int, pp_rank: int,
                  pp_size: int, p2p: P2P, loss_fn: Optional[Callable] = None, scale_grads: bool = True,
-                 style: str = "loop", program: Optional[Dict[int, List[Entry]]] = None, profile: bool = False):
+                 style: str = "loop", program: Optional[Dict[int, List[Entry]]] = None, profile: bool = False,
+                 orders: Optional[Dict[int, List[Action]]] = None, head: Optional[HeadPlan] = None,
+                 head_costs: Optional[Dict[int, float]] = None, stage_costs: Optional[Sequence[float]] = None):
         self.stages: Dict[int, StageBase] = {s.stage_index: s for s in stages}
         self.schedule = canonical_name(schedule)
         self.m = n_microbatches
@@ -100,11 +107,13 @@ class PipelineRuntime:
         if sorted(self.stages) != expected:
             raise ValueError(f"rank {pp_rank} holds stages {sorted(self.stages)}, placement '{style}' expects {expected}")
         self.s2r = [stage_to_rank(s, pp_size, style) for s in range(self.num_stages)]
+        self.head = head
         if program is None:
-            orders = generate(self.schedule, pp_size, n_microbatches, self.v, style)
+            if orders is None:
+                orders = generate(self.schedule, pp_size, n_microbatches, self.v, style)
             validate(orders, pp_size, self.v, n_microbatches, style)
             self.orders = orders
-            program = lower(orders, pp_size, self.v, style)
+            program = lower(orders, pp_size, self.v, style, head_costs=head_costs, stage_costs=stage_costs)
         else:
             self.orders = {r: [e for e in es if isinstance(e, Action) and e.op.is_compute] for r, es in program.items()}
         self.program_all = program
@@ -116,6 +125,8 @@ class PipelineRuntime:
         self.last_step_ms: float = 0.0
         self._initialized = False
         self._recv_bufs: Dict[tuple, List[torch.Tensor]] = {}
+        self._dh_full: Dict[int, torch.Tensor] = {}
+        self.head_losses: Dict[int, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ init
     def _needs_inference(self) -> bool:
@@ -134,6 +145,12 @@ class PipelineRuntime:
                     peers.add(self.s2r[s - 1])
                 if s < self.num_stages - 1:
                     peers.add(self.s2r[s + 1])
+            if self.head is not None:  # head chunks: last-stage rank <-> every chunk rank
+                last = self.s2r[self.num_stages - 1]
+                if self.rank == last:
+                    peers.update(self.head.ranks)
+                elif self.rank in self.head.ranks:
+                    peers.add(last)
             self.p2p.warmup(sorted(peers), self.rank)
         if self._needs_inference():
             prev_out = None
@@ -159,8 +176,25 @@ class PipelineRuntime:
                     self.p2p.send_specs(out_specs, self.s2r[s + 1])
         self._initialized = True
 
+    def _dh_buf(self, mb: int) -> torch.Tensor:
+        """[T, D] input-gradient buffer of the last stage for microbatch mb; the head
+        chunks' D messages land in its row slices."""
+        t = self._dh_full.get(mb)
+        if t is None:
+            h = self.head
+            t = torch.empty(h.tokens, h.d_model, dtype=h.dtype, device=self.device)
+            self._dh_full[mb] = t
+        return t
+
     def _recv_buf(self, key: tuple) -> List[torch.Tensor]:
+        kind = key[0]
+        if kind == "D":
+            return [self._dh_buf(key[2])[self.head.rows(key[1])]]
         buf = self._recv_bufs.get(key)
+        if buf is None and kind == "H":
+            h = self.head
+            buf = [torch.empty(h.chunks[key[1]], h.d_model, dtype=h.dtype, device=self.device)]
+            self._recv_bufs[key] = buf
         if buf is None:
             kind, stage, mb = key
             st = self.stages[stage]
@@ -183,6 +217,8 @@ class PipelineRuntime:
         handoff: Dict[tuple, Tuple[torch.Tensor, ...]] = {}
         outputs: Dict[int, Tuple[torch.Tensor, ...]] = {}
         mb_losses: Dict[int, torch.Tensor] = {}
+        self.head_losses = {}
+        head = self.head
         reduce_works = []
         loss_scale = 1.0 / self.m if self.scale_grads else 1.0
         S = self.num_stages
@@ -230,7 +266,17 @@ class PipelineRuntime:
                         args = tuple(self._recv_buf(key))
                     tgt = targets[a.mb] if (st.is_last and targets is not None) else None
                     out, loss = st.forward_mb(a.mb, args, tgt, self.loss_fn, loss_scale)
-                    if st.is_last:
+                    if st.is_last and head is not None:
+                        # scatter the final-norm rows to the head chunks
+                        hn = out[0]
+                        for r in head.ranks:
+                            hk = ("H", r, a.mb)
+                            piece = (hn[head.rows(r)],)
+                            if r == self.rank:
+                                handoff[hk] = piece
+                            else:
+                                send_tensors[hk] = piece
+                    elif st.is_last:
                         if return_outputs:
                             outputs[a.mb] = out
                         if loss is not None:
@@ -241,9 +287,32 @@ class PipelineRuntime:
                             handoff[nk] = out
                         else:
                             send_tensors[nk] = out
+                elif a.op == Op.H:
+                    hk = ("H", a.stage, a.mb)
+                    if hk in handoff:
+                        (h_in,) = handoff.pop(hk)
+                    else:
+                        wait_recv(hk)
+                        (h_in,) = self._recv_buf(hk)
+                    rows = head.rows(a.stage)
+                    tgt = targets[a.mb].reshape(-1)[rows]
+                    local_last = self.s2r[S - 1] == self.rank
+                    if local_last:
+                        dh = self._dh_buf(a.mb)[rows]
+                    else:
+                        dh = torch.empty_like(h_in)
+                    loss_sum = head.runner(h_in, tgt, dh, loss_scale / head.tokens)
+                    self.head_losses[a.mb] = loss_sum
+                    if not local_last:
+                        send_tensors[("D", a.stage, a.mb)] = (dh,)
                 elif a.op in (Op.B, Op.I):
                     key = ("B", a.stage, a.mb)
-                    if a.stage == S - 1:
+                    if a.stage == S - 1 and head is not None:
+                        for r in head.ranks:
+                            if r != self.rank:
+                                wait_recv(("D", r, a.mb))
+                        g = (self._dh_full.pop(a.mb),)
+                    elif a.stage == S - 1:
                         g = None
                     elif key in handoff:
                         g = handoff.pop(key)

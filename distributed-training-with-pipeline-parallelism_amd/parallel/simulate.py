@@ -21,7 +21,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 from .ir import Action, CommGroup, Entry, Op
 from .schedules import stage_to_rank
 
-DEFAULT_COSTS = {Op.F: 1.0, Op.B: 2.0, Op.I: 1.0, Op.W: 1.0, Op.REDUCE_GRAD: 0.0}
+DEFAULT_COSTS = {Op.F: 1.0, Op.B: 2.0, Op.I: 1.0, Op.W: 1.0, Op.H: 1.0, Op.REDUCE_GRAD: 0.0}
 
 
 @dataclass
@@ -47,19 +47,44 @@ class SimResult:
             json.dump(self.chrome_trace(), f)
 
 
-def _deps(a: Action, num_stages: int, split: bool) -> List[Action]:
-    """Cross-stage data dependencies of a compute action."""
+def head_ranks_of(orders) -> Tuple[int, ...]:
+    """Ranks that run a chunk of the distributed LM head (``H`` actions)."""
+    return tuple(sorted({a.stage for v in orders.values() for a in v if a is not None and a.op == Op.H}))
+
+
+def action_rank(a: Action, s2r: Sequence[int]) -> int:
+    """Rank executing an action: ``H`` actions carry their rank in the stage field."""
+    return a.stage if a.op == Op.H else s2r[a.stage]
+
+
+def in_messages(a: Action, num_stages: int, split: bool, head: Sequence[int] = ()) -> List[Tuple[Action, Optional[tuple]]]:
+    """Data inputs of a compute action: ``(producer, message key)``; the key is None for
+    state that never leaves the stage (a backward's own forward activations).
+
+    Keys: ``('F', s, m)`` activation into stage s, ``('B', s, m)`` gradient into stage s,
+    ``('H', r, m)`` head chunk r's hidden states, ``('D', r, m)`` head chunk r's input
+    gradient.  With a distributed head (``head`` = chunk ranks) the last stage's
+    backward consumes the ``D`` messages of every chunk."""
     bwd = Op.I if split else Op.B
     if a.op == Op.F:
-        return [] if a.stage == 0 else [Action(a.stage - 1, Op.F, a.mb)]
+        return [] if a.stage == 0 else [(Action(a.stage - 1, Op.F, a.mb), ("F", a.stage, a.mb))]
     if a.op in (Op.B, Op.I):
-        deps = [Action(a.stage, Op.F, a.mb)]
+        out: List[Tuple[Action, Optional[tuple]]] = [(Action(a.stage, Op.F, a.mb), None)]
         if a.stage < num_stages - 1:
-            deps.append(Action(a.stage + 1, bwd, a.mb))
-        return deps
+            out.append((Action(a.stage + 1, bwd, a.mb), ("B", a.stage, a.mb)))
+        else:
+            out += [(Action(r, Op.H, a.mb), ("D", r, a.mb)) for r in head]
+        return out
     if a.op == Op.W:
-        return [Action(a.stage, Op.I, a.mb)]
+        return [(Action(a.stage, Op.I, a.mb), None)]
+    if a.op == Op.H:
+        return [(Action(num_stages - 1, Op.F, a.mb), ("H", a.stage, a.mb))]
     return []
+
+
+def _deps(a: Action, num_stages: int, split: bool, head: Sequence[int] = ()) -> List[Action]:
+    """Cross-stage data dependencies of a compute action."""
+    return [d for d, _ in in_messages(a, num_stages, split, head)]
 
 
 def uses_split_backward(orders: Dict[int, Sequence[Optional[Action]]]) -> bool:
@@ -68,12 +93,14 @@ def uses_split_backward(orders: Dict[int, Sequence[Optional[Action]]]) -> bool:
 
 def simulate(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1, style: str = "loop",
              costs: Optional[Dict[Op, float]] = None, comm_latency: float = 0.0,
-             stage_costs: Optional[Sequence[float]] = None) -> SimResult:
+             stage_costs: Optional[Sequence[float]] = None,
+             head_costs: Optional[Dict[int, float]] = None) -> SimResult:
     """Time a per-rank compute order.  ``stage_costs`` scales each stage's op costs
-    (non-uniform partitions)."""
+    (non-uniform partitions); ``head_costs[r]`` is the cost of rank r's head chunk."""
     costs = dict(DEFAULT_COSTS, **(costs or {}))
     S = pp * v
     split = uses_split_backward(orders)
+    head = head_ranks_of(orders)
     s2r = [stage_to_rank(s, pp, style) for s in range(S)]
     seq = {r: [a for a in orders[r] if a is not None and a.op.is_compute] for r in orders}
     ptr = {r: 0 for r in seq}
@@ -88,15 +115,18 @@ def simulate(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1,
                 a = seq[r][ptr[r]]
                 ready = t_rank[r]
                 ok = True
-                for d in _deps(a, S, split):
+                for d in _deps(a, S, split, head):
                     if d not in end:
                         ok = False
                         break
-                    lat = comm_latency if s2r[d.stage] != s2r[a.stage] else 0.0
+                    lat = comm_latency if action_rank(d, s2r) != action_rank(a, s2r) else 0.0
                     ready = max(ready, end[d] + lat)
                 if not ok:
                     break
-                c = costs[a.op] * (stage_costs[a.stage] if stage_costs is not None else 1.0)
+                if a.op == Op.H:
+                    c = costs[Op.H] * (head_costs.get(a.stage, 1.0) if head_costs else 1.0)
+                else:
+                    c = costs[a.op] * (stage_costs[a.stage] if stage_costs is not None else 1.0)
                 start[a] = ready
                 end[a] = ready + c
                 t_rank[r] = end[a]
@@ -133,7 +163,9 @@ def to_grid(res: SimResult, pp: int) -> Dict[int, List[Optional[Action]]]:
 
 def check_lowered(program: Dict[int, List[Entry]], num_stages: int) -> None:
     """Raise RuntimeError if the lowered program can hang under RCCL semantics."""
-    split = uses_split_backward({r: [e for e in es if isinstance(e, Action)] for r, es in program.items()})
+    comp_orders = {r: [e for e in es if isinstance(e, Action)] for r, es in program.items()}
+    split = uses_split_backward(comp_orders)
+    head = head_ranks_of(comp_orders)
     ranks = sorted(program)
     # message key -> (sender group id, receiver group id)
     msg_groups: Dict[tuple, List[Tuple[int, int]]] = {}
@@ -176,11 +208,9 @@ def check_lowered(program: Dict[int, List[Entry]], num_stages: int) -> None:
     for r in ranks:
         for ci, a in enumerate(comp_list[r]):
             waits = []
-            for d in _deps(a, num_stages, split):
-                kind = "F" if d.op == Op.F else "B"
-                key = (r, kind, a.stage, a.mb)  # message into (a.stage) carrying d's output
-                if (r,) + (kind, a.stage, a.mb) in recv_group_of:
-                    waits.append(recv_group_of[(r,) + (kind, a.stage, a.mb)])
+            for _, key in in_messages(a, num_stages, split, head):
+                if key is not None and (r,) + key in recv_group_of:
+                    waits.append(recv_group_of[(r,) + key])
             comp_waits[(r, ci)] = waits
     ncomp = {r: len(comp_list[r]) for r in ranks}
     ngrp = {r: sum(1 for e in entries[r] if isinstance(e, CommGroup)) for r in ranks}

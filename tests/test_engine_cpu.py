@@ -22,11 +22,13 @@ def _data(cfg, dp_rank=0):
             torch.randint(0, cfg.vocab_size, (M * MBS, S), generator=g))
 
 
-def _train(name, pp, dp, schedule, steps=2):
+def _train(name, pp, dp, schedule, steps=2, split_head=None, layer_ranges="auto"):
     cfg = CFG[name]()
+    if layer_ranges == "auto":
+        layer_ranges = [(0, 2), (2, 4)] if pp == 2 else None
     tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=schedule, n_microbatches=M, mbs=MBS, seq_len=S,
                          device=torch.device("cpu"), dtype=torch.float32, lr=1e-3,
-                         layer_ranges=[(0, 2), (2, 4)] if pp == 2 else None)
+                         layer_ranges=layer_ranges, split_head=split_head, head_align=8)
     losses = []
     for _ in range(steps):
         x, y = _data(cfg, tr.mesh.dp_rank)
@@ -37,16 +39,19 @@ def _train(name, pp, dp, schedule, steps=2):
     return dict(losses=losses, sd=sd)
 
 
-def _worker(rank, world, name, pp, dp, schedule):
-    return _train(name, pp, dp, schedule)
+def _worker(rank, world, name, pp, dp, schedule, split_head=None, layer_ranges="auto"):
+    return _train(name, pp, dp, schedule, split_head=split_head, layer_ranges=layer_ranges)
 
 
 @pytest.mark.parametrize("name", ["gpt2", "llama"])
 @pytest.mark.parametrize("schedule", ["1F1B", "GPipe", "ZBH1"])
-def test_pp2_matches_pp1(name, schedule):
+@pytest.mark.parametrize("split_head", [False, True])
+def test_pp2_matches_pp1(name, schedule, split_head):
     ref = _train(name, 1, 1, "1F1B")
-    res = run_world(_worker, 2, name, 2, 1, schedule)
+    res = run_world(_worker, 2, name, 2, 1, schedule, split_head)
     assert res[1]["losses"] == pytest.approx(ref["losses"], rel=1e-5)
+    if split_head:  # every rank reports the loss
+        assert res[0]["losses"] == pytest.approx(ref["losses"], rel=1e-5)
     for r in res.values():
         for k, v in r["sd"].items():
             torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref["sd"][k]), atol=1e-4, rtol=1e-4,  # Adam amplifies fp32 reduction-order noise
@@ -60,3 +65,25 @@ def test_dp2_pp2_runs_and_replicas_agree():
         for k, v in res[a]["sd"].items():
             torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(res[b]["sd"][k]), atol=0, rtol=0)
     assert all(l == l for l in res[1]["losses"])
+
+
+@pytest.mark.parametrize("schedule,layer_ranges", [("1F1B", None), ("GPipe", [(0, 1), (1, 2), (2, 3), (3, 4)]),
+                                                   ("ZBH1", None)])
+def test_pp4_distributed_head_matches_pp1(schedule, layer_ranges):
+    """Distributed head over 4 ranks (uneven token chunks): same loss/weights as PP=1."""
+    ref = _train("gpt2", 1, 1, "1F1B")
+    res = run_world(_worker, 4, "gpt2", 4, 1, schedule, True, layer_ranges)
+    for r in range(4):
+        assert res[r]["losses"] == pytest.approx(ref["losses"], rel=1e-5)
+    for r in res.values():
+        for k, v in r["sd"].items():
+            torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref["sd"][k]), atol=1e-4, rtol=1e-4,
+                                       msg=lambda m: f"{k}: {m}")
+
+
+def test_dp2_pp2_distributed_head_replicas_agree():
+    res = run_world(_worker, 4, "llama", 2, 2, "1F1B", True)
+    for a, b in [(0, 2), (1, 3), (0, 1)]:
+        for k, v in res[a]["sd"].items():
+            if k in res[b]["sd"]:
+                torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(res[b]["sd"][k]), atol=0, rtol=0)

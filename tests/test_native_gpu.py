@@ -50,3 +50,33 @@ def test_native_gpu_vs_f32_reference(name):
         cos = torch.nn.functional.cosine_similarity(gr.flatten(), gg.flatten(), dim=0).item()
         rel = ((gr - gg).norm() / gr.norm()).item()
         assert cos > 0.99 and rel < 0.15, f"{name}:{n} cos={cos:.4f} rel={rel:.4f}"
+
+
+@pytest.mark.parametrize("tied", [True, False])
+def test_head_shard_chunks_vs_f32_reference(tied):
+    """Distributed-head chunk on the HIP path (small-M logits GEMM, split-K dX, dW
+    accumulate, fused CE) vs an f32 torch reference of the full head."""
+    from mipipe.models.native import HeadShard
+    cfg = NativeConfig.gpt2("small") if tied else NativeConfig.llama3("1b")
+    dev = torch.device("cuda")
+    head = HeadShard(cfg, dev, seed=3)
+    T, D = 2048, cfg.d_model
+    g = torch.Generator(device="cuda").manual_seed(0)
+    h = torch.randn(T, D, device=dev, generator=g).to(torch.bfloat16)
+    tgt = torch.randint(0, cfg.vocab_size, (T,), device=dev, generator=g)
+    dh = torch.empty(T, D, device=dev, dtype=torch.bfloat16)
+    loss = torch.zeros((), device=dev)
+    for sl in (slice(0, 512), slice(512, 2048)):   # uneven chunks, as a PP=8 split produces
+        loss = loss + head.run(h[sl], tgt[sl], dh[sl], 1.0 / T)
+    W = head.weight().float().clone().requires_grad_()
+    hr = h.float().clone().requires_grad_()
+    logits = hr @ W.t()
+    logits[:, cfg.vocab_size:] = -float("inf")
+    ref = torch.nn.functional.cross_entropy(logits, tgt, reduction="sum")
+    (ref / T).backward()
+    assert abs(float(loss) - float(ref)) / float(ref) < 2e-3
+    cos = torch.nn.functional.cosine_similarity(dh.float().flatten(), hr.grad.flatten(), dim=0)
+    assert cos > 0.995
+    gw = head.arena.g(head.wname)
+    cosw = torch.nn.functional.cosine_similarity(gw.flatten(), W.grad.flatten(), dim=0)
+    assert cosw > 0.995

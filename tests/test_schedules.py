@@ -6,7 +6,7 @@ import pytest
 
 import mipipe  # noqa: F401
 from mipipe.parallel import Action, Op, analytic_bubble, generate, lower, simulate
-from mipipe.parallel.ir import from_csv, to_csv
+from mipipe.parallel.ir import CommGroup, from_csv, to_csv
 from mipipe.parallel.schedules import stage_to_rank
 from mipipe.parallel.simulate import check_lowered
 from mipipe.parallel.validate import ScheduleError, validate
@@ -130,3 +130,50 @@ def test_v_placement_interleaved_lowering():
     # the chunk boundary 3 -> 4 is on the same rank under 'v': no comm for it
     keys = {op.key for es in prog.values() for e in es if not isinstance(e, Action) for op in e.ops}
     assert ("F", 4, 0) not in keys
+
+
+# ----------------------------------------------------------------------------- distributed head
+from mipipe.parallel.headsplit import head_token_split, insert_head_ops, plan_head_schedule  # noqa: E402
+
+
+def test_head_token_split_levels_load():
+    load = [1.1, 1, 1, 1, 2, 2, 2, 2.1]
+    tok = head_token_split(16384, load, 5.2, align=128)
+    assert sum(tok) == 16384 and all(t % 128 == 0 for t in tok)
+    tot = [l + 5.2 * t / 16384 for l, t in zip(load, tok)]
+    assert max(tot) - min(tot) < 0.1
+    # a rank already above the water level gets nothing
+    assert head_token_split(1024, [0, 0, 10], 1.0, align=128)[2] == 0
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+@pytest.mark.parametrize("sched", ["1F1B", "GPipe", "ZBH1", "Interleaved1F1B", "LoopedBFS"])
+def test_head_ops_lower_without_deadlock(P, sched):
+    from mipipe.parallel.schedules import SCHEDULES
+    v = 2 if SCHEDULES[sched][2] else 1
+    m = 2 * P
+    for skew in (0.0, 1.0):
+        hc = {r: 0.5 + skew * r / P for r in range(P)}
+        if skew:
+            hc.pop(1 % P, None)   # a rank without a chunk
+        orders = generate(sched, P, m, v, "loop")
+        ho, lag, mk = plan_head_schedule(orders, P, v, "loop", hc)
+        validate(ho, P, v, m, "loop")
+        for r in range(P):
+            hs = [a.mb for a in ho[r] if a.op == Op.H]
+            assert hs == (list(range(m)) if r in hc else [])
+        prog = lower(ho, P, v, "loop", head_costs=hc)   # runs the RCCL-semantics deadlock check
+        kinds = {op.key[0] for es in prog.values() for e in es if isinstance(e, CommGroup) for op in e.ops}
+        assert {"H", "D"} <= kinds
+
+
+def test_head_split_beats_last_stage_head_in_simulation():
+    """GPT-2 small PP=8: the distributed head removes the last-stage bottleneck."""
+    P, m, head = 8, 16, 5.2
+    load = [1.1, 1, 1, 1, 2, 2, 2, 2.1]
+    tok = head_token_split(16384, load, head)
+    hc = {r: 3 * head * t / 16384 for r, t in enumerate(tok) if t}
+    o = generate("1F1B", P, m, 1, "loop")
+    base = simulate(o, P, 1, "loop", stage_costs=[c + (head if s == P - 1 else 0) for s, c in enumerate(load)])
+    _, _, mk = plan_head_schedule(o, P, 1, "loop", hc, stage_costs=load)
+    assert mk < 0.6 * base.makespan
