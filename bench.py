@@ -87,7 +87,8 @@ def main():
     def sync():
         if world > 1:
             dist.barrier()
-        torch.cuda.synchronize()
+        if device.type == "cuda":
+            torch.cuda.synchronize()
 
     for _ in range(a.warmup):
         trainer.train_step(tokens, targets)
@@ -150,7 +151,7 @@ def main():
     if loss_val is not None:
         out["last_loss"] = round(loss_val, 4)
     # the loss lives on the last pipeline rank; rank 0 prints
-    if world > 1:
+    if world > 1 and trainer.head is None:
         lv = torch.tensor([loss_val if loss_val is not None else 0.0], device=device, dtype=torch.float64)
         dist.all_reduce(lv, op=dist.ReduceOp.SUM)
         out["last_loss"] = round(float(lv.item()) / dp, 4)

@@ -186,6 +186,17 @@ class PipelineTrainer:
         return self.runtime.bubble()
 
     # ------------------------------------------------------------------ checkpoint
+    def save_checkpoint(self, path: str, extra: Optional[dict] = None) -> None:
+        """Per-pipeline-rank safetensors shards keyed by global FQNs + JSON manifest
+        (collective; see utils/checkpoint.py)."""
+        from .utils.checkpoint import save_checkpoint
+        save_checkpoint(self, path, extra=extra)
+
+    def load_checkpoint(self, path: str, load_optimizer: bool = True) -> dict:
+        """Resume from a checkpoint written at any PP degree (re-split by FQN)."""
+        from .utils.checkpoint import load_checkpoint
+        return load_checkpoint(self, path, load_optimizer=load_optimizer)
+
     def state_dict(self):
         sd = {}
         for st in self.stages:
