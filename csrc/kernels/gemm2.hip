@@ -95,6 +95,102 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | (((N >> 4) & 3) << 14));
 }
 
+// ---- epilogue: one wave-row group at a time through LDS -> coalesced 16-byte bias /
+// residual / activation / store, or lane-consecutive f32 atomics for split-K
+template <int BM, int BN, int WM, int WN, int EPI, bool ACC>
+__device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 32], char* smem, int m0, int n0, int wr,
+                                         int wn, int hl, int l32, void* __restrict__ Cv,
+                                         const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
+                                         bf16_t* __restrict__ AUX, int M, int N, int64_t ldc, int64_t ldr, int64_t ldx,
+                                         float alpha, int nsplit) {
+  constexpr int WTM = BM / WM / 32, WTN = BN / WN / 32;
+  constexpr int RG = BM / WM;      // rows per group
+  constexpr int CP = BN + 4;       // f32 pitch
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll 1
+  for (int pass = 0; pass < WM; ++pass) {
+    if (wr == pass) {
+#pragma unroll
+      for (int i = 0; i < WTM; ++i)
+#pragma unroll
+        for (int j = 0; j < WTN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            const int col = wn + 32 * j + l32;
+            ct[row * CP + col] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    const int rbase = m0 + pass * RG;
+    if constexpr (ACC) {
+      if (nsplit > 1) {
+        float* C = reinterpret_cast<float*>(Cv);
+        for (int idx = threadIdx.x; idx < RG * BN; idx += NT) {
+          const int row = idx / BN, col = idx % BN;
+          const int gr = rbase + row, gc = n0 + col;
+          if (gr < M && gc < N) atomicAdd(C + (int64_t)gr * ldc + gc, alpha * ct[row * CP + col]);
+        }
+        __syncthreads();
+        continue;
+      }
+    }
+    for (int idx = threadIdx.x; idx < RG * BN / 8; idx += NT) {
+      const int row = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
+      const int gr = rbase + row, gc = n0 + c8;
+      if (gr >= M || gc >= N) continue;
+      float v[8];
+      const float4 lo = *reinterpret_cast<const float4*>(ct + row * CP + c8);
+      const float4 hi = *reinterpret_cast<const float4*>(ct + row * CP + c8 + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= alpha;
+      if constexpr (ACC) {
+        float* cp = reinterpret_cast<float*>(Cv) + (int64_t)gr * ldc + gc;
+        float4 c0 = *reinterpret_cast<float4*>(cp), c1 = *reinterpret_cast<float4*>(cp + 4);
+        c0.x += v[0]; c0.y += v[1]; c0.z += v[2]; c0.w += v[3];
+        c1.x += v[4]; c1.y += v[5]; c1.z += v[6]; c1.w += v[7];
+        *reinterpret_cast<float4*>(cp) = c0;
+        *reinterpret_cast<float4*>(cp + 4) = c1;
+      } else {
+        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RES) {
+          u16x8 bv = *reinterpret_cast<const u16x8*>(bias + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[e]);
+        }
+        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
+          u16x8 pre;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            pre[e] = f2bf(v[e]);
+            const float x = bf2f(pre[e]);
+            v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
+          }
+          *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
+        }
+        if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
+          u16x8 rv = *reinterpret_cast<const u16x8*>(R + (int64_t)gr * ldr + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += bf2f(rv[e]);
+        }
+        if constexpr (EPI == EPI_DGELU || EPI == EPI_DRELU) {
+          u16x8 xv = *reinterpret_cast<const u16x8*>(AUX + (int64_t)gr * ldx + gc);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float x = bf2f(xv[e]);
+            v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
+          }
+        }
+        u16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+        *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(Cv) + (int64_t)gr * ldc + gc) = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
 __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm2_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                       void* __restrict__ Cv, const bf16_t* __restrict__ bias,
@@ -220,92 +316,195 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
     asm volatile("" ::: "memory");
   }
 
-  // ---- epilogue: one wave-row group at a time through LDS
-  constexpr int RG = BM / WM;      // rows per group
-  constexpr int CP = BN + 4;       // f32 pitch
-  float* ct = reinterpret_cast<float*>(smem);
-#pragma unroll 1
-  for (int pass = 0; pass < WM; ++pass) {
-    if (wr == pass) {
+  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, M, N, ldc, ldr, ldx, alpha,
+                                     nsplit);
+}
+
+
+// ---------------------------------------------------------------------------------------
+// gemm3: 256x256 NT (both operands K-contiguous) with a ping-pong phase schedule.
+//
+// The K-tile (BK = 64) is cut into four 16 KiB half-tiles, each one LDS image of 128 rows:
+//   A0 = rows {0..63, 128..191}   A1 = rows {64..127, 192..255}     (wave-row halves)
+//   B0 = cols {0..31, 64..95, ..} B1 = cols {32..63, 96..127, ..}  (wave-col halves)
+// A wave (wr, wc) owns a 128x64 output tile = four 64x32 quadrants, one per phase:
+//   phase 1: A0 x B0 (reads A0 + B0)  phase 2: A0 x B1 (reads B1)
+//   phase 3: A1 x B0 (reads A1)       phase 4: A1 x B1 (no reads)
+// Phase p of K-tile t also streams half-tile p of K-tile t+1 into the other LDS buffer
+// (2 glds per thread) -- DMA is spread evenly over the loop instead of bursting once
+// per K-tile -- and a counted vmcnt(4) retires the half-tile the NEXT phase reads.
+// Wave rows run one barrier apart (waves 4-7 take an extra s_barrier up front), so on
+// every SIMD one wave issues MFMAs while its partner issues ds_reads / DMA: the
+// cdna guide's 8-phase template (§5 "256^2 8-phase template"), with 32x32x16 MFMAs.
+// ---------------------------------------------------------------------------------------
+template <int EPI, bool ACC>
+__global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
+             const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX, int M, int N,
+             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha) {
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
+  constexpr int HALF = 128 * 128;          // one half-tile image: 128 rows x 128 B
+  constexpr int BUF = 4 * HALF;            // A0 A1 B0 B1
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int wg = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int group = wg / (GROUP * gn);
+  const int first_m = group * GROUP;
+  const int gsz = min(gm - first_m, GROUP);
+  const int tm = first_m + (wg % (GROUP * gn)) % gsz;
+  const int tn = (wg % (GROUP * gn)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int wm = wr * (BM / WM), wn = wc * (BN / WN);
+
+  const int nsplit = gridDim.y;
+  const int ktiles = K / BK;
+  const int kt0 = (int)blockIdx.y * ktiles / nsplit;
+  const int nk = ((int)blockIdx.y + 1) * ktiles / nsplit - kt0;
+
+  // staging: this wave's two 1 KiB pieces (j = 0, 1) of every half-tile.  Piece rows
+  // i = 64 j + 8 wave + (lane >> 3); swz8 reads row bits 1-3, i.e. i & 15 = 8 (wave & 1) + lr.
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ swz8(8 * (wave & 1) + lr);
+  const bf16_t* pa[2];
+  const bf16_t* pb[2];
 #pragma unroll
-      for (int i = 0; i < WTM; ++i)
-#pragma unroll
-        for (int j = 0; j < WTN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
-            const int col = wn + 32 * j + l32;
-            ct[row * CP + col] = acc[i][j][r];
-          }
-    }
-    __syncthreads();
-    const int rbase = m0 + pass * RG;
-    if constexpr (ACC) {
-      if (nsplit > 1) {
-        float* C = reinterpret_cast<float*>(Cv);
-        for (int idx = threadIdx.x; idx < RG * BN; idx += NT) {
-          const int row = idx / BN, col = idx % BN;
-          const int gr = rbase + row, gc = n0 + col;
-          if (gr < M && gc < N) atomicAdd(C + (int64_t)gr * ldc + gc, alpha * ct[row * CP + col]);
-        }
-        __syncthreads();
-        continue;
-      }
-    }
-    for (int idx = threadIdx.x; idx < RG * BN / 8; idx += NT) {
-      const int row = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
-      const int gr = rbase + row, gc = n0 + c8;
-      if (gr >= M || gc >= N) continue;
-      float v[8];
-      const float4 lo = *reinterpret_cast<const float4*>(ct + row * CP + c8);
-      const float4 hi = *reinterpret_cast<const float4*>(ct + row * CP + c8 + 4);
-      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= alpha;
-      if constexpr (ACC) {
-        float* cp = reinterpret_cast<float*>(Cv) + (int64_t)gr * ldc + gc;
-        float4 c0 = *reinterpret_cast<float4*>(cp), c1 = *reinterpret_cast<float4*>(cp + 4);
-        c0.x += v[0]; c0.y += v[1]; c0.z += v[2]; c0.w += v[3];
-        c1.x += v[4]; c1.y += v[5]; c1.z += v[6]; c1.w += v[7];
-        *reinterpret_cast<float4*>(cp) = c0;
-        *reinterpret_cast<float4*>(cp + 4) = c1;
-      } else {
-        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RES) {
-          u16x8 bv = *reinterpret_cast<const u16x8*>(bias + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[e]);
-        }
-        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
-          u16x8 pre;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            pre[e] = f2bf(v[e]);
-            const float x = bf2f(pre[e]);
-            v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
-          }
-          *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
-        }
-        if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
-          u16x8 rv = *reinterpret_cast<const u16x8*>(R + (int64_t)gr * ldr + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += bf2f(rv[e]);
-        }
-        if constexpr (EPI == EPI_DGELU || EPI == EPI_DRELU) {
-          u16x8 xv = *reinterpret_cast<const u16x8*>(AUX + (int64_t)gr * ldx + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float x = bf2f(xv[e]);
-            v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
-          }
-        }
-        u16x8 o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
-        *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(Cv) + (int64_t)gr * ldc + gc) = o;
-      }
-    }
-    __syncthreads();
+  for (int j = 0; j < 2; ++j) {
+    int ra = m0 + 128 * j + 8 * wave + lr;          // A0 row; A1 = +64
+    ra = ra < M ? ra : M - 1;
+    int rb = n0 + 64 * ((wave >> 2) + 2 * j) + 8 * (wave & 3) + lr;   // B0 row (= output col); B1 = +32
+    rb = rb < N ? rb : N - 1;
+    pa[j] = A + (int64_t)ra * lda + (int64_t)kt0 * BK + lc * 8;
+    pb[j] = B + (int64_t)rb * ldb + (int64_t)kt0 * BK + lc * 8;
   }
+  // rows past the M/N edge of the A1/B1 halves: clamp by pointer (the +64/+32 offsets)
+  const bool a1_ok0 = m0 + 64 + 8 * wave + lr < M, a1_ok1 = m0 + 192 + 8 * wave + lr < M;
+  const bool b1_ok0 = n0 + 64 * (wave >> 2) + 32 + 8 * (wave & 3) + lr < N;
+  const bool b1_ok1 = n0 + 64 * ((wave >> 2) + 2) + 32 + 8 * (wave & 3) + lr < N;
+  const int64_t a1_off0 = a1_ok0 ? 64 * lda : 0, a1_off1 = a1_ok1 ? 64 * lda : 0;
+  const int64_t b1_off0 = b1_ok0 ? 32 * ldb : 0, b1_off1 = b1_ok1 ? 32 * ldb : 0;
+
+  // half-tile h (0 = A0, 1 = B0, 2 = B1, 3 = A1: consumption order) of K-tile kt -> buffer kt & 1
+  auto issue = [&](int h, int kt) {
+    char* img = smem + (kt & 1) * BUF + (h == 0 ? 0 : h == 3 ? HALF : h == 1 ? 2 * HALF : 3 * HALF);
+    const int64_t dk = (int64_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16_t* src;
+      if (h == 0) src = pa[j] + dk;
+      else if (h == 3) src = pa[j] + dk + (j ? a1_off1 : a1_off0);
+      else if (h == 1) src = pb[j] + dk;
+      else src = pb[j] + dk + (j ? b1_off1 : b1_off0);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(img + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
+
+  // prologue: all of K-tile 0; A0/B0 (read by phase 1) retired
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  wait_vmcnt<4>();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+  asm volatile("" ::: "memory");
+
+  bf16x8 af[2][4], b0[4], b1[4];
+  const int rA = wr * 64 + l32;   // image row of this wave's quadrant row-block 0
+  const int rB = wc * 32 + l32;
+
+#define G3_MFMA(I0, BF, CI)                                                           \
+  __builtin_amdgcn_sched_barrier(0);                                                  \
+  __builtin_amdgcn_s_setprio(1);                                                      \
+  _Pragma("unroll") for (int s_ = 0; s_ < 4; ++s_) {                                  \
+    acc[I0][CI] = mfma32(af[0][s_], BF[s_], acc[I0][CI]);                             \
+    acc[I0 + 1][CI] = mfma32(af[1][s_], BF[s_], acc[I0 + 1][CI]);                     \
+  }                                                                                   \
+  __builtin_amdgcn_s_setprio(0);                                                      \
+  __builtin_amdgcn_sched_barrier(0);
+#define G3_BAR()                          \
+  asm volatile("" ::: "memory");          \
+  __builtin_amdgcn_s_barrier();           \
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const bool more = t + 1 < nk;
+    // ---- phase 1: A0 x B0
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_) {
+      af[0][s_] = frag<false, BM>(buf, rA, s_, hl);
+      af[1][s_] = frag<false, BM>(buf, rA + 32, s_, hl);
+      b0[s_] = frag<false, BN>(buf + 2 * HALF, rB, s_, hl);
+    }
+    if (more) { issue(0, t + 1); wait_vmcnt<4>(); } else { wait_vmcnt<2>(); }   // B1(t) landed
+    G3_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G3_MFMA(0, b0, 0);
+    G3_BAR();
+    // ---- phase 2: A0 x B1
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_) b1[s_] = frag<false, BN>(buf + 3 * HALF, rB, s_, hl);
+    if (more) { issue(1, t + 1); wait_vmcnt<4>(); } else { wait_vmcnt<0>(); }   // A1(t) landed
+    G3_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G3_MFMA(0, b1, 1);
+    G3_BAR();
+    // ---- phase 3: A1 x B0
+#pragma unroll
+    for (int s_ = 0; s_ < 4; ++s_) {
+      af[0][s_] = frag<false, BM>(buf + HALF, rA, s_, hl);
+      af[1][s_] = frag<false, BM>(buf + HALF, rA + 32, s_, hl);
+    }
+    if (more) issue(2, t + 1);
+    G3_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G3_MFMA(2, b0, 0);
+    G3_BAR();
+    // ---- phase 4: A1 x B1; A0/B0 of K-tile t+1 retired for the next phase 1
+    if (more) { issue(3, t + 1); wait_vmcnt<4>(); }
+    G3_BAR();
+    G3_MFMA(2, b1, 1);
+    G3_BAR();
+  }
+#undef G3_MFMA
+#undef G3_BAR
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
+  __syncthreads();
+  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, M, N, ldc, ldr, ldx, alpha,
+                                     nsplit);
+}
+
+template <int EPI, bool ACC>
+static int launch3(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M, int N, int K,
+                   int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
+                   hipStream_t st) {
+  constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
+  constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
+  constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
+  auto kern = gemm3_kernel<EPI, ACC>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int nwg = ((M + 255) / 256) * ((N + 255) / 256);
+  kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
+                                          (const bf16_t*)R, (bf16_t*)X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
+  return (int)hipGetLastError();
 }
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
@@ -371,6 +570,9 @@ template <bool TA, bool TB, int EPI, bool ACC>
 static int dispatch(int cfg, const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M,
                     int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
                     int split, hipStream_t st) {
+  if constexpr (!TA && !TB) {
+    if (cfg == 4) return launch3<EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+  }
   switch (cfg) {
     case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
     case 1: return launch<256, 192, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
@@ -387,7 +589,11 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
   int split = 1;
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
-  if (force_cfg >= 0 && force_cfg < 4) cfg = force_cfg;
+  if (force_cfg >= 0 && force_cfg < 5) cfg = force_cfg;
+  // the ping-pong 256x256 engine for both-K-contiguous operands (MIPIPE_GEMM3=0 disables)
+  static const bool use3 = [] { const char* e = getenv("MIPIPE_GEMM3"); return !(e && e[0] == '0'); }();
+  if (cfg == 0 && !transA && !transB && use3 && force_cfg < 0) cfg = 4;
+  if (cfg == 4 && (transA || transB)) cfg = 0;
   if ((transA || transB) && cfg == 1) cfg = 2;
   if (!c_f32_accum) split = 1;
 #define MP_G(TA_, TB_, E_, ACC_)                                                                                  \

@@ -231,9 +231,10 @@ def test_adamw():
     assert abs(ss.item() - (g.double() ** 2).sum().item()) / ss.item() < 1e-4
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, "bias_gelu"), (1000, 2304, 256, "bias"), (256, 384, 128, "res"),
-                                       (520, 136, 64, "none"), (512, 768, 3072, "dgelu")])
+                                       (520, 136, 64, "none"), (512, 768, 3072, "dgelu"), (1000, 1000, 640, "none"),
+                                       (768, 512, 128, "bias")])
 def test_gemm2_configs(cfg, M, N, K, epi):
     from mipipe.ops import kernels as _k
     torch.manual_seed(0)
@@ -270,6 +271,19 @@ def test_gemm2_dw_splitk(cfg, M, N, K):
     g = base.clone().to(DEV)
     _k._gemm(dy.to(DEV), x.to(DEV), g, transA=True, transB=True, accum=True, cfg=cfg)
     close(g, base + dy.float().t() @ x.float(), atol=3e-2, rtol=1e-2)
+
+
+@pytest.mark.parametrize("cfg", [-1, 1, 4])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 50304), (2048, 768, 8192), (300, 200, 4096)])
+def test_gemm2_nt_splitk_accumulate(cfg, M, N, K):
+    """Both-K-contiguous operands into an f32 accumulator with split-K (distributed-head dX)."""
+    from mipipe.ops import kernels as _k
+    torch.manual_seed(0)
+    a, b = rnd(M, K, scale=0.1), rnd(N, K)
+    base = torch.randn(M, N)
+    g = base.clone().to(DEV)
+    _k._gemm(a.to(DEV), b.to(DEV), g, accum=True, cfg=cfg)
+    close(g, base + a.float() @ b.float().t(), atol=5e-2, rtol=1e-2)
 
 
 def test_linear_dx_with_transposed_weight():

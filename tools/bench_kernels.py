@@ -52,6 +52,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--cfg", type=int, default=-1, help="force a gemm2 tile config (4 = ping-pong 256x256)")
     a = ap.parse_args()
     dev = "cuda"
     res = {}
@@ -64,7 +65,7 @@ def main():
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             w = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * K ** -0.5
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            ours = lambda: _k._gemm(x, w, y)
+            ours = lambda: _k._gemm(x, w, y, cfg=a.cfg)
             lib = lambda: torch.mm(x, w.t(), out=y)
         elif kind == "fwdgelu":  # a = x w^T + b; y = gelu(a)   (fused epilogue vs addmm + gelu)
             x = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
@@ -72,21 +73,21 @@ def main():
             b = torch.randn(N, device=dev, dtype=torch.bfloat16)
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             aux = torch.empty_like(y)
-            ours = lambda: _k._gemm(x, w, y, bias=b, aux=aux, epi=_k.EPI_BIAS_GELU)
+            ours = lambda: _k._gemm(x, w, y, bias=b, aux=aux, epi=_k.EPI_BIAS_GELU, cfg=a.cfg)
             lib = lambda: F.gelu(torch.addmm(b, x, w.t(), out=aux), approximate="tanh")
         elif kind == "dxdgelu":  # da = (dy W) * gelu'(a)
             dy = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             wt = torch.randn(N, K, device=dev, dtype=torch.bfloat16) * K ** -0.5
             aux = torch.randn(M, N, device=dev, dtype=torch.bfloat16)
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            ours = lambda: _k._gemm(dy, wt, y, aux=aux, epi=_k.EPI_DGELU)
+            ours = lambda: _k._gemm(dy, wt, y, aux=aux, epi=_k.EPI_DGELU, cfg=a.cfg)
             lib = lambda: torch.mm(dy, wt.t(), out=y).mul_(aux)
         elif kind == "dx":  # dx[M,N] = dy[M,K] w[K,N]
             dy = torch.randn(M, K, device=dev, dtype=torch.bfloat16)
             w = torch.randn(K, N, device=dev, dtype=torch.bfloat16) * K ** -0.5
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             wt = w.t().contiguous()   # the arena keeps W^T: dX runs as an NT GEMM
-            ours = lambda: _k._gemm(dy, wt, y)
+            ours = lambda: _k._gemm(dy, wt, y, cfg=a.cfg)
             lib = lambda: torch.mm(dy, w, out=y)
         else:               # dw[M,N] += dy[K,M]^T x[K,N]  (f32 accumulate)
             dy = torch.randn(K, M, device=dev, dtype=torch.bfloat16)
