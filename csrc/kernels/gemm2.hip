@@ -97,7 +97,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // ---- epilogue: one wave-row group at a time through LDS -> coalesced 16-byte bias /
 // residual / activation / store, or lane-consecutive f32 atomics for split-K
-template <int BM, int BN, int WM, int WN, int EPI, bool ACC>
+template <int BM, int BN, int WM, int WN, int EPI, bool ACC, int NTH = NT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 32], char* smem, int m0, int n0, int wr,
                                          int wn, int hl, int l32, void* __restrict__ Cv,
                                          const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
@@ -126,7 +126,7 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 3
     if constexpr (ACC) {
       if (nsplit > 1) {
         float* C = reinterpret_cast<float*>(Cv);
-        for (int idx = threadIdx.x; idx < RG * BN; idx += NT) {
+        for (int idx = threadIdx.x; idx < RG * BN; idx += NTH) {
           const int row = idx / BN, col = idx % BN;
           const int gr = rbase + row, gc = n0 + col;
           if (gr < M && gc < N) atomicAdd(C + (int64_t)gr * ldc + gc, alpha * ct[row * CP + col]);
@@ -135,7 +135,7 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 3
         continue;
       }
     }
-    for (int idx = threadIdx.x; idx < RG * BN / 8; idx += NT) {
+    for (int idx = threadIdx.x; idx < RG * BN / 8; idx += NTH) {
       const int row = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
       const int gr = rbase + row, gc = n0 + c8;
       if (gr >= M || gc >= N) continue;
@@ -507,6 +507,7 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   return (int)hipGetLastError();
 }
 
+
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
 static int launch(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M, int N, int K,
                   int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
@@ -593,7 +594,7 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   // the ping-pong 256x256 engine for both-K-contiguous operands (MIPIPE_GEMM3=0 disables)
   static const bool use3 = [] { const char* e = getenv("MIPIPE_GEMM3"); return !(e && e[0] == '0'); }();
   if (cfg == 0 && !transA && !transB && use3 && force_cfg < 0) cfg = 4;
-  if (cfg == 4 && (transA || transB)) cfg = 0;
+  if (cfg >= 4 && (transA || transB)) cfg = 0;
   if ((transA || transB) && cfg == 1) cfg = 2;
   if (!c_f32_accum) split = 1;
 #define MP_G(TA_, TB_, E_, ACC_)                                                                                  \
