@@ -25,7 +25,9 @@ the measured pipeline bubble (1 - busy / step time).
 """
 from __future__ import annotations
 
+import contextlib
 import logging
+import os
 import time
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -33,6 +35,7 @@ import torch
 import torch.distributed as dist
 
 from .comm import P2P
+from .debug import DepTracker, debug_level
 from .headsplit import HeadPlan
 from .ir import Action, CommGroup, Entry, Op, format_compute_grid
 from .lower import lower
@@ -81,12 +84,32 @@ class _Timer:
         return tl, total
 
 
+class _Range:
+    """roctx range (rocprofv3 --marker-trace) + torch.profiler record_function."""
+
+    def __init__(self, name: str):
+        self.name = name
+        self.rf = torch.autograd.profiler.record_function(name)
+
+    def __enter__(self):
+        self.rf.__enter__()
+        if torch.cuda.is_available():
+            torch.cuda.nvtx.range_push(self.name)
+        return self
+
+    def __exit__(self, *exc):
+        if torch.cuda.is_available():
+            torch.cuda.nvtx.range_pop()
+        return self.rf.__exit__(*exc)
+
+
 class PipelineRuntime:
     def __init__(self, stages: Sequence[StageBase], schedule: str, n_microbatches: int, pp_rank: int,
                  pp_size: int, p2p: P2P, loss_fn: Optional[Callable] = None, scale_grads: bool = True,
                  style: str = "loop", program: Optional[Dict[int, List[Entry]]] = None, profile: bool = False,
                  orders: Optional[Dict[int, List[Action]]] = None, head: Optional[HeadPlan] = None,
-                 head_costs: Optional[Dict[int, float]] = None, stage_costs: Optional[Sequence[float]] = None):
+                 head_costs: Optional[Dict[int, float]] = None, stage_costs: Optional[Sequence[float]] = None,
+                 debug: Optional[int] = None):
         self.stages: Dict[int, StageBase] = {s.stage_index: s for s in stages}
         self.schedule = canonical_name(schedule)
         self.m = n_microbatches
@@ -127,6 +150,10 @@ class PipelineRuntime:
         self._recv_bufs: Dict[tuple, List[torch.Tensor]] = {}
         self._dh_full: Dict[int, torch.Tensor] = {}
         self.head_losses: Dict[int, torch.Tensor] = {}
+        lvl = debug_level() if debug is None else int(debug)
+        self.deps: Optional[DepTracker] = DepTracker(pp_rank, lvl) if lvl > 0 else None
+        # roctx / torch.profiler ranges per action ("PP:<action>", as torch schedules.py:2245)
+        self.ranges = os.environ.get("MIPIPE_RANGES", "0") == "1"
 
     # ------------------------------------------------------------------ init
     def _needs_inference(self) -> bool:
@@ -225,9 +252,28 @@ class PipelineRuntime:
         if self.profile:
             self.timer.begin_step()
 
+        deps = self.deps
+
         def wait_recv(key):
             for w in recv_works.pop(key, []):
                 w.wait()
+            if deps is not None:
+                deps.on_wait(key)
+
+        def read_recv(key, action):
+            if deps is not None:
+                deps.on_read(key, action)
+            return self._recv_buf(key)
+
+        def produce(key, tensors, action, local):
+            if deps is not None:
+                deps.on_produce(key, action, tensors)
+            (handoff if local else send_tensors)[key] = tensors
+
+        def rng(a):
+            if not self.ranges:
+                return contextlib.nullcontext()
+            return _Range(f"PP:{a}")
 
         for idx, e in enumerate(self.program):
             try:
@@ -235,10 +281,14 @@ class PipelineRuntime:
                     sends, recvs, rkeys = [], [], []
                     for op in e.ops:
                         if op.action.op.is_send:
+                            if deps is not None:
+                                deps.on_send(op.key, send_tensors)
                             ts = send_tensors.pop(op.key)
                             sends += [(t, op.peer) for t in ts]
                             send_keep.append(ts)
                         else:
+                            if deps is not None:
+                                deps.on_post_recv(op.key)
                             bufs = self._recv_buf(op.key)
                             recvs += [(t, op.peer) for t in bufs]
                             rkeys += [op.key] * len(bufs)
@@ -255,85 +305,16 @@ class PipelineRuntime:
                         reduce_works.append(w)
                     continue
                 t_s = self.timer.mark() if self.profile else None
-                if a.op == Op.F:
-                    key = ("F", a.stage, a.mb)
-                    if a.stage == 0:
-                        args = tuple(inputs[a.mb])
-                    elif key in handoff:
-                        args = handoff.pop(key)
-                    else:
-                        wait_recv(key)
-                        args = tuple(self._recv_buf(key))
-                    tgt = targets[a.mb] if (st.is_last and targets is not None) else None
-                    out, loss = st.forward_mb(a.mb, args, tgt, self.loss_fn, loss_scale)
-                    if st.is_last and head is not None:
-                        # scatter the final-norm rows to the head chunks
-                        hn = out[0]
-                        for r in head.ranks:
-                            hk = ("H", r, a.mb)
-                            piece = (hn[head.rows(r)],)
-                            if r == self.rank:
-                                handoff[hk] = piece
-                            else:
-                                send_tensors[hk] = piece
-                    elif st.is_last:
-                        if return_outputs:
-                            outputs[a.mb] = out
-                        if loss is not None:
-                            mb_losses[a.mb] = loss
-                    else:
-                        nk = ("F", a.stage + 1, a.mb)
-                        if self.s2r[a.stage + 1] == self.rank:
-                            handoff[nk] = out
-                        else:
-                            send_tensors[nk] = out
-                elif a.op == Op.H:
-                    hk = ("H", a.stage, a.mb)
-                    if hk in handoff:
-                        (h_in,) = handoff.pop(hk)
-                    else:
-                        wait_recv(hk)
-                        (h_in,) = self._recv_buf(hk)
-                    rows = head.rows(a.stage)
-                    tgt = targets[a.mb].reshape(-1)[rows]
-                    local_last = self.s2r[S - 1] == self.rank
-                    if local_last:
-                        dh = self._dh_buf(a.mb)[rows]
-                    else:
-                        dh = torch.empty_like(h_in)
-                    loss_sum = head.runner(h_in, tgt, dh, loss_scale / head.tokens)
-                    self.head_losses[a.mb] = loss_sum
-                    if not local_last:
-                        send_tensors[("D", a.stage, a.mb)] = (dh,)
-                elif a.op in (Op.B, Op.I):
-                    key = ("B", a.stage, a.mb)
-                    if a.stage == S - 1 and head is not None:
-                        for r in head.ranks:
-                            if r != self.rank:
-                                wait_recv(("D", r, a.mb))
-                        g = (self._dh_full.pop(a.mb),)
-                    elif a.stage == S - 1:
-                        g = None
-                    elif key in handoff:
-                        g = handoff.pop(key)
-                    else:
-                        wait_recv(key)
-                        g = tuple(self._recv_buf(key))
-                    gin = st.backward_mb(a.mb, g) if a.op == Op.B else st.backward_input_mb(a.mb, g)
-                    if a.stage > 0:
-                        nk = ("B", a.stage - 1, a.mb)
-                        gin = tuple(x for x in gin if x is not None)
-                        if self.s2r[a.stage - 1] == self.rank:
-                            handoff[nk] = gin
-                        else:
-                            send_tensors[nk] = gin
-                elif a.op == Op.W:
-                    st.backward_weight_mb(a.mb)
+                with rng(a):
+                    self._run_compute(a, st, inputs, targets, return_outputs, loss_scale, handoff, outputs,
+                                      mb_losses, wait_recv, read_recv, produce)
                 if self.profile:
                     self.timer.add(a, t_s, self.timer.mark())
             except Exception:
                 self._report_failure(idx)
                 raise
+        if deps is not None:
+            deps.finish(send_tensors, handoff)
         for w in send_keep:
             if hasattr(w, "wait"):
                 w.wait()
@@ -349,6 +330,71 @@ class PipelineRuntime:
         if self.stages.get(S - 1) is not None and return_outputs:
             return [outputs[i] for i in sorted(outputs)]
         return None
+
+    def _run_compute(self, a: Action, st, inputs, targets, return_outputs, loss_scale, handoff, outputs, mb_losses,
+                     wait_recv, read_recv, produce) -> None:
+        """One compute action: gather its inputs (same-rank hand-off or a waited receive),
+        run it, and publish its outputs (hand-off or pending send)."""
+        S = self.num_stages
+        head = self.head
+        if a.op == Op.F:
+            key = ("F", a.stage, a.mb)
+            if a.stage == 0:
+                args = tuple(inputs[a.mb])
+            elif key in handoff:
+                args = handoff.pop(key)
+            else:
+                wait_recv(key)
+                args = tuple(read_recv(key, a))
+            tgt = targets[a.mb] if (st.is_last and targets is not None) else None
+            out, loss = st.forward_mb(a.mb, args, tgt, self.loss_fn, loss_scale)
+            if st.is_last and head is not None:
+                # scatter the final-norm rows to the head chunks
+                hn = out[0]
+                for r in head.ranks:
+                    produce(("H", r, a.mb), (hn[head.rows(r)],), a, r == self.rank)
+            elif st.is_last:
+                if return_outputs:
+                    outputs[a.mb] = out
+                if loss is not None:
+                    mb_losses[a.mb] = loss
+            else:
+                produce(("F", a.stage + 1, a.mb), out, a, self.s2r[a.stage + 1] == self.rank)
+        elif a.op == Op.H:
+            hk = ("H", a.stage, a.mb)
+            if hk in handoff:
+                (h_in,) = handoff.pop(hk)
+            else:
+                wait_recv(hk)
+                (h_in,) = read_recv(hk, a)
+            rows = head.rows(a.stage)
+            tgt = targets[a.mb].reshape(-1)[rows]
+            local_last = self.s2r[S - 1] == self.rank
+            dh = self._dh_buf(a.mb)[rows] if local_last else torch.empty_like(h_in)
+            self.head_losses[a.mb] = head.runner(h_in, tgt, dh, loss_scale / head.tokens)
+            if not local_last:
+                produce(("D", a.stage, a.mb), (dh,), a, False)
+        elif a.op in (Op.B, Op.I):
+            key = ("B", a.stage, a.mb)
+            if a.stage == S - 1 and head is not None:
+                for r in head.ranks:
+                    if r != self.rank:
+                        wait_recv(("D", r, a.mb))
+                        read_recv(("D", r, a.mb), a)
+                g = (self._dh_full.pop(a.mb),)
+            elif a.stage == S - 1:
+                g = None
+            elif key in handoff:
+                g = handoff.pop(key)
+            else:
+                wait_recv(key)
+                g = tuple(read_recv(key, a))
+            gin = st.backward_mb(a.mb, g) if a.op == Op.B else st.backward_input_mb(a.mb, g)
+            if a.stage > 0:
+                gin = tuple(x for x in gin if x is not None)
+                produce(("B", a.stage - 1, a.mb), gin, a, self.s2r[a.stage - 1] == self.rank)
+        elif a.op == Op.W:
+            st.backward_weight_mb(a.mb)
 
     # ------------------------------------------------------------------ diagnostics
     def bubble(self) -> float:
