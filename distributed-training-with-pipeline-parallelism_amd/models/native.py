@@ -472,13 +472,29 @@ class Block:
 # ======================================================================================
 
 
+# Sustained rates of this engine's kernels on MI355X (profiles/r1_v2_*, r1_v1_kernel_microbench):
+# the projection GEMMs of a layer run at ~700 TF/s, the big-N head GEMMs at ~850, flash
+# attention at ~230 fwd / ~180 bwd (D=64) and the fused CE streams logits at ~4 TB/s.
+_E_GEMM, _E_HEAD, _E_ATTN_F, _E_ATTN_B, _BW_CE = 700e12, 850e12, 230e12, 180e12, 4.0e12
+
+
 def stage_cost_model(cfg: NativeConfig, seq_len: int = 1024) -> Tuple[float, float, float]:
-    """(layer, head, embedding) costs in layer units (forward FLOPs; the head includes
-    its CE / final-norm overhead)."""
+    """(layer, head, embedding) costs in forward-layer units: the pipeline simulator
+    prices F = 1, B = 2 per layer unit and a head chunk at 3 x its share of the head.
+
+    Costs are *time* estimates from per-kernel sustained rates, not FLOP ratios: the
+    LM head is one large, efficient GEMM family while a layer mixes smaller GEMMs with
+    attention, so FLOPs alone overprice the head (GPT-2 small: 5.2 vs ~3.3 measured)."""
     d = cfg.d_model
-    layer_cost = (cfg.flops_per_token(seq_len) / 3.0 - 2 * d * cfg.vocab_size) / cfg.n_layers
-    head_cost = (2 * d * cfg.vocab_padded) / layer_cost + 0.3
-    return 1.0, head_cost, 0.1
+    mm = d * cfg.qkv_dim + d * d + (3 if cfg.activation == "swiglu" else 2) * d * cfg.d_ff
+    attn = 2.0 * seq_len * d * (0.5 if cfg.causal else 1.0)
+    if cfg.cross_attn:
+        mm += 4 * d * d
+        attn *= 2
+    t_layer = 3 * 2 * mm / _E_GEMM + 2 * attn / _E_ATTN_F + 2.5 * 2 * attn / _E_ATTN_B   # fwd + bwd, per token
+    t_head = 3 * 2 * d * cfg.vocab_padded / _E_HEAD + 2 * 2 * cfg.vocab_padded / _BW_CE
+    head_units = t_head / t_layer
+    return 1.0, head_units + 0.1, 0.1
 
 
 def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 1024,
