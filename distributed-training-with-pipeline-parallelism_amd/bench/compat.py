@@ -190,3 +190,65 @@ def compute_speedup_and_efficiency(df):
             out.append(dict(n_layers=L, n_heads=H, num_processes=P, schedule=row["schedule"],
                             throughput=row["throughput"], speedup=sp, efficiency=sp / P * 100))
     return pd.DataFrame(out)
+
+
+def throughput_pivot(df):
+    """Mean throughput by (layers, heads) x (schedule, processes) -- the notebook's
+    summary table (nb:766-782)."""
+    return df.pivot_table(index=["n_layers", "n_heads"], columns=["schedule", "num_processes"], values="throughput",
+                          aggfunc="mean")
+
+
+def plot_speedup_efficiency(eff_df, path: str) -> None:
+    """1x2 figure: speedup vs GPipe and 'efficiency' per L{L}_H{H} config (nb:880-941)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    fig, axes = plt.subplots(1, 2, figsize=(14, 5))
+    for (sched, P), g in eff_df.groupby(["schedule", "num_processes"]):
+        labels = [f"L{l}_H{h}" for l, h in zip(g["n_layers"], g["n_heads"])]
+        axes[0].plot(labels, g["speedup"], marker="o", label=f"{sched} P={P}")
+        axes[1].plot(labels, g["efficiency"], marker="o", label=f"{sched} P={P}")
+    axes[0].set_title("speedup vs GPipe")
+    axes[1].set_title("efficiency = speedup / P x 100")
+    for ax in axes:
+        ax.tick_params(axis="x", rotation=45)
+        ax.legend(fontsize=8)
+    fig.tight_layout()
+    fig.savefig(path)
+    plt.close(fig)
+
+
+def plot_throughput(df, path: str) -> None:
+    """Grid of throughput vs processes per (L, H), one line per schedule (nb:972-1002)."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    Ls, Hs = sorted(df["n_layers"].unique()), sorted(df["n_heads"].unique())
+    fig, axes = plt.subplots(len(Ls), len(Hs), figsize=(4 * len(Hs), 3 * len(Ls)), squeeze=False)
+    for i, L in enumerate(Ls):
+        for j, H in enumerate(Hs):
+            ax = axes[i][j]
+            g = df[(df["n_layers"] == L) & (df["n_heads"] == H)]
+            for sched, gs in g.groupby("schedule"):
+                gs = gs.sort_values("num_processes")
+                ax.plot(gs["num_processes"], gs["throughput"], marker="o", label=sched)
+            ax.set_title(f"L={L} H={H}")
+            ax.set_xlabel("processes")
+            ax.set_ylabel("tok/s")
+            ax.legend(fontsize=7)
+    fig.tight_layout()
+    fig.savefig(path)
+    plt.close(fig)
+
+
+def environment_report() -> dict:
+    """Torch / ROCm / device report (the notebook's environment cell, nb:256-259)."""
+    import os as _os
+    rep = {"torch": torch.__version__, "hip": getattr(torch.version, "hip", None),
+           "gpu_available": torch.cuda.is_available(), "cpu_count": _os.cpu_count()}
+    if torch.cuda.is_available():
+        rep["devices"] = [torch.cuda.get_device_name(i) for i in range(torch.cuda.device_count())]
+    for k, v in rep.items():
+        print(f"{k}: {v}")
+    return rep

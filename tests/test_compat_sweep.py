@@ -1,0 +1,39 @@
+"""Reference-compatible experiment API: the notebook's launcher,
+sweep, speedup/efficiency analysis, pivot table, plots and environment report, on
+CPU/gloo (the reference's own configuration), both engines."""
+import os
+
+import pytest
+
+import mipipe  # noqa: F401
+from mipipe.bench import compat
+
+
+@pytest.mark.parametrize("engine", ["torch", "native"])
+def test_run_one_experiment(engine):
+    m = compat.run_one_experiment(4, 4, 2, "1F1B", batch_size=8, seq_length=16, num_iterations=1, device="cpu",
+                                  engine=engine, timeout=300)
+    assert "error" not in m, m
+    assert m["tokens_processed"] == 8 * 16 * 1 and m["throughput"] > 0
+
+
+def test_unknown_schedule_reports_error():
+    m = compat.run_one_experiment(4, 4, 2, "NoSuchSchedule", batch_size=8, seq_length=16, num_iterations=1,
+                                  device="cpu", timeout=120)
+    assert "error" in m
+
+
+def test_sweep_analysis_tables_and_plots(tmp_path):
+    df = compat.run_all_experiments(n_heads_list=(4,), n_layers_list=(4,), num_processes_list=(2,),
+                                    schedules=("GPipe", "1F1B", "Interleaved1F1B"), num_iterations=1,
+                                    batch_size=8, seq_length=16, device="cpu", timeout=300)
+    assert len(df) == 3 and set(df["schedule"]) == {"GPipe", "1F1B", "Interleaved1F1B"}
+    eff = compat.compute_speedup_and_efficiency(df)
+    assert len(eff) == 2 and (eff["efficiency"] == eff["speedup"] / 2 * 100).all()
+    piv = compat.throughput_pivot(df)
+    assert piv.shape == (1, 3)
+    compat.plot_speedup_efficiency(eff, str(tmp_path / "eff.png"))
+    compat.plot_throughput(df, str(tmp_path / "thr.png"))
+    assert os.path.getsize(tmp_path / "eff.png") > 0 and os.path.getsize(tmp_path / "thr.png") > 0
+    rep = compat.environment_report()
+    assert "torch" in rep and rep["cpu_count"] > 0
