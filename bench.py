@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--dp", type=int, default=1)
     ap.add_argument("--v", type=int, default=None, help="virtual stages per rank (interleaved)")
     ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--graphs", type=int, default=1, help="replay per-microbatch stage compute as HIP graphs")
     ap.add_argument("--no-split-head", action="store_true",
                     help="keep the LM head on the last stage (default with PP>1: distributed head)")
     ap.add_argument("--no-bubble", action="store_true", help="skip the profiled bubble-measurement step")
@@ -78,11 +79,14 @@ def main():
     cfg = NativeConfig.by_name(a.model)
     trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m,
                               mbs=a.mbs, seq_len=a.seq, v=a.v, device=device, recompute=a.recompute, seed=0,
-                              split_head=False if a.no_split_head else None)
+                              split_head=False if a.no_split_head else None, graphs=bool(a.graphs))
     gb = dp * m * a.mbs
     g = torch.Generator(device=device).manual_seed(1234 + trainer.mesh.dp_rank)
     tokens = torch.randint(0, cfg.vocab_size, (m * a.mbs, a.seq), device=device, generator=g)
     targets = torch.randint(0, cfg.vocab_size, (m * a.mbs, a.seq), device=device, generator=g)
+
+    if a.graphs:
+        trainer.capture_graphs(tokens, targets)   # setup: capture per-microbatch HIP graphs
 
     def sync():
         if world > 1:
@@ -145,6 +149,7 @@ def main():
                    "micro_batch": a.mbs, "microbatches": m, "schedule": trainer.schedule, "v": trainer.v,
                    "parallelism": f"pp{pp}" + (f"_dp{dp}" if dp > 1 else ""),
                    "layer_split": trainer.layer_ranges, "optimizer": "AdamW(fused, clip 1.0)",
+                   "hip_graphs": bool(a.graphs),
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
                    else "last stage"},
     }

@@ -83,7 +83,7 @@ class PipelineTrainer:
                  device=None, lr: float = 3e-4, weight_decay: float = 0.1, max_grad_norm: float = 1.0,
                  recompute: bool = False, profile: bool = False, seed: int = 0, style: str = "loop",
                  mesh: Optional[Mesh] = None, layer_ranges=None, dtype=torch.bfloat16,
-                 split_head: Optional[bool] = None, head_align: Optional[int] = None):
+                 split_head: Optional[bool] = None, head_align: Optional[int] = None, graphs: bool = False):
         self.cfg = cfg
         self.schedule = canonical_name(schedule)
         if v is None:
@@ -123,6 +123,9 @@ class PipelineTrainer:
             orders, self.head_lag, self.planned_makespan = plan_head_schedule(base, pp, v, style, head_costs,
                                                                               stage_costs)
             head_plan = HeadPlan(chunks, cfg.d_model, runner=self.head.run, dtype=dtype)
+            if graphs and self.device.type == "cuda":
+                from .parallel.graphs import GraphCache
+                head_plan.graphs = GraphCache()
             self.head_chunks = chunks
         self.stages: List[NativeStage] = []
         for s in my_stages:
@@ -130,7 +133,7 @@ class PipelineTrainer:
                                 recompute=recompute, mbs=mbs, seq_len=seq_len, dtype=dtype, head=self.head)
             egroup = self.mesh.embed_group if (tied_pp and (s == 0 or s == num_stages - 1)) else None
             self.stages.append(NativeStage(model, mbs, seq_len, dp_group=self.mesh.dp_group, embed_group=egroup,
-                                           seed=seed + 1000 * self.mesh.dp_rank))
+                                           seed=seed + 1000 * self.mesh.dp_rank, graphs=graphs))
         p2p = P2P(self.mesh.pp_group, self.mesh.pipe_ranks, self.device)
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
                                        scale_grads=True, style=style, profile=profile, orders=orders,
@@ -181,6 +184,19 @@ class PipelineTrainer:
         if losses:
             return torch.stack(losses).mean()
         return None
+
+    def capture_graphs(self, tokens: Optional[torch.Tensor] = None, targets: Optional[torch.Tensor] = None) -> None:
+        """Setup, not training: run the pipeline program twice without an optimizer step
+        (eager lazy-init, then HIP-graph capture of every per-microbatch action) and
+        discard the gradients.  Later ``train_step`` calls replay the graphs."""
+        if not any(st.graphs is not None for st in self.stages):
+            return
+        inputs = [(c,) for c in torch.tensor_split(tokens, self.m, dim=0)] if self.is_first else None
+        tg = list(torch.tensor_split(targets, self.m, dim=0)) if self.is_last else None
+        while min(st.step_id for st in self.stages) < 2:
+            self.runtime.step(inputs, tg, [], return_outputs=False)
+        for a in self.optimizer.arenas:
+            a.grad.zero_()
 
     def bubble(self) -> float:
         return self.runtime.bubble()

@@ -7,6 +7,7 @@ import torch
 import torch.distributed as dist
 
 from ..parallel.dp import allreduce_flat
+from ..parallel.graphs import GraphCache
 from ..parallel.stage import StageBase
 from .config import NativeConfig
 from .native import MBContext, NativeModel, _seed
@@ -23,7 +24,7 @@ class NativeStage(StageBase):
     """
 
     def __init__(self, model: NativeModel, mbs: int, seq_len: int, dp_group=None, embed_group=None,
-                 seed: int = 1234):
+                 seed: int = 1234, graphs: bool = False):
         self.model = model
         self.cfg: NativeConfig = model.cfg
         self.stage_index = model.stage_index
@@ -46,6 +47,15 @@ class NativeStage(StageBase):
         else:  # hidden states (the last stage's final-norm output with a distributed head)
             self.output_specs = [((T, D), model.arena.dtype)]
         self._ctx = {}
+        # HIP graphs (parallel/graphs.py): step 1 runs eagerly (lazy kernel init), every
+        # (op, microbatch) action is captured on its first later use and replayed after
+        if graphs and (model.device.type != "cuda" or self.cfg.dropout > 0):
+            graphs = False
+        self.graphs = GraphCache() if graphs else None
+        self._gctx = {}
+
+    def _graphed(self) -> bool:
+        return self.graphs is not None and self.step_id > 1
 
     @property
     def arena(self):
@@ -56,6 +66,8 @@ class NativeStage(StageBase):
         self.step_id += 1
 
     def forward_mb(self, mb, args, target, loss_fn, loss_scale):
+        if self._graphed():
+            return self._forward_graphed(mb, args, target, loss_scale)
         ctx = MBContext(mb, _seed(self.seed, self.step_id, mb))
         x = args[0]
         out = self.model.forward(x, ctx, self.mbs, self.S, target=target if self.is_last else None,
@@ -73,19 +85,57 @@ class NativeStage(StageBase):
         return grad_outputs[0]
 
     def backward_mb(self, mb, grad_outputs):
+        if self._graphed():
+            return self._backward_graphed("B", mb, grad_outputs, True)
         ctx = self._ctx.pop(mb)
         dy = self._dy(grad_outputs)
         dx = self.model.backward(dy, ctx, self.mbs, self.S, weight_grads=True)
         return (dx,) if dx is not None else ()
 
     def backward_input_mb(self, mb, grad_outputs):
+        if self._graphed():
+            return self._backward_graphed("I", mb, grad_outputs, False)
         ctx = self._ctx.pop(mb)
         dy = self._dy(grad_outputs)
         dx = self.model.backward(dy, ctx, self.mbs, self.S, weight_grads=False)
         return (dx,) if dx is not None else ()
 
     def backward_weight_mb(self, mb):
+        if self._graphed():
+            self.graphs.run(("W", mb), (), lambda ins: self.model.backward_weight(mb))
+            return
         self.model.backward_weight(mb)
+
+    # ------------------------------------------------------------------ HIP graphs
+    def _forward_graphed(self, mb, args, target, loss_scale):
+        last_loss = self.is_last and not self.split_head and target is not None
+        ins = (args[0],) + ((target,) if last_loss else ())
+
+        def fn(ins):
+            ctx = MBContext(mb, _seed(self.seed, 0, mb))
+            out = self.model.forward(ins[0], ctx, self.mbs, self.S, target=ins[1] if last_loss else None,
+                                     loss_scale=loss_scale)
+            self._gctx[mb] = ctx
+            return out
+
+        out = self.graphs.run(("F", mb), ins, fn, keep=lambda: self._gctx[mb])
+        if self.is_last and not self.split_head:
+            if not last_loss:
+                return (out,), None
+            loss = out.clone()
+            return (loss.detach(),), loss
+        return (out,), None
+
+    def _backward_graphed(self, op, mb, grad_outputs, weight_grads):
+        dy = self._dy(grad_outputs)
+        ins = (dy,) if dy is not None else ()
+
+        def fn(ins):
+            return self.model.backward(ins[0] if ins else None, self._gctx[mb], self.mbs, self.S,
+                                       weight_grads=weight_grads)
+
+        dx = self.graphs.run((op, mb), ins, fn, keep=lambda: self.model.defer_w.get(mb))
+        return (dx,) if dx is not None else ()
 
     def infer_output_specs(self, args):
         return self.output_specs

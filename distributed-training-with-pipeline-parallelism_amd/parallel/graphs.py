@@ -1,0 +1,76 @@
+"""HIP-graph capture of per-microbatch stage compute.
+
+A stage's forward (or backward) for microbatch slot ``mb`` is the same sequence of
+kernel launches on the same buffers every step: static shapes and, with the flat
+parameter arena and persistent receive buffers, static pointers.  :class:`GraphCache`
+captures each such action once (``torch.cuda.CUDAGraph`` = hipGraph on ROCm), then
+replays it with one launch.  That removes the Python/launch overhead (~0.4 ms per
+GPT-2 layer fwd+bwd, measured) that otherwise bounds small microbatches and deep
+pipelines.  Design rules:
+
+* every captured action has its own private memory pool, and all tensors the action
+  saves for a later action (forward activations read by the backward) are kept
+  referenced by the cache, so no later allocation can alias them;
+* inputs are captured by pointer; if a later call passes a tensor at another address
+  (e.g. the user's token chunk) it is copied into the captured buffer first;
+* communication stays outside the graphs (RCCL work is posted by the runtime between
+  replays, and ordered by stream waits), as do optimizer steps whose scalars change.
+
+Graphs are off by default on CPU and for configurations with dropout (the seed is a
+kernel argument and would be frozen into the graph).
+"""
+from __future__ import annotations
+
+from typing import Any, Callable, Dict, Hashable, List, Sequence
+
+import torch
+
+
+def _tensors(obj, out: List[torch.Tensor]) -> List[torch.Tensor]:
+    if isinstance(obj, torch.Tensor):
+        out.append(obj)
+    elif isinstance(obj, dict):
+        for v in obj.values():
+            _tensors(v, out)
+    elif isinstance(obj, (list, tuple)):
+        for v in obj:
+            _tensors(v, out)
+    elif hasattr(obj, "__dict__") and not callable(obj):
+        _tensors(vars(obj), out)
+    return out
+
+
+class GraphCache:
+    def __init__(self):
+        self.graphs: Dict[Hashable, tuple] = {}
+        self.captures = 0
+        self.replays = 0
+
+    def __contains__(self, key) -> bool:
+        return key in self.graphs
+
+    def run(self, key: Hashable, inputs: Sequence[torch.Tensor], fn: Callable[[Sequence[torch.Tensor]], Any],
+            keep: Callable[[], Any] = None) -> Any:
+        """Replay the graph captured for ``key`` (capturing it on first use).  ``keep``
+        returns objects whose tensors must outlive the capture (saved activations)."""
+        entry = self.graphs.get(key)
+        if entry is None:
+            g = torch.cuda.CUDAGraph()
+            torch.cuda.synchronize()
+            with torch.cuda.graph(g):
+                out = fn(inputs)
+            kept = _tensors(keep(), []) if keep is not None else []
+            entry = (g, list(inputs), out, kept)
+            self.graphs[key] = entry
+            self.captures += 1
+        else:
+            g, static_in, out, _ = entry
+            for s, t in zip(static_in, inputs):
+                if s.data_ptr() != t.data_ptr():
+                    s.copy_(t)
+            self.replays += 1
+        entry[0].replay()
+        return entry[2]
+
+    def clear(self) -> None:
+        self.graphs.clear()

@@ -191,6 +191,7 @@ class HeadPlan:
     runner: Optional[Callable] = None
     dtype: object = None
     offsets: List[int] = field(default_factory=list)
+    graphs: object = None   # GraphCache: chunks replayed as HIP graphs after the first step
 
     def __post_init__(self):
         self.offsets = [sum(self.chunks[:r]) for r in range(len(self.chunks))]

@@ -149,6 +149,7 @@ class PipelineRuntime:
         self._initialized = False
         self._recv_bufs: Dict[tuple, List[torch.Tensor]] = {}
         self._dh_full: Dict[int, torch.Tensor] = {}
+        self._steps = 0
         self.head_losses: Dict[int, torch.Tensor] = {}
         lvl = debug_level() if debug is None else int(debug)
         self.deps: Optional[DepTracker] = DepTracker(pp_rank, lvl) if lvl > 0 else None
@@ -246,6 +247,7 @@ class PipelineRuntime:
         mb_losses: Dict[int, torch.Tensor] = {}
         self.head_losses = {}
         head = self.head
+        self._steps += 1
         reduce_works = []
         loss_scale = 1.0 / self.m if self.scale_grads else 1.0
         S = self.num_stages
@@ -370,8 +372,16 @@ class PipelineRuntime:
             rows = head.rows(a.stage)
             tgt = targets[a.mb].reshape(-1)[rows]
             local_last = self.s2r[S - 1] == self.rank
-            dh = self._dh_buf(a.mb)[rows] if local_last else torch.empty_like(h_in)
-            self.head_losses[a.mb] = head.runner(h_in, tgt, dh, loss_scale / head.tokens)
+            scale = loss_scale / head.tokens
+            if head.graphs is not None and self._steps > 1:
+                def fn(ins, local_last=local_last, mb=a.mb):
+                    d = self._dh_buf(mb)[rows] if local_last else torch.empty_like(ins[0])
+                    return d, head.runner(ins[0], ins[1], d, scale)
+                dh, loss = head.graphs.run(("H", a.mb), (h_in, tgt), fn)
+                self.head_losses[a.mb] = loss.clone()
+            else:
+                dh = self._dh_buf(a.mb)[rows] if local_last else torch.empty_like(h_in)
+                self.head_losses[a.mb] = head.runner(h_in, tgt, dh, scale)
             if not local_last:
                 produce(("D", a.stage, a.mb), (dh,), a, False)
         elif a.op in (Op.B, Op.I):
@@ -381,7 +391,7 @@ class PipelineRuntime:
                     if r != self.rank:
                         wait_recv(("D", r, a.mb))
                         read_recv(("D", r, a.mb), a)
-                g = (self._dh_full.pop(a.mb),)
+                g = (self._dh_buf(a.mb),)   # persistent per microbatch (graph-safe)
             elif a.stage == S - 1:
                 g = None
             elif key in handoff:

@@ -80,3 +80,25 @@ def test_head_shard_chunks_vs_f32_reference(tied):
     gw = head.arena.g(head.wname)
     cosw = torch.nn.functional.cosine_similarity(gw.flatten(), W.grad.flatten(), dim=0)
     assert cosw > 0.995
+
+
+@pytest.mark.parametrize("recompute", [False, True])
+def test_hip_graph_replay_matches_eager(recompute):
+    """PP=1 GPT-2-shaped training with per-microbatch HIP graphs == eager, step by step."""
+    from mipipe.engine import PipelineTrainer
+    cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=3, n_heads=4, d_ff=1024, max_seq_len=256)
+    g = torch.Generator().manual_seed(0)
+    x = torch.randint(0, 1000, (4, 256), generator=g).cuda()
+    y = torch.randint(0, 1000, (4, 256), generator=g).cuda()
+    res = {}
+    for graphs in (False, True):
+        tr = PipelineTrainer(cfg, pp=1, n_microbatches=2, mbs=2, seq_len=256, device=torch.device("cuda"),
+                             recompute=recompute, graphs=graphs, seed=5)
+        if graphs:
+            tr.capture_graphs(x, y)
+            assert tr.stages[0].graphs.captures >= 4
+        res[graphs] = ([float(tr.train_step(x, y)) for _ in range(3)], tr.stages[0].arena.master.clone())
+        if graphs:
+            assert tr.stages[0].graphs.replays >= 6
+    assert res[True][0] == res[False][0]
+    assert torch.equal(res[True][1], res[False][1])
