@@ -121,7 +121,7 @@ __device__ __forceinline__ uint64_t drop_idx(int bh, int q, int k, int Sk) {
 // forward
 // ==========================================================================================
 template <int DP, bool CAUSAL, bool DROP>
-__global__ void __launch_bounds__(256, 2) attn_fwd_kernel(
+__global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
     float* __restrict__ LSE, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
     int64_t os, float scale, float p_drop, uint64_t seed) {
@@ -189,27 +189,30 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_kernel(
         s0 = mfma32(a0, qf[s], s0);
         s1 = mfma32(a1, qf[s], s1);
       }
-      // ---- scale, mask, tile max
+      // ---- mask (only tiles that cross the causal diagonal or the key end), tile max on
+      // raw scores; p = 2^(s*c - m) is one v_fma + one v_exp (scale folded, log2 units)
+      const bool edge = (n0 + 64 > Sk) || (CAUSAL && n0 + 63 > m0 + 32 * w + shift);
+      if (edge) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+          const int ka = n0 + kr, kb2 = n0 + 32 + kr;
+          if (ka >= Sk || (CAUSAL && ka > qrow + shift)) s0[r] = -INFINITY;
+          if (kb2 >= Sk || (CAUSAL && kb2 > qrow + shift)) s1[r] = -INFINITY;
+        }
+      }
       float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
-        const int k0 = n0 + kr, k1 = n0 + 32 + kr;
-        float v0 = s0[r] * c, v1 = s1[r] * c;
-        if (k0 >= Sk || (CAUSAL && k0 > qrow + shift)) v0 = -INFINITY;
-        if (k1 >= Sk || (CAUSAL && k1 > qrow + shift)) v1 = -INFINITY;
-        s0[r] = v0;
-        s1[r] = v1;
-        mx = fmaxf(mx, fmaxf(v0, v1));
-      }
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float m_new = fmaxf(m_run, mx);
+      const float m_new = fmaxf(m_run, mx * c);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = exp2f(m_run - m_use);
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
       float rs = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        float p0 = exp2f(s0[r] - m_use), p1 = exp2f(s1[r] - m_use);
+        float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], c, -m_use));
+        float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c, -m_use));
         rs += p0 + p1;
         if (DROP) {
           const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
@@ -391,12 +394,23 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
           pacc = mfma32(ag, vf[s], pacc);
         }
         f32x16 pm, ds;
+        // per-row stats: rows 32u + 8g + 4hl + 0..3 are contiguous -> one 16-byte LDS read
+        float4 lsv[4], dlv[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          lsv[g] = *reinterpret_cast<const float4*>(ls + 32 * u + 8 * g + 4 * hl);
+          dlv[g] = *reinterpret_cast<const float4*>(dl + 32 * u + 8 * g + 4 * hl);
+        }
+        // causal mask only where this wave's keys can exceed the tile's queries; rows past
+        // Sq carry lse = +inf (p = 0) and keys past Sk only feed their own unwritten outputs
+        const bool edge = CAUSAL && (k0 + 32 * w + 31 > q0 + 32 * u + shift);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qr = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl;
           const int q = q0 + qr;
-          float p = exp2f(sacc[r] * c - ls[qr]);
-          if (!kvalid || q >= Sq || (CAUSAL && key > q + shift)) p = 0.f;
+          const float lv = (&lsv[r >> 2].x)[r & 3], dv_ = (&dlv[r >> 2].x)[r & 3];
+          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -lv));
+          if (edge && key > q + shift) p = 0.f;
           float dpv = pacc[r];
           float pd = p;
           if (DROP) {
@@ -405,7 +419,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
             dpv = dpv * msk;
           }
           pm[r] = pd;                      // dropped P for dV
-          ds[r] = p * (dpv - dl[qr]);      // dS
+          ds[r] = p * (dpv - dv_);         // dS
         }
         (void)keep;
         // dV^T += dO^T P ;  dK^T += Q^T dS     (A via transposed LDS reads of the row images)
@@ -460,7 +474,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
 // backward dQ: workgroup = 128 queries of one (b, h) (forward structure)
 // ==========================================================================================
 template <int DP, bool CAUSAL, bool DROP>
-__global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(
+__global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     float* __restrict__ DELTA,
@@ -541,6 +555,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(
         p0 = mfma32(av0, gf[s], p0);  // dP^T = V dO^T
         p1 = mfma32(av1, gf[s], p1);
       }
+      // causal / key-end mask only on edge tiles; invalid query rows have lse = +inf
+      const bool edge = (n0 + 64 > Sk) || (CAUSAL && n0 + 63 > m0 + 32 * w + shift);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
@@ -549,8 +565,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq_kernel(
           const int kk = n0 + 32 * half + kr;
           float sv = half ? s1[r] : s0[r];
           float dpv = half ? p1[r] : p0[r];
-          float p = exp2f(sv * c - lse);
-          if (kk >= Sk || (CAUSAL && kk > qrow + shift) || !qvalid) p = 0.f;
+          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse));
+          if (edge && (kk >= Sk || (CAUSAL && kk > qrow + shift))) p = 0.f;
           if (DROP) dpv *= dropout_scale(seed, drop_idx(bh, qrow, kk, Sk), p_drop);
           const float dsv = p * (dpv - dlt);
           if (half) s1[r] = dsv; else s0[r] = dsv;

@@ -100,5 +100,7 @@ def test_hip_graph_replay_matches_eager(recompute):
         res[graphs] = ([float(tr.train_step(x, y)) for _ in range(3)], tr.stages[0].arena.master.clone())
         if graphs:
             assert tr.stages[0].graphs.replays >= 6
-    assert res[True][0] == res[False][0]
-    assert torch.equal(res[True][1], res[False][1])
+    # split-K dW uses f32 atomics (summation order varies run to run), so equal up to rounding
+    assert res[True][0] == pytest.approx(res[False][0], rel=1e-4)
+    # (Adam turns atomics-order noise of near-zero grads into lr-sized steps)
+    torch.testing.assert_close(res[True][1], res[False][1], atol=2e-3, rtol=1e-3)
