@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--dp", type=int, default=1)
     ap.add_argument("--v", type=int, default=None, help="virtual stages per rank (interleaved)")
     ap.add_argument("--recompute", action="store_true")
-    ap.add_argument("--graphs", type=int, default=1, help="replay per-microbatch stage compute as HIP graphs")
+    ap.add_argument("--graphs", type=int, default=None,
+                    help="replay per-microbatch stage compute as HIP graphs (default: on for 1 GPU)")
     ap.add_argument("--no-split-head", action="store_true",
                     help="keep the LM head on the last stage (default with PP>1: distributed head)")
     ap.add_argument("--no-bubble", action="store_true", help="skip the profiled bubble-measurement step")
@@ -77,6 +78,8 @@ def main():
     pp = world // dp
     m = a.microbatches if a.microbatches is not None else max(2, 2 * pp)
     cfg = NativeConfig.by_name(a.model)
+    if a.graphs is None:
+        a.graphs = 1 if world == 1 else 0
     trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m,
                               mbs=a.mbs, seq_len=a.seq, v=a.v, device=device, recompute=a.recompute, seed=0,
                               split_head=False if a.no_split_head else None, graphs=bool(a.graphs))

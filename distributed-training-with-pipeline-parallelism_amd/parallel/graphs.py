@@ -57,7 +57,8 @@ class GraphCache:
         if entry is None:
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
-            with torch.cuda.graph(g):
+            # thread-local capture: the RCCL watchdog thread may query events meanwhile
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
                 out = fn(inputs)
             kept = _tensors(keep(), []) if keep is not None else []
             entry = (g, list(inputs), out, kept)
