@@ -25,7 +25,7 @@ from .parallel.comm import P2P
 from .parallel.headsplit import HeadPlan, head_token_split, plan_head_schedule
 from .parallel.mesh import Mesh, build_mesh
 from .parallel.runtime import PipelineRuntime
-from .parallel.schedules import SCHEDULES, canonical_name, generate, rank_stages, stage_to_rank
+from .parallel.schedules import REQUIRED_STYLE, SCHEDULES, canonical_name, generate, rank_stages, stage_to_rank
 
 
 class FlatAdamW:
@@ -86,6 +86,8 @@ class PipelineTrainer:
                  split_head: Optional[bool] = None, head_align: Optional[int] = None, graphs: bool = False):
         self.cfg = cfg
         self.schedule = canonical_name(schedule)
+        style = REQUIRED_STYLE.get(self.schedule, style)
+        self.style = style
         if v is None:
             v = SCHEDULES[self.schedule][1]
         if not SCHEDULES[self.schedule][2]:
@@ -105,6 +107,10 @@ class PipelineTrainer:
         self.layer_ranges = layer_ranges
         my_stages = rank_stages(self.mesh.pp_rank, pp, v, style)
         tied_pp = cfg.tie_embeddings and num_stages > 1 and not self.split_head
+        # V placement puts the first and the last stage on rank 0: tie them locally
+        self._tie_local = tied_pp and 0 in my_stages and (num_stages - 1) in my_stages
+        if self._tie_local:
+            tied_pp = False
         self.head: Optional[HeadShard] = None
         orders = head_plan = head_costs = stage_costs = None
         self.head_chunks = None
@@ -170,6 +176,12 @@ class PipelineTrainer:
         tg = list(torch.tensor_split(targets, self.m, dim=0)) if self.is_last else None
         losses: List[torch.Tensor] = []
         self.runtime.step(inputs, tg, losses, return_outputs=False)
+        if self._tie_local:
+            by_idx = {st.stage_index: st for st in self.stages}
+            g0 = by_idx[0].arena.g("tok_embeddings.weight")
+            gl = by_idx[len(self.layer_ranges) - 1].arena.g("tok_embeddings.weight")
+            g0.add_(gl)      # both copies were already DP-reduced with their stage arenas
+            gl.copy_(g0)
         if self.head is not None:
             # replicated head: one gradient all-reduce over every rank (pipeline x DP)
             if dist.is_initialized() and dist.get_world_size() > 1:

@@ -141,8 +141,18 @@ class ScheduleZBH1(_PipelineSchedule):
     _name = "ZBH1"
 
 
+class ScheduleZBVZeroBubble(_PipelineSchedule):
+    """Zero-bubble V schedule: two stages per rank in V placement (rank r holds stages
+    r and 2P-1-r); stages must be built for ``style='v'``."""
+    _name = "ZBV"
+
+    def __init__(self, stages, n_microbatches, loss_fn=None, scale_grads=True, group=None, pipe_ranks=None,
+                 style: str = "v", profile: bool = False):
+        super().__init__(stages, n_microbatches, loss_fn, scale_grads, group, pipe_ranks, "v", profile)
+
+
 _CLASSES = {"GPipe": ScheduleGPipe, "1F1B": Schedule1F1B, "Interleaved1F1B": ScheduleInterleaved1F1B,
-            "LoopedBFS": ScheduleLoopedBFS, "ZBH1": ScheduleZBH1}
+            "LoopedBFS": ScheduleLoopedBFS, "ZBH1": ScheduleZBH1, "ZBV": ScheduleZBVZeroBubble}
 
 
 def get_schedule_class(name: str):

@@ -190,7 +190,10 @@ def _greedy_schedule(pp: int, m: int, v: int, style: str, costs: Dict[Op, float]
                     t = ready_time(a)
                     if t is not None:
                         cands.append((0, t, -s, a))
-                if fwd_next[s] < m and inflight[r] < max_inflight(r):
+                # the stash bound gates only the rank's entry chunk: later chunks' forwards
+                # are what drains the stash (multi-chunk V placement)
+                entry = s == min(x for x in range(S) if s2r[x] == r)
+                if fwd_next[s] < m and (inflight[r] < max_inflight(r) or not entry):
                     a = Action(s, Op.F, fwd_next[s])
                     t = ready_time(a)
                     if t is not None:
@@ -217,21 +220,20 @@ def _greedy_schedule(pp: int, m: int, v: int, style: str, costs: Dict[Op, float]
         rank_time[r] = end
         order[r].append(a)
         n_done += 1
+        # stash accounting in chunk units: +1 per forward, -1 when the chunk's activations
+        # are released (after B, or after W with a split backward)
         if a.op == Op.F:
             fwd_next[a.stage] += 1
-            if a.stage == min(s for s in range(S) if s2r[s] == r):
-                inflight[r] += 1
+            inflight[r] += 1
         elif a.op in (Op.B, Op.I):
             bwd_next[a.stage] += 1
             if a.op == Op.I:
                 pending_w[r].append(Action(a.stage, Op.W, a.mb))
-            elif a.stage == min(s for s in range(S) if s2r[s] == r):
+            else:
                 inflight[r] -= 1
         elif a.op == Op.W:
             pending_w[r].remove(a)
-            # activations of a microbatch are released only after its weight grad
-            if a.stage == min(s for s in range(S) if s2r[s] == r):
-                inflight[r] -= 1
+            inflight[r] -= 1
     return order
 
 
@@ -240,6 +242,20 @@ def gen_zb_h1(pp: int, m: int, v: int = 1, style: str = "loop") -> Dict[int, Lis
         raise ValueError("ZBH1 runs one stage per rank")
     return _greedy_schedule(pp, m, 1, style, {Op.F: 1.0, Op.I: 1.0, Op.W: 1.0, Op.B: 2.0},
                             max_inflight=lambda r: pp - r + 1, split_backward=True)
+
+
+def gen_zbv(pp: int, m: int, v: int = 2, style: str = "v") -> Dict[int, List[Action]]:
+    """Zero-bubble V schedule (ZB-V; the dependency's ScheduleZBVZeroBubble, torch
+    schedules.py:2287-3216 family): two chunks per rank in V placement (rank r holds
+    stages r and 2P-1-r, so the last chunk's output returns to rank 0's neighbour for
+    free), split backward with weight-grad fill, 1F1B-level activation memory
+    (2P half-size chunks in flight per rank)."""
+    if v != 2:
+        raise ValueError("ZBV runs two stages per rank")
+    if style != "v":
+        raise ValueError("ZBV needs the 'v' stage placement")
+    return _greedy_schedule(pp, m, 2, "v", {Op.F: 1.0, Op.I: 1.0, Op.W: 1.0, Op.B: 2.0},
+                            max_inflight=lambda r: 2 * pp, split_backward=True)
 
 
 # ----------------------------------------------------------------------------------------
@@ -253,12 +269,16 @@ SCHEDULES: Dict[str, Tuple[Callable[..., Dict[int, List[Action]]], int, bool]] =
     "Interleaved1F1B": (gen_interleaved_1f1b, 2, True),
     "LoopedBFS": (gen_looped_bfs, 2, True),
     "ZBH1": (gen_zb_h1, 1, False),
+    "ZBV": (gen_zbv, 2, True),
 }
+# schedules that only exist for one stage placement
+REQUIRED_STYLE: Dict[str, str] = {"ZBV": "v"}
 
 _ALIASES = {k.lower(): k for k in SCHEDULES}
 _ALIASES.update({"gpipe": "GPipe", "1f1b": "1F1B", "interleaved": "Interleaved1F1B",
                  "interleaved1f1b": "Interleaved1F1B", "loopedbfs": "LoopedBFS", "bfs": "LoopedBFS",
-                 "zbh1": "ZBH1", "zb": "ZBH1", "zerobubble": "ZBH1"})
+                 "zbh1": "ZBH1", "zb": "ZBH1", "zerobubble": "ZBH1", "zbv": "ZBV",
+                 "zbvzerobubble": "ZBV"})
 
 
 def canonical_name(name: str) -> str:

@@ -87,3 +87,15 @@ def test_dp2_pp2_distributed_head_replicas_agree():
         for k, v in res[a]["sd"].items():
             if k in res[b]["sd"]:
                 torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(res[b]["sd"][k]), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("split_head", [False, True])
+def test_pp2_zbv_matches_pp1(split_head):
+    ref = _train("gpt2", 1, 1, "1F1B")
+    res = run_world(_worker, 2, "gpt2", 2, 1, "ZBV", split_head, None)
+    # V placement: the last stage (and the loss) lives on rank 0
+    assert res[0]["losses"] == pytest.approx(ref["losses"], rel=1e-5)
+    for r in res.values():
+        for k, v in r["sd"].items():
+            torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref["sd"][k]), atol=1e-4, rtol=1e-4,
+                                       msg=lambda m: f"{k}: {m}")

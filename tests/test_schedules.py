@@ -177,3 +177,16 @@ def test_head_split_beats_last_stage_head_in_simulation():
     base = simulate(o, P, 1, "loop", stage_costs=[c + (head if s == P - 1 else 0) for s, c in enumerate(load)])
     _, _, mk = plan_head_schedule(o, P, 1, "loop", hc, stage_costs=load)
     assert mk < 0.6 * base.makespan
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_zbv_valid_lowerable_and_low_bubble(P):
+    m = 2 * P
+    o = generate("ZBV", P, m, 2, "v")
+    validate(o, P, 2, m, "v")
+    lower(o, P, 2, "v")
+    for r in range(P):   # V placement: rank r holds stages r and 2P-1-r
+        assert {a.stage for a in o[r]} == {r, 2 * P - 1 - r}
+    zbv = simulate(o, P, 2, "v", stage_costs=[0.5] * (2 * P)).bubble
+    f1b = simulate(generate("1F1B", P, m, 1, "loop"), P, 1, "loop").bubble
+    assert zbv < 0.6 * f1b
