@@ -411,12 +411,23 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
 
-  // prologue: all of K-tile 0; A0/B0 (read by phase 1) retired
+  // Half-tile DMA runs ~1.5 K-tiles ahead, one half-tile (2 glds per thread) per phase so
+  // the DMA issue cost is spread evenly; a slot is re-filled >= 2 phases after its last
+  // ds_read (WAR across the staggered wave rows, cdna guide §5 "8-phase template"):
+  //   tile t  phase 1: B1(t+1)   phase 2: A1(t+1)   phase 3: A0(t+2)   phase 4: B0(t+2)
+  // Each phase's counted vmcnt(8) retires exactly the half-tile the next phase reads; the
+  // last two K-tiles drain with vmcnt(0).
   issue(0, 0);
   issue(1, 0);
   issue(2, 0);
   issue(3, 0);
-  wait_vmcnt<4>();
+  if (nk > 1) {
+    issue(0, 1);
+    issue(1, 1);
+    wait_vmcnt<8>();
+  } else {
+    wait_vmcnt<4>();
+  }
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
@@ -442,7 +453,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
 
   for (int t = 0; t < nk; ++t) {
     const char* buf = smem + (t & 1) * BUF;
-    const bool more = t + 1 < nk;
+    const bool steady = t + 2 < nk;
     // ---- phase 1: A0 x B0
 #pragma unroll
     for (int s_ = 0; s_ < 4; ++s_) {
@@ -450,7 +461,8 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
       af[1][s_] = frag<false, BM>(buf, rA + 32, s_, hl);
       b0[s_] = frag<false, BN>(buf + 2 * HALF, rB, s_, hl);
     }
-    if (more) { issue(0, t + 1); wait_vmcnt<4>(); } else { wait_vmcnt<2>(); }   // B1(t) landed
+    if (t + 1 < nk) issue(2, t + 1);
+    if (steady) wait_vmcnt<8>(); else wait_vmcnt<0>();   // B1(t) landed
     G3_BAR();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     G3_MFMA(0, b0, 0);
@@ -458,24 +470,30 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
     // ---- phase 2: A0 x B1
 #pragma unroll
     for (int s_ = 0; s_ < 4; ++s_) b1[s_] = frag<false, BN>(buf + 3 * HALF, rB, s_, hl);
-    if (more) { issue(1, t + 1); wait_vmcnt<4>(); } else { wait_vmcnt<0>(); }   // A1(t) landed
+    if (t + 1 < nk) issue(3, t + 1);
+    if (steady) wait_vmcnt<8>(); else wait_vmcnt<0>();   // A1(t) landed
     G3_BAR();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     G3_MFMA(0, b1, 1);
     G3_BAR();
-    // ---- phase 3: A1 x B0
+    // ---- phase 3: A1 x B0; refill A0 of this buffer for K-tile t+2
 #pragma unroll
     for (int s_ = 0; s_ < 4; ++s_) {
       af[0][s_] = frag<false, BM>(buf + HALF, rA, s_, hl);
       af[1][s_] = frag<false, BM>(buf + HALF, rA + 32, s_, hl);
     }
-    if (more) issue(2, t + 1);
+    if (steady) issue(0, t + 2);
     G3_BAR();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     G3_MFMA(2, b0, 0);
     G3_BAR();
-    // ---- phase 4: A1 x B1; A0/B0 of K-tile t+1 retired for the next phase 1
-    if (more) { issue(3, t + 1); wait_vmcnt<4>(); }
+    // ---- phase 4: A1 x B1; refill B0; A0/B0 of K-tile t+1 retired for the next phase 1
+    if (steady) {
+      issue(1, t + 2);
+      wait_vmcnt<8>();
+    } else {
+      wait_vmcnt<0>();
+    }
     G3_BAR();
     G3_MFMA(2, b1, 1);
     G3_BAR();
