@@ -26,16 +26,43 @@ _MAX_DIMS = 8
 Spec = Tuple[Tuple[int, ...], torch.dtype]
 
 
+class _StagedRecv:
+    """Receive into a host buffer, copied to the device tensor on ``wait``."""
+
+    def __init__(self, work, host: torch.Tensor, dev: torch.Tensor):
+        self.work, self.host, self.dev = work, host, dev
+
+    def wait(self):
+        self.work.wait()
+        self.dev.copy_(self.host)
+        return True
+
+
+class _StagedSend:
+    """Send of a host copy; keeps the copy alive until the transfer completed."""
+
+    def __init__(self, work, host: torch.Tensor):
+        self.work, self.host = work, host
+
+    def wait(self):
+        return self.work.wait()
+
+
 class P2P:
     """Thin wrapper around ``torch.distributed`` p2p for one pipeline group.
 
-    ``ranks[i]`` is the global rank of pipeline rank ``i``.
+    ``ranks[i]`` is the global rank of pipeline rank ``i``.  With the gloo backend and
+    GPU tensors (``MIPIPE_DIST_BACKEND=gloo``: several ranks sharing one GPU, used to
+    test the whole multi-process GPU stack on a single-GPU box) transfers are staged
+    through host memory; with RCCL they go device to device over xGMI.
     """
 
     def __init__(self, group: Optional[dist.ProcessGroup], ranks: Sequence[int], device: torch.device):
         self.group = group
         self.ranks = list(ranks)
         self.device = device
+        self.host_staged = (device.type == "cuda" and dist.is_initialized()
+                            and dist.get_backend(group) == "gloo")
 
     def global_rank(self, pipe_rank: int) -> int:
         return self.ranks[pipe_rank]
@@ -43,14 +70,27 @@ class P2P:
     def post(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
         """Post one group; returns (send_works, recv_works) aligned with the inputs."""
         ops = []
+        staged = []
         for t, peer in sends:
+            if self.host_staged:
+                t = t.detach().to("cpu")
+                staged.append(t)
             ops.append(dist.P2POp(dist.isend, t, self.global_rank(peer), self.group))
+        host_recv = []
         for t, peer in recvs:
+            if self.host_staged:
+                h = torch.empty(t.shape, dtype=t.dtype)
+                host_recv.append((h, t))
+                t = h
             ops.append(dist.P2POp(dist.irecv, t, self.global_rank(peer), self.group))
         if not ops:
             return [], []
         works = dist.batch_isend_irecv(ops)
-        return works[: len(sends)], works[len(sends):]
+        sw, rw = works[: len(sends)], works[len(sends):]
+        if self.host_staged:
+            sw = [_StagedSend(w, h) for w, h in zip(sw, staged)]
+            rw = [_StagedRecv(w, h, d) for w, (h, d) in zip(rw, host_recv)]
+        return sw, rw
 
     # -------------------------------------------------------------- spec exchange
     def _pack(self, specs: Sequence[Spec]) -> torch.Tensor:
@@ -62,7 +102,7 @@ class P2P:
             buf[base + 1] = len(shape)
             for j, d in enumerate(shape):
                 buf[base + 2 + j] = d
-        return buf.to(self.device)
+        return buf if self.host_staged else buf.to(self.device)
 
     @staticmethod
     def _unpack(buf: torch.Tensor) -> List[Spec]:
@@ -81,7 +121,8 @@ class P2P:
         dist.send(self._pack(specs), self.global_rank(peer), group=self.group)
 
     def recv_specs(self, peer: int) -> List[Spec]:
-        buf = torch.zeros(1 + 8 * (2 + _MAX_DIMS), dtype=torch.int64, device=self.device)
+        buf = torch.zeros(1 + 8 * (2 + _MAX_DIMS), dtype=torch.int64,
+                          device="cpu" if self.host_staged else self.device)
         dist.recv(buf, self.global_rank(peer), group=self.group)
         return self._unpack(buf)
 
@@ -94,8 +135,9 @@ class P2P:
         for peer in sorted(set(peers)):
             if peer == my_rank:
                 continue
-            t_send = torch.ones(1, device=self.device)
-            t_recv = torch.zeros(1, device=self.device)
+            dev = "cpu" if self.host_staged else self.device
+            t_send = torch.ones(1, device=dev)
+            t_recv = torch.zeros(1, device=dev)
             s, r = self.post([(t_send, peer)], [(t_recv, peer)])
             for w in s + r:
                 w.wait()

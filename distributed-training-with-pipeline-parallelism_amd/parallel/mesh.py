@@ -27,10 +27,16 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) ->
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
-    use_gpu = torch.cuda.is_available() and backend != "gloo"
+    backend = backend or os.environ.get("MIPIPE_DIST_BACKEND") or None
+    # MIPIPE_DIST_BACKEND=gloo on a GPU box: every rank computes on the GPU (ranks may
+    # share one device) while gloo carries the traffic through host memory -- a test
+    # mode for the multi-process GPU stack on a single-GPU machine
+    gloo_on_gpu = backend == "gloo" and torch.cuda.is_available() and os.environ.get("MIPIPE_GLOO_GPU", "1") == "1"
+    use_gpu = torch.cuda.is_available() and (backend != "gloo" or gloo_on_gpu)
     if use_gpu:
-        torch.cuda.set_device(local_rank)
-        device = torch.device("cuda", local_rank)
+        dev_index = local_rank % torch.cuda.device_count() if gloo_on_gpu else local_rank
+        torch.cuda.set_device(dev_index)
+        device = torch.device("cuda", dev_index)
     else:
         device = torch.device("cpu")
     if backend is None:

@@ -1,0 +1,52 @@
+"""Multi-rank pipeline training check on GPU (ranks may share one GPU with
+MIPIPE_DIST_BACKEND=gloo).  Prints the per-step losses as one JSON line on rank 0.
+
+    torchrun --nproc-per-node 2 --master-addr 127.0.0.1 tools/mp_gpu_check.py --schedule 1F1B [--graphs 1]"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--schedule", default="1F1B")
+    ap.add_argument("--graphs", type=int, default=0)
+    ap.add_argument("--split-head", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    import torch.distributed as dist
+    import mipipe  # noqa: F401
+    from mipipe.engine import PipelineTrainer
+    from mipipe.models.config import NativeConfig
+    from mipipe.parallel.mesh import init_distributed
+    rank, world, _, device = init_distributed()
+    cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=4, n_heads=4, d_ff=1024, max_seq_len=256)
+    m, mbs, S = 8, 2, 256   # same data for every world size
+    tr = PipelineTrainer(cfg, pp=world, schedule=a.schedule if world > 1 else "1F1B", n_microbatches=m, mbs=mbs,
+                         seq_len=S, device=device, seed=3, graphs=bool(a.graphs),
+                         split_head=bool(a.split_head), lr=1e-3)
+    g = torch.Generator(device=device).manual_seed(11)
+    x = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
+    y = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
+    if a.graphs:
+        tr.capture_graphs(x, y)
+    losses = []
+    for _ in range(a.steps):
+        loss = tr.train_step(x, y)
+        v = torch.tensor([float(loss) if loss is not None else 0.0], dtype=torch.float64, device=device)
+        if world > 1 and tr.head is None:
+            dist.all_reduce(v)
+        losses.append(float(v.item()))
+    if rank == 0:
+        print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
