@@ -297,8 +297,54 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restric
 }
 
 // ==========================================================================================
+// glds staging of [64][DP] row tiles straight into the swizzled LDS image
+// ==========================================================================================
+// A 1 KiB LDS-DMA piece is PR = 1024 / (2 DP) image rows; lane l lands at byte 16 l of the
+// piece, so the XOR swizzle is applied on the SOURCE column (cdna guide §5.4 rule 21).
+// Columns past D (head dim padded to DP) read column 0 of the same row instead: finite
+// data that only meets zero K/V columns or feeds unwritten output columns.
+template <int DP>
+struct GTile {
+  static constexpr int CPR = DP / 8;           // 16-byte chunks per row
+  static constexpr int PR = 1024 / (DP * 2);   // rows per piece
+  static constexpr int PPW = (64 / PR) / 4;    // pieces per wave (4 waves)
+  int lr, phys;
+  __device__ __forceinline__ void init() {
+    const int lane = threadIdx.x & 63;
+    lr = lane / CPR;
+    phys = lane % CPR;
+  }
+  // rows row0 .. row0+63 of a token-major tensor (row stride `stride`, column offset
+  // already in `base`) -> LDS image `img`
+  __device__ __forceinline__ void issue(const bf16_t* base, int64_t stride, int row0, int nrows, int D, char* img,
+                                        int wave) const {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wave + 4 * i;
+      const int row = p * PR + lr;
+      const int chunk = (phys & ~15) | ((phys & 15) ^ chunk_swz<DP>(row));
+      int col = chunk * 8;
+      col = col < D ? col : 0;
+      int gr = row0 + row;
+      gr = gr < nrows ? gr : nrows - 1;
+      __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)gr * stride + col),
+                                       (__attribute__((address_space(3))) void*)(img + p * 1024), 16, 0, 0);
+    }
+  }
+};
+
+template <int N>
+__device__ __forceinline__ void attn_wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | (((N >> 4) & 3) << 14));
+}
+
+// ==========================================================================================
 // backward dK / dV: workgroup = 128 keys (4 waves x 32) of one (b, kv head)
 // ==========================================================================================
+// Q / dO tiles and the per-row LSE / delta stream through an NBUF-deep LDS ring by
+// LDS-DMA (2 tiles in flight for DP <= 128): no staging registers, one raw barrier per
+// tile, counted vmcnt.  Same math as before: key on the MFMA lane, P and dS are the B
+// operands of dV^T += dO^T P and dK^T += Q^T dS.
 template <int DP, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
@@ -307,22 +353,21 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     int64_t ks, int64_t vs, int64_t os, int64_t dks, int64_t dvs, float scale, float p_drop, uint64_t seed) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE = 64 * DP * 2;
-#define qbuf(i) (smem + (i) * TILE)
-#define gbuf(i) (smem + (2 + (i)) * TILE)
-  float* lse_s = reinterpret_cast<float*>(smem + 4 * TILE);  // [2][64]
-  float* del_s = lse_s + 128;                                 // [2][64]
+  constexpr int BUFB = 2 * TILE + 512;               // Q, dO, lse[64], delta[64]
+  constexpr int NBUF = DP <= 128 ? 3 : 2;
+  constexpr int LOOK = NBUF - 1;                     // tiles issued ahead
+  using GT = GTile<DP>;
 
-  const int nkb = (Sk + 127) / 128;
   const int kb = (int)blockIdx.x;
   const int bhk = blockIdx.y;
   const int b = bhk / Hkv, hk = bhk % Hkv;
   const int grp = H / Hkv;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int k0 = kb * 128;
   const int key = k0 + 32 * w + l32;  // this lane's key (MFMA column)
   const bool kvalid = key < Sk;
   const int shift = Sk - Sq;
-  (void)nkb;
 
   // K and V of this wave's 32 keys as B operands: lane holds K[key][16s + 8hl + j]
   bf16x8 kf[DP / 16], vf[DP / 16];
@@ -340,46 +385,52 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     dv[d] = {};
   }
   const float c = scale * LOG2E;
-  const float keep = DROP ? 1.f / (1.f - p_drop) : 1.f;
   // first query that can see key k0: q >= k0 - shift
   const int q_begin = CAUSAL ? max(0, ((k0 - shift) / 64) * 64) : 0;
   const int ntq = (Sq - q_begin + 63) / 64;
   const int total = ntq * grp;
 
-  Stage64<DP> qst, gst;
+  GT gt;
+  gt.init();
   auto issue = [&](int it) {
     const int hq = hk * grp + it / ntq;
     const int q0 = q_begin + (it % ntq) * 64;
-    qst.load(Q + (int64_t)b * Sq * qs + (int64_t)hq * D, qs, q0, Sq, D);
-    gst.load(dO + (int64_t)b * Sq * os + (int64_t)hq * D, os, q0, Sq, D);
-  };
-  auto stats = [&](int it, int buf) {
-    const int hq = hk * grp + it / ntq;
-    const int q0 = q_begin + (it % ntq) * 64;
-    if (threadIdx.x < 64) {
-      const int q = q0 + threadIdx.x;
+    char* buf = smem + (it % NBUF) * BUFB;
+    gt.issue(Q + (int64_t)b * Sq * qs + (int64_t)hq * D, qs, q0, Sq, D, buf, w);
+    gt.issue(dO + (int64_t)b * Sq * os + (int64_t)hq * D, os, q0, Sq, D, buf + TILE, w);
+    if (w == 0) {  // per-row stats, 4 bytes per lane (rows past Sq are masked in the math)
+      const int q = min(q0 + lane, Sq - 1);
       const int64_t idx = ((int64_t)b * H + hq) * Sq + q;
-      lse_s[buf * 64 + threadIdx.x] = q < Sq ? LSE[idx] : INFINITY;
-      del_s[buf * 64 + threadIdx.x] = q < Sq ? DELTA[idx] : 0.f;
+      __builtin_amdgcn_global_load_lds((const void*)(LSE + idx),
+                                       (__attribute__((address_space(3))) void*)(buf + 2 * TILE), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(DELTA + idx),
+                                       (__attribute__((address_space(3))) void*)(buf + 2 * TILE + 256), 4, 0, 0);
     }
   };
-  if (total > 0) {
-    issue(0);
-    qst.store(qbuf(0));
-    gst.store(gbuf(0));
-    stats(0, 0);
-  }
+  constexpr int PER_TILE = 2 * GT::PPW;  // DMA instructions per tile per wave (+2 on wave 0)
+#pragma unroll
+  for (int i = 0; i < LOOK; ++i)
+    if (i < total) issue(i);
+
   for (int it = 0; it < total; ++it) {
-    const int cur = it & 1;
     const int hq = hk * grp + it / ntq;
     const int q0 = q_begin + (it % ntq) * 64;
     const int bhq = b * H + hq;
-    if (it + 1 < total) issue(it + 1);
-    __syncthreads();
-    const char* qb = qbuf(cur);
-    const char* gb = gbuf(cur);
-    const float* ls = lse_s + cur * 64;
-    const float* dl = del_s + cur * 64;
+    // tile `it` landed (LOOK-1 younger tiles may stay in flight), then publish to all waves
+    if (LOOK == 2 && it + 1 < total) {
+      if (w == 0) attn_wait_vmcnt<PER_TILE + 2>(); else attn_wait_vmcnt<PER_TILE>();
+    } else {
+      attn_wait_vmcnt<0>();
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // the buffer of tile it-1 is free now: refill it with tile it+LOOK
+    if (it + LOOK < total) issue(it + LOOK);
+    const char* qb = smem + (it % NBUF) * BUFB;
+    const char* gb = qb + TILE;
+    const float* ls = reinterpret_cast<const float*>(qb + 2 * TILE);
+    const float* dl = ls + 64;
     const bool skip = CAUSAL && (k0 + 32 * w > q0 + 63 + shift);  // all of this wave's keys masked
     if (!skip) {
 #pragma unroll
@@ -401,16 +452,16 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
           lsv[g] = *reinterpret_cast<const float4*>(ls + 32 * u + 8 * g + 4 * hl);
           dlv[g] = *reinterpret_cast<const float4*>(dl + 32 * u + 8 * g + 4 * hl);
         }
-        // causal mask only where this wave's keys can exceed the tile's queries; rows past
-        // Sq carry lse = +inf (p = 0) and keys past Sk only feed their own unwritten outputs
-        const bool edge = CAUSAL && (k0 + 32 * w + 31 > q0 + 32 * u + shift);
+        // masks only where needed: the causal diagonal and query rows past Sq (their
+        // stats were clamped); keys past Sk only feed their own unwritten outputs
+        const bool edge = (q0 + 64 > Sq) || (CAUSAL && (k0 + 32 * w + 31 > q0 + 32 * u + shift));
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int qr = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl;
           const int q = q0 + qr;
           const float lv = (&lsv[r >> 2].x)[r & 3], dv_ = (&dlv[r >> 2].x)[r & 3];
           float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -lv));
-          if (edge && key > q + shift) p = 0.f;
+          if (edge && (q >= Sq || (CAUSAL && key > q + shift))) p = 0.f;
           float dpv = pacc[r];
           float pd = p;
           if (DROP) {
@@ -421,7 +472,6 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
           pm[r] = pd;                      // dropped P for dV
           ds[r] = p * (dpv - dv_);         // dS
         }
-        (void)keep;
         // dV^T += dO^T P ;  dK^T += Q^T dS     (A via transposed LDS reads of the row images)
         const bf16x8 pb0 = pack8(pm, 0), pb1 = pack8(pm, 1);
         const bf16x8 db0 = pack8(ds, 0), db1 = pack8(ds, 1);
@@ -439,11 +489,6 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
           dk[d] = mfma32(aq1, db1, dk[d]);
         }
       }
-    }
-    if (it + 1 < total) {
-      qst.store(qbuf(cur ^ 1));
-      gst.store(gbuf(cur ^ 1));
-      stats(it + 1, cur ^ 1);
     }
   }
   // ---- epilogue: lane = key, registers = d
@@ -612,8 +657,6 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
 
 #undef kbuf
 #undef vbuf
-#undef qbuf
-#undef gbuf
 // ==========================================================================================
 // launchers
 // ==========================================================================================
@@ -645,7 +688,7 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
                                  dqs, scale, p, seed);
   }
   {
-    const size_t lds = 4 * 64 * DP * 2 + 4 * 128 * sizeof(float);
+    const size_t lds = (DP <= 128 ? 3 : 2) * (2 * 64 * DP * 2 + 512);
     auto kern = attn_bwd_dkdv_kernel<DP, CAUSAL, DROP>;
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     dim3 grid((Sk + 127) / 128, B * Hkv);

@@ -168,7 +168,8 @@ def test_swiglu_and_rope():
 
 ATTN = [  # B, S, H, Hkv, D, causal
     (2, 256, 4, 4, 64, True), (2, 256, 4, 4, 64, False), (1, 200, 2, 2, 64, True),
-    (2, 128, 8, 8, 96, False), (1, 256, 4, 2, 128, True), (1, 128, 4, 4, 192, False), (1, 1024, 2, 2, 64, True)]
+    (2, 128, 8, 8, 96, False), (1, 256, 4, 2, 128, True), (1, 128, 4, 4, 192, False), (1, 1024, 2, 2, 64, True),
+    (1, 200, 4, 2, 128, True), (2, 136, 4, 4, 64, False)]
 
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,causal", ATTN)
