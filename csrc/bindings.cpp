@@ -41,7 +41,8 @@ int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, cons
 int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st);
 int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
              int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
-             int epilogue, int c_f32_accum, float alpha, int force_cfg, hipStream_t st);
+             int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, hipStream_t st);
+int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg, int* split_out);
 int mp_gemm(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
             int epilogue, int c_f32_accum, float alpha, hipStream_t st);
@@ -252,10 +253,16 @@ bool gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torc
   TORCH_CHECK((transB ? B.size(0) : B.size(1)) == K && (transB ? B.size(1) : B.size(0)) == N, "gemm2: B mismatch");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm2: inner dims must be contiguous");
   TORCH_CHECK(!accum || C.scalar_type() == torch::kFloat32, "gemm2: accumulate needs f32 C");
+  // split-K slabs (plain stores + one reduce pass instead of f32 atomics)
+  int split = 1;
+  mp_gemm2_plan(M, N, K, transA, transB, accum, (int)force_cfg, &split);
+  torch::Tensor ws;
+  if (accum && split > 1) ws = torch::empty({(int64_t)split * M * N}, C.options().dtype(torch::kFloat32));
   const int rc = mp_gemm2(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual),
                           mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),
                           residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
-                          transA, transB, epilogue, accum, (float)alpha, (int)force_cfg, cur_stream());
+                          transA, transB, epilogue, accum, (float)alpha, (int)force_cfg,
+                          ws.defined() ? ws.data_ptr<float>() : nullptr, cur_stream());
   if (rc == -2 || rc == -1) return false;
   check(rc, "gemm2");
   return true;

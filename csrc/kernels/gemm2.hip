@@ -101,8 +101,8 @@ template <int BM, int BN, int WM, int WN, int EPI, bool ACC, int NTH = NT>
 __device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 32], char* smem, int m0, int n0, int wr,
                                          int wn, int hl, int l32, void* __restrict__ Cv,
                                          const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
-                                         bf16_t* __restrict__ AUX, int M, int N, int64_t ldc, int64_t ldr, int64_t ldx,
-                                         float alpha, int nsplit) {
+                                         bf16_t* __restrict__ AUX, float* __restrict__ WS, int M, int N, int64_t ldc,
+                                         int64_t ldr, int64_t ldx, float alpha, int nsplit) {
   constexpr int WTM = BM / WM / 32, WTN = BN / WN / 32;
   constexpr int RG = BM / WM;      // rows per group
   constexpr int CP = BN + 4;       // f32 pitch
@@ -124,6 +124,23 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 3
     __syncthreads();
     const int rbase = m0 + pass * RG;
     if constexpr (ACC) {
+      if (nsplit > 1 && WS != nullptr) {
+        // split-K partial slab [split][M][N] with plain 16-byte stores; a reduce kernel
+        // adds the slabs into C (f32 atomics run at ~1.3 TB/s chip-wide and bounded the
+        // dW GEMMs; MI355X_MICROARCH.md "Global float atomics")
+        float* slab = WS + (int64_t)blockIdx.y * M * N;
+        for (int idx = threadIdx.x; idx < RG * BN / 4; idx += NTH) {
+          const int row = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
+          const int gr = rbase + row, gc = n0 + c4;
+          if (gr < M && gc < N) {
+            float4 v = *reinterpret_cast<const float4*>(ct + row * CP + c4);
+            v.x *= alpha; v.y *= alpha; v.z *= alpha; v.w *= alpha;
+            *reinterpret_cast<float4*>(slab + (int64_t)gr * N + gc) = v;
+          }
+        }
+        __syncthreads();
+        continue;
+      }
       if (nsplit > 1) {
         float* C = reinterpret_cast<float*>(Cv);
         for (int idx = threadIdx.x; idx < RG * BN; idx += NTH) {
@@ -194,9 +211,10 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 3
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
 __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm2_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                       void* __restrict__ Cv, const bf16_t* __restrict__ bias,
-                                                      const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX, int M,
-                                                      int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
-                                                      int64_t ldr, int64_t ldx, float alpha) {
+                                                      const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+                                                      float* __restrict__ WS, int M, int N, int K, int64_t lda,
+                                                      int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx,
+                                                      float alpha) {
   static_assert(WM * WN == 8, "8 waves");
   constexpr int WTM = BM / WM / 32, WTN = BN / WN / 32;
   static_assert(WTM * 32 * WM == BM && WTN * 32 * WN == BN, "tile/wave mismatch");
@@ -316,8 +334,8 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
     asm volatile("" ::: "memory");
   }
 
-  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, M, N, ldc, ldr, ldx, alpha,
-                                     nsplit);
+  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, WS, M, N, ldc, ldr, ldx,
+                                     alpha, nsplit);
 }
 
 
@@ -340,8 +358,9 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
 template <int EPI, bool ACC>
 __global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
-             const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX, int M, int N,
-             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha) {
+             const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+             float* __restrict__ WS, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr,
+             int64_t ldx, float alpha) {
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
   constexpr int HALF = 128 * 128;          // one half-tile image: 128 rows x 128 B
   constexpr int BUF = 4 * HALF;            // A0 A1 B0 B1
@@ -502,12 +521,13 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
 #undef G3_BAR
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
   __syncthreads();
-  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, M, N, ldc, ldr, ldx, alpha,
-                                     nsplit);
+  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, WS, M, N, ldc, ldr, ldx,
+                                     alpha, nsplit);
 }
 
 template <int EPI, bool ACC>
-static int launch3(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M, int N, int K,
+static int launch3(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
+                   int N, int K,
                    int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
                    hipStream_t st) {
   constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
@@ -521,13 +541,14 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   }
   const int nwg = ((M + 255) / 256) * ((N + 255) / 256);
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
-                                          (const bf16_t*)R, (bf16_t*)X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
+                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
   return (int)hipGetLastError();
 }
 
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
-static int launch(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M, int N, int K,
+static int launch(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
+                  int N, int K,
                   int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
                   hipStream_t st) {
   constexpr int STAGE = (BM + BN) * BK * 2;
@@ -541,7 +562,7 @@ static int launch(const void* A, const void* B, void* C, const void* bias, const
   }
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
-                                          (const bf16_t*)R, (bf16_t*)X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
+                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
   return (int)hipGetLastError();
 }
 
@@ -586,26 +607,45 @@ static int choose(int M, int N, int K, bool acc, bool outer, int* split_out) {
 using namespace g2;
 
 template <bool TA, bool TB, int EPI, bool ACC>
-static int dispatch(int cfg, const void* A, const void* B, void* C, const void* bias, const void* R, void* X, int M,
+static int dispatch(int cfg, const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws,
+                    int M,
                     int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
                     int split, hipStream_t st) {
   if constexpr (!TA && !TB) {
-    if (cfg == 4) return launch3<EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    if (cfg == 4) return launch3<EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
   }
   switch (cfg) {
-    case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
-    case 1: return launch<256, 192, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
-    case 2: return launch<256, 128, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
-    default: return launch<128, 128, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    case 1: return launch<256, 192, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    case 2: return launch<256, 128, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    default: return launch<128, 128, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
   }
 }
 
-// returns -2 if the (layout, epilogue) combination is not instantiated here (caller falls back to v1)
-extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux,
-                        int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux,
-                        int transA, int transB, int epilogue, int c_f32_accum, float alpha, int force_cfg,
-                        hipStream_t st) {
-  if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
+// C[M,N] (f32, row stride ldc) += sum over the split-K slabs ws[s][M][N]
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C, int M,
+                                                            int N, int64_t ldc, int split) {
+  const int64_t n4 = (int64_t)M * N / 4;
+  const int64_t slab = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 4;
+    const int m = (int)(e / N), n = (int)(e % N);
+    float4 acc = *reinterpret_cast<const float4*>(ws + e);
+    for (int s = 1; s < split; ++s) {
+      const float4 v = *reinterpret_cast<const float4*>(ws + s * slab + e);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    float4* cp = reinterpret_cast<float4*>(C + (int64_t)m * ldc + n);
+    float4 c = *cp;
+    c.x += acc.x; c.y += acc.y; c.z += acc.z; c.w += acc.w;
+    *cp = c;
+  }
+}
+
+// tile config + split-K factor the engine will use for this problem (callers size the
+// split-K workspace from it: split * M * N f32)
+extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg,
+                             int* split_out) {
   int split = 1;
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
   if (force_cfg >= 0 && force_cfg < 5) cfg = force_cfg;
@@ -615,10 +655,26 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   if (cfg >= 4 && (transA || transB)) cfg = 0;
   if ((transA || transB) && cfg == 1) cfg = 2;
   if (!c_f32_accum) split = 1;
+  *split_out = split;
+  return cfg;
+}
+
+// returns -2 if the (layout, epilogue) combination is not instantiated here (caller falls back to v1).
+// With split-K (f32 accumulate) and a workspace of split*M*N floats the partial products go
+// to slabs + one reduce pass; without a workspace they are added with f32 atomics.
+extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux,
+                        int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux,
+                        int transA, int transB, int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws,
+                        hipStream_t st) {
+  if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
+  int split = 1;
+  const int cfg = mp_gemm2_plan(M, N, K, transA, transB, c_f32_accum, force_cfg, &split);
+  float* wsp = split > 1 ? ws : nullptr;
+  int rc = -2;
 #define MP_G(TA_, TB_, E_, ACC_)                                                                                  \
-  if ((bool)transA == TA_ && (bool)transB == TB_ && epilogue == E_ && (bool)c_f32_accum == ACC_)                 \
-    return dispatch<TA_, TB_, E_, ACC_>(cfg, A, B, C, bias, residual, aux, M, N, K, lda, ldb, ldc, ld_res, ld_aux, \
-                                        alpha, split, st);
+  if (rc == -2 && (bool)transA == TA_ && (bool)transB == TB_ && epilogue == E_ && (bool)c_f32_accum == ACC_)     \
+    rc = dispatch<TA_, TB_, E_, ACC_>(cfg, A, B, C, bias, residual, aux, wsp, M, N, K, lda, ldb, ldc, ld_res,       \
+                                      ld_aux, alpha, split, st);
   MP_G(false, false, EPI_NONE, false)
   MP_G(false, false, EPI_BIAS, false)
   MP_G(false, false, EPI_BIAS_GELU, false)
@@ -630,5 +686,11 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   MP_G(true, true, EPI_NONE, true)
   MP_G(false, false, EPI_NONE, true)
 #undef MP_G
-  return -2;
+  if (rc == 0 && wsp != nullptr) {
+    const int64_t n4 = (int64_t)M * N / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
+    splitk_reduce_kernel<<<blocks, 256, 0, st>>>(wsp, reinterpret_cast<float*>(C), M, N, ldc, split);
+    rc = (int)hipGetLastError();
+  }
+  return rc;
 }
