@@ -67,9 +67,85 @@ __global__ void __launch_bounds__(256) xent_kernel(bf16_t* __restrict__ logits, 
   }
 }
 
+// Register-resident variant: 512 threads hold the whole row (CPT 16-byte chunks each), so
+// the logits are read from HBM exactly once and the gradient written once; exp2 with
+// log2(e) folded into one fma.
+template <int CPT, bool WRITE_GRAD>
+__global__ void __launch_bounds__(512) xent_reg_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ target,
+                                                       float* __restrict__ loss, int T, int V, int Vp,
+                                                       float grad_scale, int64_t ignore_index) {
+  __shared__ float red[16];
+  constexpr float L2E = 1.4426950408889634f;
+  const int row = blockIdx.x;
+  bf16_t* x = logits + (size_t)row * Vp;
+  const int64_t tgt = target[row];
+  const int nchunk = Vp >> 3;
+  u16x8 v[CPT];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + 512 * i;
+    if (c < nchunk) {
+      v[i] = *reinterpret_cast<const u16x8*>(x + c * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c * 8 + e < V) m = fmaxf(m, bf2f(v[i][e]));
+    }
+  }
+  const float gm = block_max<512>(m, red);
+  const float mc = gm * L2E;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + 512 * i;
+    if (c < nchunk) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c * 8 + e < V) s += __builtin_amdgcn_exp2f(__builtin_fmaf(bf2f(v[i][e]), L2E, -mc));
+    }
+  }
+  __syncthreads();
+  const float gs = block_sum<512>(s, red);
+  const float lse = gm + __logf(gs);
+  const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
+  if (threadIdx.x == 0) loss[row] = valid ? lse - bf2f(x[tgt]) : 0.f;
+  if (!WRITE_GRAD) return;
+  __syncthreads();  // x[tgt] read before it is overwritten
+  const float sc = valid ? grad_scale : 0.f;
+  const float lc = lse * L2E;
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + 512 * i;
+    if (c < nchunk) {
+      u16x8 o;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int j = c * 8 + e;
+        float g = 0.f;
+        if (j < V) g = (__builtin_amdgcn_exp2f(__builtin_fmaf(bf2f(v[i][e]), L2E, -lc)) - (j == tgt ? 1.f : 0.f)) * sc;
+        o[e] = f2bf(g);
+      }
+      *reinterpret_cast<u16x8*>(x + c * 8) = o;
+    }
+  }
+}
+
 extern "C" int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss, int T, int V, int Vp,
                                float grad_scale, int64_t ignore_index, int write_grad, hipStream_t st) {
   if (Vp % 8 != 0 || V > Vp) return -1;
+  const int nchunk = Vp / 8;
+#define MP_XR(CPT)                                                                                               \
+  if (nchunk <= 512 * CPT) {                                                                                     \
+    if (write_grad)                                                                                              \
+      xent_reg_kernel<CPT, true><<<T, 512, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,          \
+                                                    ignore_index);                                              \
+    else                                                                                                         \
+      xent_reg_kernel<CPT, false><<<T, 512, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,         \
+                                                     ignore_index);                                             \
+    return (int)hipGetLastError();                                                                               \
+  }
+  MP_XR(4) MP_XR(16) MP_XR(32)
+#undef MP_XR
   if (write_grad)
     xent_kernel<true><<<T, 256, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale, ignore_index);
   else
