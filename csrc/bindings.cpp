@@ -34,7 +34,7 @@ int mp_attn_fwd(const void* q, const void* k, const void* v, void* o, float* lse
                 int Hkv, int D, int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride, int causal,
                 float scale, float p_drop, uint64_t seed, hipStream_t st);
 int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
-                float* delta, void* dq, void* dk, void* dv, float* dq_acc, int B, int Sq, int Sk, int H, int Hkv, int D,
+                float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int Hkv, int D,
                 int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride, int64_t dq_stride,
                 int64_t dk_stride, int64_t dv_stride, int causal, float scale, float p_drop, uint64_t seed,
                 hipStream_t st);
@@ -215,11 +215,11 @@ void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o
 
 void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o, torch::Tensor dout,
               torch::Tensor lse, torch::Tensor delta, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv,
-              torch::Tensor dq_acc, int64_t B, int64_t Sq, int64_t Sk, int64_t H, int64_t Hkv, int64_t D, bool causal,
+              int64_t B, int64_t Sq, int64_t Sk, int64_t H, int64_t Hkv, int64_t D, bool causal,
               double scale, double p, int64_t seed) {
   TORCH_CHECK(o.stride(0) == dout.stride(0), "o and dout must share a row stride");
   check(mp_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
-                    delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), dq_acc.data_ptr<float>(), B,
+                    delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B,
                     Sq, Sk, H, Hkv, D, q.stride(0), k.stride(0), v.stride(0), o.stride(0), dq.stride(0), dk.stride(0),
                     dv.stride(0), causal, (float)scale, (float)p, (uint64_t)seed, cur_stream()),
         "attn_bwd");

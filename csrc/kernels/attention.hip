@@ -270,33 +270,6 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
 }
 
 // ==========================================================================================
-// backward preprocess: delta = rowsum(dO * O)  (f32, per (b, h, query))
-// ==========================================================================================
-__global__ void __launch_bounds__(256) attn_delta_kernel(const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO,
-                                                         float* __restrict__ delta, int B, int Sq, int H, int D,
-                                                         int64_t os) {
-  const int lane = threadIdx.x & 63;
-  const int64_t item = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // (b, q, h)
-  if (item >= (int64_t)B * Sq * H) return;
-  const int h = item % H;
-  const int64_t tq = item / H;  // b*Sq + q
-  const bf16_t* orow = O + tq * os + (int64_t)h * D;
-  const bf16_t* drow = dO + tq * os + (int64_t)h * D;
-  float acc = 0.f;
-  for (int c = lane * 4; c < D; c += 256) {
-    u16x4 a = *reinterpret_cast<const u16x4*>(orow + c);
-    u16x4 g = *reinterpret_cast<const u16x4*>(drow + c);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) acc += bf2f(a[e]) * bf2f(g[e]);
-  }
-  acc = wave_sum(acc);
-  if (lane == 0) {
-    const int64_t b = tq / Sq, q = tq % Sq;
-    delta[(b * H + h) * Sq + q] = acc;
-  }
-}
-
-// ==========================================================================================
 // glds staging of [64][DP] row tiles straight into the swizzled LDS image
 // ==========================================================================================
 // A 1 KiB LDS-DMA piece is PR = 1024 / (2 DP) image rows; lane l lands at byte 16 l of the
@@ -724,11 +697,10 @@ extern "C" int mp_attn_fwd(const void* q, const void* k, const void* v, void* o,
 }
 
 extern "C" int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout,
-                           const float* lse, float* delta, void* dq, void* dk, void* dv, float* dq_acc, int B, int Sq,
+                           const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int Sq,
                            int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs,
                            int64_t dks, int64_t dvs, int causal, float scale, float p_drop, uint64_t seed,
                            hipStream_t st) {
-  (void)dq_acc;
   const int DP = pick_dp(D);
   if (DP < 0 || D % 8 || H % Hkv) return -1;
   const bool drop = p_drop > 0.f;

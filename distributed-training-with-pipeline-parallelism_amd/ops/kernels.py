@@ -504,7 +504,7 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B: int, Sq: int, Sk: int, H: int, 
     if _gpu(q):
         if delta is None:
             delta = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
-        _ext().attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, delta, B, Sq, Sk, H, Hkv, D, bool(causal),
+        _ext().attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, H, Hkv, D, bool(causal),
                         float(scale), float(p_drop), int(seed))
         return dq, dk, dv
     rep = H // Hkv
