@@ -278,7 +278,12 @@ void transpose(torch::Tensor in, torch::Tensor out) {
 
 }  // namespace
 
+namespace mipipe_comm {
+void register_rccl(pybind11::module& m);
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  mipipe_comm::register_rccl(m);
   m.doc() = "mipipe gfx950 HIP kernels";
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);

@@ -14,6 +14,7 @@ as small int64 tensors once at init (no pickling).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -48,6 +49,42 @@ class _StagedSend:
         return self.work.wait()
 
 
+class _NativeWork:
+    """Handle of one grouped transfer on the native RCCL engine; ``wait`` makes the
+    current stream wait (no host block), like torch's NCCL Work."""
+
+    def __init__(self, engine, handle: int):
+        self.engine, self.handle = engine, handle
+
+    def wait(self):
+        self.engine.wait(self.handle)
+        return True
+
+
+def load_native_rccl(ext) -> None:
+    """Bind the engine to the librccl PyTorch loaded (one RCCL per process)."""
+    ext.RcclP2P.load(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+
+
+def make_native_engine(group, ranks: Sequence[int], my_pipe_rank: int, device: torch.device):
+    """Collective over the pipeline group: pipeline rank 0 draws an RCCL unique id, the
+    group broadcasts it, every rank joins the communicator (csrc/comm/rccl_p2p.cpp)."""
+    from ..ops.kernels import load_ext
+    ext = load_ext()
+    if ext is None or not hasattr(ext, "RcclP2P"):
+        raise RuntimeError("MIPIPE_P2P=native needs the built extension (_C.so)")
+    load_native_rccl(ext)
+    n = 128
+    buf = torch.zeros(n, dtype=torch.uint8, device=device)
+    if my_pipe_rank == 0:
+        uid = ext.RcclP2P.unique_id()
+        buf.copy_(torch.frombuffer(bytearray(uid), dtype=torch.uint8))
+    if len(ranks) > 1:
+        dist.broadcast(buf, src=ranks[0], group=group)
+    uid = bytes(buf.cpu().tolist())
+    return ext.RcclP2P(uid, len(ranks), my_pipe_rank, device.index if device.index is not None else 0)
+
+
 class P2P:
     """Thin wrapper around ``torch.distributed`` p2p for one pipeline group.
 
@@ -63,12 +100,25 @@ class P2P:
         self.device = device
         self.host_staged = (device.type == "cuda" and dist.is_initialized()
                             and dist.get_backend(group) == "gloo")
+        # MIPIPE_P2P=native: grouped ncclSend/ncclRecv from the C++ engine on its own comm
+        # stream instead of torch.distributed.batch_isend_irecv
+        self.engine = None
+        if (os.environ.get("MIPIPE_P2P", "torch") == "native" and device.type == "cuda" and dist.is_initialized()
+                and not self.host_staged and len(self.ranks) > 1):
+            me = self.ranks.index(dist.get_rank())
+            self.engine = make_native_engine(group, self.ranks, me, device)
 
     def global_rank(self, pipe_rank: int) -> int:
         return self.ranks[pipe_rank]
 
     def post(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
         """Post one group; returns (send_works, recv_works) aligned with the inputs."""
+        if self.engine is not None:
+            if not sends and not recvs:
+                return [], []
+            h = self.engine.post([(t, p) for t, p in sends], [(t, p) for t, p in recvs])
+            w = _NativeWork(self.engine, h)
+            return [w] * len(sends), [w] * len(recvs)
         ops = []
         staged = []
         for t, peer in sends:

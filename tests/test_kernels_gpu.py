@@ -313,3 +313,26 @@ def test_norm_bwd_fused_colsums():
         outs.append((ds, dw, db, c1, c2))
     for a, g in zip(*outs):
         close(g, a, atol=5e-2, rtol=2e-2)
+
+
+def test_native_rccl_engine_self_transfer():
+    """csrc/comm/rccl_p2p.cpp: a one-rank communicator sends to itself (grouped send+recv on
+    the engine's comm stream, stream-ordered completion), and only one RCCL is loaded."""
+    from mipipe.ops import kernels as _k
+    from mipipe.parallel.comm import load_native_rccl
+    ext = _k.load_ext()
+    load_native_rccl(ext)
+    eng = ext.RcclP2P(ext.RcclP2P.unique_id(), 1, 0, torch.cuda.current_device())
+    src = torch.randn(1 << 20, device=DEV).to(torch.bfloat16)
+    dst = torch.empty_like(src)
+    src2 = torch.arange(1000, device=DEV, dtype=torch.int64)
+    dst2 = torch.zeros_like(src2)
+    h = eng.post([(src, 0), (src2, 0)], [(dst, 0), (dst2, 0)])
+    eng.wait(h)
+    torch.cuda.synchronize()
+    assert torch.equal(dst, src) and torch.equal(dst2, src2)
+    assert eng.query(h)
+    eng.close()
+    with open("/proc/self/maps") as f:
+        libs = {line.split()[-1] for line in f if "librccl" in line}
+    assert len(libs) == 1, libs

@@ -64,16 +64,18 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
         if force or _newer([k] + headers, o):
             jobs_list.append(base + ["-c", k, "-o", o])
     incs, tlib, abi = _torch_paths()
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(OBJ, "bindings.o")
-    objs.append(bobj)
-    if force or _newer([bsrc], bobj):
-        cmd = base + [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
-                      "-DTORCH_EXTENSION_NAME=_C", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1"]
-        for i in incs:
-            cmd += ["-isystem", i]
-        cmd += ["-isystem", sysconfig.get_paths()["include"], "-c", bsrc, "-o", bobj]
-        jobs_list.append(cmd)
+    # translation units that include torch: the pybind module and the native RCCL engine
+    for bsrc in (os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "comm", "rccl_p2p.cpp")):
+        bobj = os.path.join(OBJ, os.path.basename(bsrc) + ".o")
+        objs.append(bobj)
+        if force or _newer([bsrc], bobj):
+            cmd = base + [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
+                          "-DTORCH_EXTENSION_NAME=_C", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
+                          "-isystem", "/opt/rocm/include"]
+            for i in incs:
+                cmd += ["-isystem", i]
+            cmd += ["-isystem", sysconfig.get_paths()["include"], "-c", bsrc, "-o", bobj]
+            jobs_list.append(cmd)
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         for msg in ex.map(_run, jobs_list):
             if verbose and msg:
@@ -81,7 +83,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
     if force or jobs_list or not os.path.exists(OUT) or _newer(objs, OUT):
         link = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT] + objs + [
             "-L", tlib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
-            f"-Wl,-rpath,{tlib}"]
+            "-ldl", f"-Wl,-rpath,{tlib}"]
         _run(link)
     return OUT
 
