@@ -34,6 +34,14 @@ constexpr int NT = 512;
 
 __device__ __forceinline__ int swz8(int row) { return (((row >> 1) & 1) << 2) | ((row >> 2) & 3); }
 __device__ __forceinline__ int swz16(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+// K-contiguous image swizzle for the 16x16x32 fragment read (lane = 16 q + i reads row
+// r0 + i, chunk c + q): chunk ^ g(row bits 1-3) with g mapping row pairs {0,1,6,7} ->
+// {6,7,4,5} and {2..5} -> {0..3} makes all four ds_read_b128 lane groups hit 16
+// distinct 16-byte bank slots (MI355X_MICROARCH.md LDS table); swz8 would be 2-way here
+__device__ __forceinline__ int swzq(int row) { return (((row >> 1) & 7) + 6) & 7; }
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
 
 // K-contiguous image [rows][64 k]: 128-byte rows, 8 chunks
 __device__ __forceinline__ int offK(int row, int chunk) { return row * 128 + 16 * (chunk ^ swz8(row)); }
@@ -64,13 +72,35 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int rc, int s, int hl) {
   }
 }
 
+// 16x16x32 fragment: lane l holds rows/cols base + (l & 15), k = 32 s + 8 (l >> 4) + 0..7
+// (K-contiguous images use the swzq swizzle; outer-contiguous ones two tr reads, 8 k-rows
+// per 16-lane group, conflict-free under offO's swz16)
+template <bool OUTER, int COLS>
+__device__ __forceinline__ bf16x8 frag16(const char* img, int base, int s) {
+  const int lane = threadIdx.x & 63;
+  if constexpr (!OUTER) {
+    const int row = base + (lane & 15), chunk = 4 * s + (lane >> 4);
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * (chunk ^ swzq(row)));
+  } else {
+    const int i = lane & 15, q = i >> 2, p = i & 3;
+    const int col = base + 4 * p;
+    const int r0 = 32 * s + 8 * (lane >> 4);
+    const char* a0 = img + offO<COLS>(r0 + q, col >> 3) + ((col & 7) << 1);
+    const char* a1 = img + offO<COLS>(r0 + 4 + q, col >> 3) + ((col & 7) << 1);
+    s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a0));
+    s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a1));
+    s16x8 r = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  }
+}
+
 // global source (bf16 element pointer) of the 16 bytes that land at byte `pos` of an image
-template <bool OUTER, int ROWS>
+template <bool OUTER, int ROWS, bool M16 = false>
 __device__ __forceinline__ const bf16_t* src_of(const bf16_t* base, int64_t ld, int pos, int outer0, int outer_lim,
                                                 int k0) {
   if constexpr (!OUTER) {  // [ROWS][64k]
     const int row = pos >> 7, phys = (pos >> 4) & 7;
-    const int chunk = phys ^ swz8(row);
+    const int chunk = phys ^ (M16 ? swzq(row) : swz8(row));
     int o = outer0 + row;
     o = o < outer_lim ? o : outer_lim - 1;  // clamp: rows past the edge only feed masked outputs
     return base + (int64_t)o * ld + k0 + chunk * 8;
@@ -97,30 +127,55 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // ---- epilogue: one wave-row group at a time through LDS -> coalesced 16-byte bias /
 // residual / activation / store, or lane-consecutive f32 atomics for split-K
-template <int BM, int BN, int WM, int WN, int EPI, bool ACC, int NTH = NT>
-__device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 32], char* smem, int m0, int n0, int wr,
-                                         int wn, int hl, int l32, void* __restrict__ Cv,
+// accumulator layout of the 32x32x16 engines: acc[i][j] element r -> wave-local
+// row 32 i + (r & 3) + 8 (r >> 2) + 4 hl, column wn + 32 j + l32
+template <int WTM, int WTN>
+struct Stage32 {
+  f32x16 (&acc)[WTM][WTN];
+  int wn, hl, l32;
+  __device__ __forceinline__ void operator()(float* ct, int CP) const {
+#pragma unroll
+    for (int i = 0; i < WTM; ++i)
+#pragma unroll
+      for (int j = 0; j < WTN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          const int col = wn + 32 * j + l32;
+          ct[row * CP + col] = acc[i][j][r];
+        }
+  }
+};
+
+// accumulator layout of the 16x16x32 engines: acc[i][j] element r -> wave-local
+// row 16 i + 4 (lane >> 4) + r, column wn + 16 j + (lane & 15)
+template <int TM, int TN>
+struct Stage16 {
+  f32x4 (&acc)[TM][TN];
+  int wn, lane;
+  __device__ __forceinline__ void operator()(float* ct, int CP) const {
+    const int rq = 4 * (lane >> 4), c = wn + (lane & 15);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ct[(16 * i + rq + r) * CP + c + 16 * j] = acc[i][j][r];
+  }
+};
+
+template <int BM, int BN, int WM, int WN, int EPI, bool ACC, int NTH = NT, class StageF>
+__device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0, int n0, int wr,
+                                         void* __restrict__ Cv,
                                          const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
                                          bf16_t* __restrict__ AUX, float* __restrict__ WS, int M, int N, int64_t ldc,
                                          int64_t ldr, int64_t ldx, float alpha, int nsplit) {
-  constexpr int WTM = BM / WM / 32, WTN = BN / WN / 32;
   constexpr int RG = BM / WM;      // rows per group
   constexpr int CP = BN + 4;       // f32 pitch
   float* ct = reinterpret_cast<float*>(smem);
 #pragma unroll 1
   for (int pass = 0; pass < WM; ++pass) {
-    if (wr == pass) {
-#pragma unroll
-      for (int i = 0; i < WTM; ++i)
-#pragma unroll
-        for (int j = 0; j < WTN; ++j)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
-            const int col = wn + 32 * j + l32;
-            ct[row * CP + col] = acc[i][j][r];
-          }
-    }
+    if (wr == pass) stage(ct, CP);
     __syncthreads();
     const int rbase = m0 + pass * RG;
     if constexpr (ACC) {
@@ -208,7 +263,7 @@ __device__ __forceinline__ void epilogue(f32x16 (&acc)[BM / WM / 32][BN / WN / 3
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
+template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC, bool M16>
 __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm2_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                       void* __restrict__ Cv, const bf16_t* __restrict__ bias,
                                                       const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
@@ -257,8 +312,8 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
     const int p = wave + 8 * i;            // wave-uniform piece index
     const int pos = p * 1024 + lane * 16;  // this lane's byte in the stage
     pisA[i] = p * 1024 < A_BYTES;
-    if (pisA[i]) psrc[i] = src_of<TA, BM>(A, lda, pos, m0, M, kbase);
-    else psrc[i] = src_of<TB, BN>(B, ldb, pos - A_BYTES, n0, N, kbase);
+    if (pisA[i]) psrc[i] = src_of<TA, BM, M16>(A, lda, pos, m0, M, kbase);
+    else psrc[i] = src_of<TB, BN, M16>(B, ldb, pos - A_BYTES, n0, N, kbase);
   }
   auto issue = [&](int stage, int kt) {
     char* sb = smem + stage * STAGE;
@@ -273,6 +328,7 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
     }
   };
 
+  if constexpr (!M16) {
   f32x16 acc[WTM][WTN];
 #pragma unroll
   for (int i = 0; i < WTM; ++i)
@@ -334,8 +390,68 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
     asm volatile("" ::: "memory");
   }
 
-  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, WS, M, N, ldc, ldr, ldx,
-                                     alpha, nsplit);
+  epilogue<BM, BN, WM, WN, EPI, ACC>(Stage32<WTM, WTN>{acc, wn, hl, l32}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M,
+                                     N, ldc, ldr, ldx, alpha, nsplit);  } else {
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{};
+
+  issue(0, 0);
+  if (nk > 1) {
+    issue(1, 1);
+    wait_vmcnt<PW>();
+  } else {
+    wait_vmcnt<0>();
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nk; ++t) {
+    const char* sa = smem + (t & 1) * STAGE;
+    const char* sbB = sa + A_BYTES;
+    // two 32-deep k-substeps; substep 1's fragments are read under substep 0's MFMAs
+    bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[0][i] = frag16<TA, BM>(sa, wm + 16 * i, 0);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[0][j] = frag16<TB, BN>(sbB, wn + 16 * j, 0);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[1][i] = frag16<TA, BM>(sa, wm + 16 * i, 1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) bfr[1][j] = frag16<TB, BN>(sbB, wn + 16 * j, 1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[s][i], bfr[s][j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) {
+      issue(t & 1, t + 2);
+      wait_vmcnt<PW>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  epilogue<BM, BN, WM, WN, EPI, ACC>(Stage16<TM, TN>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M, N, ldc,
+                                     ldr, ldx, alpha, nsplit);
+  }
+
 }
 
 
@@ -355,7 +471,7 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
 // every SIMD one wave issues MFMAs while its partner issues ds_reads / DMA: the
 // cdna guide's 8-phase template (§5 "256^2 8-phase template"), with 32x32x16 MFMAs.
 // ---------------------------------------------------------------------------------------
-template <int EPI, bool ACC>
+template <int EPI, bool ACC, bool M16>
 __global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
              const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
@@ -390,7 +506,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   // staging: this wave's two 1 KiB pieces (j = 0, 1) of every half-tile.  Piece rows
   // i = 64 j + 8 wave + (lane >> 3); swz8 reads row bits 1-3, i.e. i & 15 = 8 (wave & 1) + lr.
   const int lr = lane >> 3;
-  const int lc = (lane & 7) ^ swz8(8 * (wave & 1) + lr);
+  const int lc = (lane & 7) ^ (M16 ? swzq(8 * (wave & 1) + lr) : swz8(8 * (wave & 1) + lr));
   const bf16_t* pa[2];
   const bf16_t* pb[2];
 #pragma unroll
@@ -426,6 +542,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
     }
   };
 
+  if constexpr (!M16) {
   f32x16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x16{};
@@ -521,11 +638,120 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
 #undef G3_BAR
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
   __syncthreads();
-  epilogue<BM, BN, WM, WN, EPI, ACC>(acc, smem, m0, n0, wr, wn, hl, l32, Cv, bias, R, AUX, WS, M, N, ldc, ldr, ldx,
-                                     alpha, nsplit);
+  epilogue<BM, BN, WM, WN, EPI, ACC>(Stage32<4, 2>{acc, wn, hl, l32}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M,
+                                     N, ldc, ldr, ldx, alpha, nsplit);
+  } else {
+  // 16x16x32 MFMAs: same phases, DMA and barriers; a phase quadrant (64 rows x 32 cols)
+  // is 4 x 2 blocks of 16x16, K = 64 in two 32-deep steps (16 MFMAs of 16 cycles)
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+  // Half-tile DMA runs ~1.5 K-tiles ahead, one half-tile (2 glds per thread) per phase so
+  // the DMA issue cost is spread evenly; a slot is re-filled >= 2 phases after its last
+  // ds_read (WAR across the staggered wave rows, cdna guide §5 "8-phase template"):
+  //   tile t  phase 1: B1(t+1)   phase 2: A1(t+1)   phase 3: A0(t+2)   phase 4: B0(t+2)
+  // Each phase's counted vmcnt(8) retires exactly the half-tile the next phase reads; the
+  // last two K-tiles drain with vmcnt(0).
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  if (nk > 1) {
+    issue(0, 1);
+    issue(1, 1);
+    wait_vmcnt<8>();
+  } else {
+    wait_vmcnt<4>();
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+  asm volatile("" ::: "memory");
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int q = lane >> 4;
+  const int rA = wr * 64 + (lane & 15);
+  const int rB = wc * 32 + (lane & 15);
+  auto fq = [&](const char* img, int row, int st) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * ((4 * st + q) ^ swzq(row)));
+  };
+
+#define G4_MFMA(R0, BF, C0)                                                              \
+  __builtin_amdgcn_sched_barrier(0);                                                     \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                       \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                       \
+  _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                       \
+    acc[R0 + i_][C0 + j_] = mfma16(af[i_][s_], BF[j_][s_], acc[R0 + i_][C0 + j_]);       \
+  __builtin_amdgcn_s_setprio(0);                                                         \
+  __builtin_amdgcn_sched_barrier(0);
+#define G3_BAR()                          \
+  asm volatile("" ::: "memory");          \
+  __builtin_amdgcn_s_barrier();           \
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const bool steady = t + 2 < nk;
+    // ---- phase 1: A0 x B0
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][s_] = fq(buf, rA + 16 * i, s_);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[j][s_] = fq(buf + 2 * HALF, rB + 16 * j, s_);
+    }
+    if (t + 1 < nk) issue(2, t + 1);
+    if (steady) wait_vmcnt<8>(); else wait_vmcnt<0>();   // B1(t) landed
+    G3_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G4_MFMA(0, b0, 0);
+    G3_BAR();
+    // ---- phase 2: A0 x B1
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b1[j][s_] = fq(buf + 3 * HALF, rB + 16 * j, s_);
+    if (t + 1 < nk) issue(3, t + 1);
+    if (steady) wait_vmcnt<8>(); else wait_vmcnt<0>();   // A1(t) landed
+    G3_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G4_MFMA(0, b1, 2);
+    G3_BAR();
+    // ---- phase 3: A1 x B0; refill A0 of this buffer for K-tile t+2
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][s_] = fq(buf + HALF, rA + 16 * i, s_);
+    if (steady) issue(0, t + 2);
+    G3_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G4_MFMA(4, b0, 0);
+    G3_BAR();
+    // ---- phase 4: A1 x B1; refill B0
+    if (steady) {
+      issue(1, t + 2);
+      wait_vmcnt<8>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    G3_BAR();
+    G4_MFMA(4, b1, 2);
+    G3_BAR();
+  }
+#undef G4_MFMA
+#undef G3_BAR
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
+  __syncthreads();
+  epilogue<BM, BN, WM, WN, EPI, ACC>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M, N, ldc,
+                                     ldr, ldx, alpha, nsplit);
+  }
 }
 
-template <int EPI, bool ACC>
+template <int EPI, bool ACC, bool M16>
 static int launch3(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
                    int N, int K,
                    int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
@@ -533,7 +759,7 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
   constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
   constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
-  auto kern = gemm3_kernel<EPI, ACC>;
+  auto kern = gemm3_kernel<EPI, ACC, M16>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -554,7 +780,11 @@ static int launch(const void* A, const void* B, void* C, const void* bias, const
   constexpr int STAGE = (BM + BN) * BK * 2;
   constexpr int EPI_BYTES = (BM / WM) * (BN + 4) * 4;
   constexpr int LDS = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
-  auto kern = gemm2_kernel<BM, BN, WM, WN, TA, TB, EPI, ACC>;
+  static const bool m16 = [] { const char* e = getenv("MIPIPE_GEMM_M16"); return !(e && e[0] == '0'); }();
+  // 16x16x32 only for K-contiguous operands: with the transposed (tr-read) images of the
+  // TT dW GEMMs it measured 1.8x slower (dw_qkv 374 vs 688 TF), so those keep 32x32x16
+  auto kern = (m16 && !TA && !TB) ? gemm2_kernel<BM, BN, WM, WN, TA, TB, EPI, ACC, !TA && !TB>
+                                  : gemm2_kernel<BM, BN, WM, WN, TA, TB, EPI, ACC, false>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -612,7 +842,8 @@ static int dispatch(int cfg, const void* A, const void* B, void* C, const void* 
                     int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
                     int split, hipStream_t st) {
   if constexpr (!TA && !TB) {
-    if (cfg == 4) return launch3<EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
   }
   switch (cfg) {
     case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
@@ -648,10 +879,19 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
                              int* split_out) {
   int split = 1;
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
-  if (force_cfg >= 0 && force_cfg < 5) cfg = force_cfg;
-  // the ping-pong 256x256 engine for both-K-contiguous operands (MIPIPE_GEMM3=0 disables)
+  if (force_cfg >= 0 && force_cfg < 6) cfg = force_cfg;
+  // the ping-pong 256x256 engine for both-K-contiguous operands (MIPIPE_GEMM3=0 disables;
+  // MIPIPE_GEMM_M16=1 selects its 16x16x32-MFMA build)
   static const bool use3 = [] { const char* e = getenv("MIPIPE_GEMM3"); return !(e && e[0] == '0'); }();
-  if (cfg == 0 && !transA && !transB && use3 && force_cfg < 0) cfg = 4;
+  static const bool m16 = [] { const char* e = getenv("MIPIPE_GEMM_M16"); return !(e && e[0] == '0'); }();
+  if (cfg == 0 && !transA && !transB && use3 && force_cfg < 0) cfg = m16 ? 5 : 4;
+  // 16x16x32 MFMAs hold a higher clock under load (MI355X_MICROARCH.md DVFS item 7): the
+  // M16 ping-pong engine beat the 256x192 / 256x128 gemm2 tiles on every measured NT
+  // shape, including grids of fewer tiles than CUs (N = 768: 27.5 vs 30.8 us)
+  if (!transA && !transB && use3 && m16 && force_cfg < 0 && split == 1 && cfg != 5) {
+    const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
+    if (t256 >= 96) cfg = 5;
+  }
   if (cfg >= 4 && (transA || transB)) cfg = 0;
   if ((transA || transB) && cfg == 1) cfg = 2;
   if (!c_f32_accum) split = 1;

@@ -232,7 +232,7 @@ def test_adamw():
     assert abs(ss.item() - (g.double() ** 2).sum().item()) / ss.item() < 1e-4
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, "bias_gelu"), (1000, 2304, 256, "bias"), (256, 384, 128, "res"),
                                        (520, 136, 64, "none"), (512, 768, 3072, "dgelu"), (1000, 1000, 640, "none"),
                                        (768, 512, 128, "bias")])
@@ -274,7 +274,7 @@ def test_gemm2_dw_splitk(cfg, M, N, K):
     close(g, base + dy.float().t() @ x.float(), atol=3e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 4])
+@pytest.mark.parametrize("cfg", [-1, 1, 4, 5])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 50304), (2048, 768, 8192), (300, 200, 4096)])
 def test_gemm2_nt_splitk_accumulate(cfg, M, N, K):
     """Both-K-contiguous operands into an f32 accumulator with split-K (distributed-head dX)."""
