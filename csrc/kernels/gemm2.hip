@@ -414,17 +414,37 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
     const char* sa = smem + (t & 1) * STAGE;
     const char* sbB = sa + A_BYTES;
     // two 32-deep k-substeps; substep 1's fragments are read under substep 0's MFMAs
+    // (transposed layouts: one fragment set, the compiler overlaps what registers allow --
+    // double-buffering the 256x256 TT tile spilled)
+    if constexpr (TA || TB) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 af1[TM], bf1[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af1[i] = frag16<TA, BM>(sa, wm + 16 * i, s);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bf1[j] = frag16<TB, BN>(sbB, wn + 16 * j, s);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af1[i], bf1[j], acc[i][j]);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else {
     bf16x8 af[2][TM], bfr[2][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) af[0][i] = frag16<TA, BM>(sa, wm + 16 * i, 0);
 #pragma unroll
     for (int j = 0; j < TN; ++j) bfr[0][j] = frag16<TB, BN>(sbB, wn + 16 * j, 0);
 #pragma unroll
-    for (int i = 0; i < TM; ++i) af[1][i] = frag16<TA, BM>(sa, wm + 16 * i, 1);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) bfr[1][j] = frag16<TB, BN>(sbB, wn + 16 * j, 1);
-#pragma unroll
     for (int s = 0; s < 2; ++s) {
+      if (s == 0) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) af[1][i] = frag16<TA, BM>(sa, wm + 16 * i, 1);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) bfr[1][j] = frag16<TB, BN>(sbB, wn + 16 * j, 1);
+      }
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -433,6 +453,7 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[s][i], bfr[s][j], acc[i][j]);
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
+    }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
@@ -783,7 +804,8 @@ static int launch(const void* A, const void* B, void* C, const void* bias, const
   static const bool m16 = [] { const char* e = getenv("MIPIPE_GEMM_M16"); return !(e && e[0] == '0'); }();
   // 16x16x32 only for K-contiguous operands: with the transposed (tr-read) images of the
   // TT dW GEMMs it measured 1.8x slower (dw_qkv 374 vs 688 TF), so those keep 32x32x16
-  auto kern = (m16 && !TA && !TB) ? gemm2_kernel<BM, BN, WM, WN, TA, TB, EPI, ACC, !TA && !TB>
+  static const bool m16t = [] { const char* e = getenv("MIPIPE_GEMM_M16T"); return e && e[0] == '1'; }();
+  auto kern = (m16 && (m16t || (!TA && !TB))) ? gemm2_kernel<BM, BN, WM, WN, TA, TB, EPI, ACC, true>
                                   : gemm2_kernel<BM, BN, WM, WN, TA, TB, EPI, ACC, false>;
   static bool attr = false;
   if (!attr) {
