@@ -154,7 +154,10 @@ def main():
                    "layer_split": trainer.layer_ranges, "optimizer": "AdamW(fused, clip 1.0)",
                    "hip_graphs": bool(a.graphs),
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
-                   else "last stage"},
+                   else "last stage",
+                   "head_lag": getattr(trainer, "head_lag", None),
+                   "planned_efficiency": None if getattr(trainer, "planned_makespan", None) is None else
+                   round(trainer.planned_ideal / trainer.planned_makespan, 3)},
     }
     if loss_val is not None:
         out["last_loss"] = round(loss_val, 4)

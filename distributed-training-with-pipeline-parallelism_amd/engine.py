@@ -128,6 +128,8 @@ class PipelineTrainer:
             base = generate(self.schedule, pp, n_microbatches, v, style)
             orders, self.head_lag, self.planned_makespan = plan_head_schedule(base, pp, v, style, head_costs,
                                                                               stage_costs)
+            # no-bubble time in the same units (F = 1, B = 2 per stage-cost unit)
+            self.planned_ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * n_microbatches / pp
             head_plan = HeadPlan(chunks, cfg.d_model, runner=self.head.run, dtype=dtype)
             if graphs and self.device.type == "cuda":
                 from .parallel.graphs import GraphCache

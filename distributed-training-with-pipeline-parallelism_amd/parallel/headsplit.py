@@ -159,11 +159,17 @@ def insert_head_ops(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: i
 
 def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int, style: str,
                        head_costs: Dict[int, float], stage_costs: Optional[Sequence[float]] = None,
-                       comm: float = 0.05, lags: Sequence[int] = (0, 1, 2),
+                       comm: float = 0.05, lags: Sequence[int] = (0, 1, 2, 3, 4, 6, 8, 12, 16),
                        policies: Sequence[str] = ("head_first", "fill")
                        ) -> Tuple[Dict[int, List[Action]], int, float]:
     """Best of ``insert_head_ops`` over the candidate last-stage lags (simulated
-    makespan).  Returns (orders, lag, makespan)."""
+    makespan).  Returns (orders, lag, makespan).
+
+    Deep lags matter with 1F1B: the last stage's B(i) waits for every rank's H(i), which
+    waits for its F(i) -- a round trip on the critical cycle unless the last stage has
+    `lag` more forwards to run meanwhile.  GPT-2 small, PP=2, m=8: lag <= 2 planned 0.755
+    of ideal, lag 8 0.912; each unit of lag stashes one more microbatch per stage
+    (hundreds of MB at GPT-2 scale, cheap next to 288 GB of HBM)."""
     best = None
     for pol in policies:
         for lag in lags:
