@@ -39,6 +39,9 @@ int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, cons
                 int64_t dk_stride, int64_t dv_stride, int causal, float scale, float p_drop, uint64_t seed,
                 hipStream_t st);
 int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st);
+int mp_set_drop_step_attn(uint64_t v, hipStream_t st);
+int mp_set_drop_step_elem(uint64_t v, hipStream_t st);
+int mp_set_drop_step_norm(uint64_t v, hipStream_t st);
 int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
              int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
              int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, hipStream_t st);
@@ -257,7 +260,7 @@ bool gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torc
   int split = 1;
   mp_gemm2_plan(M, N, K, transA, transB, accum, (int)force_cfg, &split);
   torch::Tensor ws;
-  if (accum && split > 1) ws = torch::empty({(int64_t)split * M * N}, C.options().dtype(torch::kFloat32));
+  if (split > 1) ws = torch::empty({(int64_t)split * M * N}, C.options().dtype(torch::kFloat32));
   const int rc = mp_gemm2(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual),
                           mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),
                           residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
@@ -274,6 +277,15 @@ void transpose(torch::Tensor in, torch::Tensor out) {
   check(mp_transpose(in.data_ptr(), out.data_ptr(), in.size(0), in.size(1), in.stride(0), out.stride(0),
                      cur_stream()),
         "transpose");
+}
+
+// training-step counter the dropout kernels mix into their seeds (mp_common.h
+// step_seed): stream-ordered, issued before a step's first replay, never captured
+void set_dropout_step(int64_t step) {
+  const uint64_t v = (uint64_t)step;
+  check(mp_set_drop_step_attn(v, cur_stream()), "set_drop_step");
+  check(mp_set_drop_step_elem(v, cur_stream()), "set_drop_step");
+  check(mp_set_drop_step_norm(v, cur_stream()), "set_drop_step");
 }
 
 }  // namespace
@@ -304,4 +316,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm);
   m.def("gemm2", &gemm2);
   m.def("transpose", &transpose);
+  m.def("set_dropout_step", &set_dropout_step);
 }

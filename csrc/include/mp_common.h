@@ -82,6 +82,22 @@ __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
   return (uint32_t)x;
 }
 
+// Graph-safe dropout: every kernel that drops mixes a per-process training-step counter
+// into its seed on entry.  The counter lives in device memory (one copy per translation
+// unit, written by a 1-thread kernel before each step, outside any captured graph), so a
+// HIP graph captured once draws a fresh mask every replay while the forward and the
+// backward of one step still agree.
+static __device__ uint64_t mp_drop_step;
+__device__ __forceinline__ uint64_t step_seed(uint64_t seed) {
+  return seed ^ (mp_drop_step * 0xA24BAED4963EE407ull + 0x2545F4914F6CDD1Dull);
+}
+#define MP_DROP_STEP_SETTER(NAME)                                                     \
+  __global__ void NAME##_kernel(uint64_t v) { mp_drop_step = v; }                    \
+  extern "C" int NAME(uint64_t v, hipStream_t st) {                                  \
+    NAME##_kernel<<<1, 1, 0, st>>>(v);                                               \
+    return (int)hipGetLastError();                                                   \
+  }
+
 // keep with probability (1-p): returns scale (1/(1-p)) or 0
 __device__ __forceinline__ float dropout_scale(uint64_t seed, uint64_t idx, float p) {
   const uint32_t thr = (uint32_t)(p * 4294967296.0f);

@@ -125,6 +125,7 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
     float* __restrict__ LSE, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
     int64_t os, float scale, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE = 64 * DP * 2;  // bytes per [64][DP] tile
 #define kbuf(i) (smem + (i) * TILE)
@@ -324,6 +325,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs,
     int64_t ks, int64_t vs, int64_t os, int64_t dks, int64_t dvs, float scale, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE = 64 * DP * 2;
   constexpr int BUFB = 2 * TILE + 512;               // Q, dO, lse[64], delta[64]
@@ -498,6 +500,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
     float* __restrict__ DELTA,
     bf16_t* __restrict__ dQ, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
     int64_t os, int64_t dqs, float scale, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE = 64 * DP * 2;
 #define kbuf(i) (smem + (i) * TILE)
@@ -714,3 +717,5 @@ extern "C" int mp_attn_bwd(const void* q, const void* k, const void* v, const vo
 #undef MP_B
   return -1;
 }
+
+MP_DROP_STEP_SETTER(mp_set_drop_step_attn)

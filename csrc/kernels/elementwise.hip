@@ -27,6 +27,7 @@ __device__ __forceinline__ float act_g(float x, int act) {
 
 __global__ void __launch_bounds__(256) act_fwd_kernel(const bf16_t* __restrict__ a, bf16_t* __restrict__ g, int64_t n,
                                                       int act, float p, uint64_t seed) {
+  if (p > 0.f) seed = step_seed(seed);
   const int64_t n8 = n / 8;
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
     u16x8 v = reinterpret_cast<const u16x8*>(a)[i];
@@ -46,6 +47,7 @@ template <int MODE>
 __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ a,
                                                      bf16_t* __restrict__ da, float* __restrict__ dbias, int rows,
                                                      int cols, int rows_per_block, int act, float p, uint64_t seed) {
+  if (p > 0.f) seed = step_seed(seed);
   __shared__ float red[4][64 * 8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int chunk = blockIdx.y * 64 + lane;
@@ -239,3 +241,5 @@ extern "C" int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi
   transpose_kernel<<<grid, 256, 0, st>>>((const bf16_t*)in, (bf16_t*)out, R, C, ldi, ldo);
   return (int)hipGetLastError();
 }
+
+MP_DROP_STEP_SETTER(mp_set_drop_step_elem)

@@ -127,6 +127,45 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // ---- epilogue: one wave-row group at a time through LDS -> coalesced 16-byte bias /
 // residual / activation / store, or lane-consecutive f32 atomics for split-K
+// the fused epilogue of 8 consecutive outputs (row gr, columns gc..gc+7) -> bf16 C
+template <int EPI>
+__device__ __forceinline__ void epi_store8(float (&v)[8], int gr, int gc, bf16_t* __restrict__ C, int64_t ldc,
+                                           const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
+                                           int64_t ldr, bf16_t* __restrict__ AUX, int64_t ldx) {
+  if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RES) {
+    u16x8 bv = *reinterpret_cast<const u16x8*>(bias + gc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[e]);
+  }
+  if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
+    u16x8 pre;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pre[e] = f2bf(v[e]);
+      const float x = bf2f(pre[e]);
+      v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
+    }
+    *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
+  }
+  if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
+    u16x8 rv = *reinterpret_cast<const u16x8*>(R + (int64_t)gr * ldr + gc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += bf2f(rv[e]);
+  }
+  if constexpr (EPI == EPI_DGELU || EPI == EPI_DRELU) {
+    u16x8 xv = *reinterpret_cast<const u16x8*>(AUX + (int64_t)gr * ldx + gc);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = bf2f(xv[e]);
+      v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
+    }
+  }
+  u16x8 o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+  *reinterpret_cast<u16x8*>(C + (int64_t)gr * ldc + gc) = o;
+}
+
 // accumulator layout of the 32x32x16 engines: acc[i][j] element r -> wave-local
 // row 32 i + (r & 3) + 8 (r >> 2) + 4 hl, column wn + 32 j + l32
 template <int WTM, int WTN>
@@ -225,38 +264,7 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
         *reinterpret_cast<float4*>(cp) = c0;
         *reinterpret_cast<float4*>(cp + 4) = c1;
       } else {
-        if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RES) {
-          u16x8 bv = *reinterpret_cast<const u16x8*>(bias + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[e]);
-        }
-        if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
-          u16x8 pre;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            pre[e] = f2bf(v[e]);
-            const float x = bf2f(pre[e]);
-            v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
-          }
-          *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
-        }
-        if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
-          u16x8 rv = *reinterpret_cast<const u16x8*>(R + (int64_t)gr * ldr + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += bf2f(rv[e]);
-        }
-        if constexpr (EPI == EPI_DGELU || EPI == EPI_DRELU) {
-          u16x8 xv = *reinterpret_cast<const u16x8*>(AUX + (int64_t)gr * ldx + gc);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float x = bf2f(xv[e]);
-            v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
-          }
-        }
-        u16x8 o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
-        *reinterpret_cast<u16x8*>(reinterpret_cast<bf16_t*>(Cv) + (int64_t)gr * ldc + gc) = o;
+        epi_store8<EPI>(v, gr, gc, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, AUX, ldx);
       }
     }
     __syncthreads();
@@ -836,12 +844,15 @@ static int choose(int M, int N, int K, bool acc, bool outer, int* split_out) {
     if (outer && CFGS[c].bn == 192) continue;  // outer-contig images need power-of-two widths
     const int tiles = ((M + CFGS[c].bm - 1) / CFGS[c].bm) * ((N + CFGS[c].bn - 1) / CFGS[c].bn);
     const float area = (float)(CFGS[c].bm * CFGS[c].bn) / (256.f * 256.f) * (c == 3 ? 2.f : 1.f);
-    const int max_split = acc ? (kt / 4 < 32 ? kt / 4 : 32) : 1;
+    // bf16 outputs split too (f32 slabs + one reduce pass that applies the epilogue):
+    // small-M problems (1024-token microbatches) otherwise fill 24-48 of 256 CUs
+    const int max_split = acc ? (kt / 4 < 32 ? kt / 4 : 32) : (kt / 3 < 8 ? kt / 3 : 8);
     for (int s = 1; s <= (max_split > 1 ? max_split : 1); ++s) {
       const int work = tiles * s;
       const int rounds = (work + slots - 1) / slots;
       const int kper = (kt + s - 1) / s;
-      const float epi = s > 1 ? 6.f : 2.f;  // f32 atomics vs a bf16/f32 store, in k-tile units
+      // f32 slab store (+ the reduce pass for bf16 outputs) vs a direct store, in k-tile units
+      const float epi = s > 1 ? (acc ? 6.f : 8.f) : 2.f;
       const float t = rounds * (kper + epi + 2.f) * area / CFGS[c].eff;  // +2: prologue fill
       if (t < best_t * 0.999f) {
         best_t = t;
@@ -895,6 +906,39 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restr
   }
 }
 
+// bf16 C[M,N] = epilogue(alpha-scaled sum of the split-K slabs ws[s][M][N])
+template <int EPI>
+__global__ void __launch_bounds__(256) splitk_epi_kernel(const float* __restrict__ ws, bf16_t* __restrict__ C, int M,
+                                                         int N, int64_t ldc, int split, const bf16_t* __restrict__ bias,
+                                                         const bf16_t* __restrict__ R, int64_t ldr,
+                                                         bf16_t* __restrict__ AUX, int64_t ldx) {
+  const int64_t n8 = (int64_t)M * N / 8;
+  const int64_t slab = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t e = i * 8;
+    const int m = (int)(e / N), n = (int)(e % N);
+    float4 a = *reinterpret_cast<const float4*>(ws + e), b = *reinterpret_cast<const float4*>(ws + e + 4);
+    for (int s = 1; s < split; ++s) {
+      const float4 c = *reinterpret_cast<const float4*>(ws + s * slab + e);
+      const float4 d = *reinterpret_cast<const float4*>(ws + s * slab + e + 4);
+      a.x += c.x; a.y += c.y; a.z += c.z; a.w += c.w;
+      b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+    }
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    epi_store8<EPI>(v, m, n, C, ldc, bias, R, ldr, AUX, ldx);
+  }
+}
+
+template <int EPI>
+static int launch_splitk_epi(const float* ws, void* C, int M, int N, int64_t ldc, int split, const void* bias,
+                             const void* R, int64_t ldr, void* X, int64_t ldx, hipStream_t st) {
+  const int64_t n8 = (int64_t)M * N / 8;
+  const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
+  splitk_epi_kernel<EPI><<<blocks, 256, 0, st>>>(ws, (bf16_t*)C, M, N, ldc, split, (const bf16_t*)bias,
+                                                 (const bf16_t*)R, ldr, (bf16_t*)X, ldx);
+  return (int)hipGetLastError();
+}
+
 // tile config + split-K factor the engine will use for this problem (callers size the
 // split-K workspace from it: split * M * N f32)
 extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg,
@@ -916,7 +960,9 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   }
   if (cfg >= 4 && (transA || transB)) cfg = 0;
   if ((transA || transB) && cfg == 1) cfg = 2;
-  if (!c_f32_accum) split = 1;
+  // bf16-output split-K runs the f32-accumulate instantiation (NT or TT) into slabs
+  if (!c_f32_accum && transA != transB) split = 1;
+  if (!c_f32_accum && split > 1 && (cfg == 4 || cfg == 5)) cfg = transA ? 0 : cfg;
   *split_out = split;
   return cfg;
 }
@@ -933,6 +979,27 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   const int cfg = mp_gemm2_plan(M, N, K, transA, transB, c_f32_accum, force_cfg, &split);
   float* wsp = split > 1 ? ws : nullptr;
   int rc = -2;
+  if (!c_f32_accum && split > 1) {
+    // bf16 output, split-K: partial products into f32 slabs (alpha applied there), then
+    // one pass sums them and applies the fused epilogue
+    if (ws == nullptr) return -1;
+    if (transA && transB) rc = dispatch<true, true, EPI_NONE, true>(cfg, A, B, nullptr, nullptr, nullptr, nullptr, ws, M, N, K,
+                                                              lda, ldb, N, 0, 0, alpha, split, st);
+    else rc = dispatch<false, false, EPI_NONE, true>(cfg, A, B, nullptr, nullptr, nullptr, nullptr, ws, M, N, K, lda, ldb,
+                                                     N, 0, 0, alpha, split, st);
+    if (rc != 0) return rc;
+    switch (epilogue) {
+      case EPI_NONE: return launch_splitk_epi<EPI_NONE>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_BIAS: return launch_splitk_epi<EPI_BIAS>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_BIAS_GELU: return launch_splitk_epi<EPI_BIAS_GELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_BIAS_RELU: return launch_splitk_epi<EPI_BIAS_RELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_BIAS_RES: return launch_splitk_epi<EPI_BIAS_RES>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_RES: return launch_splitk_epi<EPI_RES>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_DGELU: return launch_splitk_epi<EPI_DGELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_DRELU: return launch_splitk_epi<EPI_DRELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      default: return -2;
+    }
+  }
 #define MP_G(TA_, TB_, E_, ACC_)                                                                                  \
   if (rc == -2 && (bool)transA == TA_ && (bool)transB == TB_ && epilogue == E_ && (bool)c_f32_accum == ACC_)     \
     rc = dispatch<TA_, TB_, E_, ACC_>(cfg, A, B, C, bias, residual, aux, wsp, M, N, K, lda, ldb, ldc, ld_res,       \

@@ -21,6 +21,7 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(
     const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, const bf16_t* __restrict__ w,
     const bf16_t* __restrict__ bias, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y, float* __restrict__ mean_out,
     float* __restrict__ rstd_out, int rows, int D, float eps, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -102,6 +103,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
     bf16_t* __restrict__ ds_out, bf16_t* __restrict__ dbranch, float* __restrict__ dw, float* __restrict__ dbias,
     float* __restrict__ cs_res, float* __restrict__ cs_ds, int rows, int D, int rows_per_block, float p_drop,
     uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   __shared__ float red[4][2][MAXJ * 64 * 8 > 1024 ? 1024 : MAXJ * 64 * 8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int nchunk = D >> 3;
@@ -307,3 +309,5 @@ extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w
 #undef MP_B
   return -2;
 }
+
+MP_DROP_STEP_SETTER(mp_set_drop_step_norm)

@@ -10,6 +10,7 @@ from ..parallel.dp import allreduce_flat
 from ..parallel.graphs import GraphCache
 from ..parallel.stage import StageBase
 from .config import NativeConfig
+from .. import ops
 from .native import MBContext, NativeModel, _seed
 
 
@@ -49,7 +50,9 @@ class NativeStage(StageBase):
         self._ctx = {}
         # HIP graphs (parallel/graphs.py): step 1 runs eagerly (lazy kernel init), every
         # (op, microbatch) action is captured on its first later use and replayed after
-        if graphs and (model.device.type != "cuda" or self.cfg.dropout > 0):
+        # (dropout stays graph-safe: kernels mix a device-side step counter into their
+        # seeds, ops.set_dropout_step, so replays draw fresh masks)
+        if graphs and model.device.type != "cuda":
             graphs = False
         self.graphs = GraphCache() if graphs else None
         self._gctx = {}
@@ -64,11 +67,15 @@ class NativeStage(StageBase):
     def clear_runtime_states(self):
         self._ctx.clear()
         self.step_id += 1
+        if self.cfg.dropout > 0 and self.model.device.type == "cuda":
+            ops.set_dropout_step(self.step_id, self.model.device)
 
     def forward_mb(self, mb, args, target, loss_fn, loss_scale):
         if self._graphed():
             return self._forward_graphed(mb, args, target, loss_scale)
-        ctx = MBContext(mb, _seed(self.seed, self.step_id, mb))
+        # on the GPU the step enters through the device counter (set_dropout_step), so
+        # eager and graph-replayed steps draw identical masks; the CPU ops see the seed only
+        ctx = MBContext(mb, _seed(self.seed, 0 if self.model.device.type == "cuda" else self.step_id, mb))
         x = args[0]
         out = self.model.forward(x, ctx, self.mbs, self.S, target=target if self.is_last else None,
                                  loss_scale=loss_scale)

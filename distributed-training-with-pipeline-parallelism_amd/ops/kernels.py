@@ -537,6 +537,15 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B: int, Sq: int, Sk: int, H: int, 
 # ======================================================================================
 # optimizer
 # ======================================================================================
+def set_dropout_step(step: int, device: Optional[torch.device] = None) -> None:
+    """Set the training-step counter every dropout kernel mixes into its seed (device
+    memory, stream-ordered on the current stream).  Issued once per step outside any
+    captured graph, it lets HIP-graph replays draw a fresh mask each step.  No-op on CPU."""
+    if device is not None and device.type != "cuda":
+        return
+    _ext().set_dropout_step(int(step))
+
+
 def sumsq(g: torch.Tensor, out: torch.Tensor):
     if _gpu(g):
         _ext().sumsq(g, out)

@@ -16,8 +16,10 @@ pipelines.  Design rules:
 * communication stays outside the graphs (RCCL work is posted by the runtime between
   replays, and ordered by stream waits), as do optimizer steps whose scalars change.
 
-Graphs are off by default on CPU and for configurations with dropout (the seed is a
-kernel argument and would be frozen into the graph).
+Graphs are off on CPU.  Dropout is graph-safe: the per-site seeds are static kernel
+arguments, and every dropout kernel mixes in a device-side training-step counter
+(``ops.set_dropout_step``, written before each step outside the graphs), so each replay
+draws a new mask and the backward regenerates the forward's.
 """
 from __future__ import annotations
 

@@ -104,3 +104,43 @@ def test_hip_graph_replay_matches_eager(recompute):
     assert res[True][0] == pytest.approx(res[False][0], rel=1e-4)
     # (Adam turns atomics-order noise of near-zero grads into lr-sized steps)
     torch.testing.assert_close(res[True][1], res[False][1], atol=2e-3, rtol=1e-3)
+
+
+def test_dropout_graphs_match_eager_and_refresh_masks():
+    """Dropout under HIP-graph replay (graph-safe seeds, ops.set_dropout_step): a graphed
+    trainer follows the eager one step for step (same masks), and the masks change from
+    step to step (the losses of repeated identical steps without an update differ)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mipipe.engine import PipelineTrainer
+    cfg = NativeConfig.reference(n_layers=2, n_heads=4, dim=256, vocab_size=1000, dropout=0.1, dim_feedforward=512)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randint(0, cfg.vocab_size, (8, 128), device=dev, generator=g)
+    y = torch.randint(0, cfg.vocab_size, (8, 128), device=dev, generator=g)
+    runs = {}
+    for graphs in (False, True):
+        tr = PipelineTrainer(cfg, pp=1, n_microbatches=2, mbs=4, seq_len=128, device=dev, seed=5, graphs=graphs)
+        if graphs:
+            tr.capture_graphs(x, y)
+            assert tr.stages[0].graphs is not None and len(tr.stages[0].graphs.graphs) > 0
+        else:   # the same two setup passes, eagerly, so the step counters line up
+            for _ in range(2):
+                tr.runtime.step([(c,) for c in torch.tensor_split(x, 2)], list(torch.tensor_split(y, 2)), [],
+                                return_outputs=False)
+            for a in tr.optimizer.arenas:
+                a.grad.zero_()
+        runs[graphs] = [float(tr.train_step(x, y)) for _ in range(4)]
+        if graphs:
+            assert tr.stages[0].graphs.replays > 0
+    assert runs[True] == pytest.approx(runs[False], rel=1e-5, abs=1e-5)
+    # fresh masks every step: forward-only losses of one weight state differ across steps
+    tr = PipelineTrainer(cfg, pp=1, n_microbatches=2, mbs=4, seq_len=128, device=dev, seed=5, graphs=True)
+    tr.capture_graphs(x, y)
+    ls = []
+    for _ in range(3):
+        losses = []
+        tr.runtime.step([(c,) for c in torch.tensor_split(x, 2)], list(torch.tensor_split(y, 2)), losses,
+                        return_outputs=False)
+        ls.append(float(torch.stack(losses).sum()))
+    assert len(set(ls)) == 3, ls

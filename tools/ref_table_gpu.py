@@ -1,0 +1,97 @@
+"""The reference's own benchmark workload on ONE MI355X.
+
+BASELINE.md Table 1 times `Transformer(ModelArgs(dim=768, n_layers=L, n_heads=H,
+vocab_size=10000))` (post-LN decoder layers with cross-attention over h, ReLU FFN 2048,
+dropout 0.1) at batch 32 x seq 128, 4 microbatches, 2 warmup + 5 timed iterations, on a
+10-core CPU with gloo (helper:98-143, nb:679-732).  This runs the same model family
+(native explicit-backward twin, `NativeConfig.reference`) and the same batch / microbatch
+/ iteration counts through `PipelineTrainer` at PP=1 on one GPU, bf16, dropout on, and
+prints one JSON line per (L, H) next to the reference's best published run for that
+(L, H) (any P, any schedule) and its GPipe P=2 run.
+
+Differences, stated: one GPU instead of P CPU processes (the multi-GPU rows need the
+8-GPU node the driver owns); each timed step here also runs the AdamW update (the
+reference times fwd+bwd only, §2.8-1); timing brackets all work with a device sync.
+
+    python tools/ref_table_gpu.py [--json out.json]
+"""
+import argparse
+import json
+import os
+import re
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def reference_rows():
+    """(L, H, P, schedule) -> tok/s, parsed from BASELINE.md Table 1."""
+    rows = {}
+    pat = re.compile(r"^\| tokens/s \| (\d+) \| (\d+) \| (\d+) \| (\w+) \| \d+ \| ([\d,\.]+) \|")
+    with open(os.path.join(ROOT, "BASELINE.md")) as f:
+        for line in f:
+            m = pat.match(line)
+            if m:
+                L, H, P, sched, v = m.groups()
+                rows[(int(L), int(H), int(P), sched)] = float(v.replace(",", ""))
+    return rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-graphs", action="store_true")
+    a = ap.parse_args()
+    import torch
+    import mipipe  # noqa: F401
+    from mipipe.engine import PipelineTrainer
+    from mipipe.models.config import NativeConfig
+
+    ref = reference_rows()
+    dev = torch.device("cuda", 0)
+    B, S, m = 32, 128, 4
+    out = []
+    for L in (4, 8, 12):
+        for H in (4, 8, 12):
+            cfg = NativeConfig.reference(n_layers=L, n_heads=H)
+            tr = PipelineTrainer(cfg, pp=1, schedule="1F1B", n_microbatches=m, mbs=B // m, seq_len=S, device=dev,
+                                 seed=0, graphs=not a.no_graphs)
+            g = torch.Generator(device="cuda").manual_seed(L * 100 + H)
+            x = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
+            y = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
+            if not a.no_graphs:
+                tr.capture_graphs(x, y)   # setup (not timed): per-microbatch HIP graphs, dropout-safe
+            for _ in range(a.warmup):
+                tr.train_step(x, y)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.iters):
+                loss = tr.train_step(x, y)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            tok_s = B * S * a.iters / dt
+            mine = {k: v for k, v in ref.items() if k[0] == L and k[1] == H}
+            best_k = max(mine, key=mine.get)
+            row = {"L": L, "H": H, "tokens_per_s": round(tok_s, 1), "ms_per_iter": round(dt / a.iters * 1e3, 3),
+                   "loss": round(float(loss), 4), "ref_best_tok_s": mine[best_k],
+                   "ref_best_run": f"P={best_k[2]} {best_k[3]}", "ref_gpipe_p2_tok_s": mine.get((L, H, 2, "GPipe")),
+                   "x_vs_ref_best": round(tok_s / mine[best_k], 1)}
+            out.append(row)
+            print(json.dumps(row), flush=True)
+            del tr
+            torch.cuda.empty_cache()
+    summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
+                         "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, bf16, AdamW step included, "
+                         + ("eager" if a.no_graphs else "HIP graphs"),
+               "rows": out}
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(summary, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
