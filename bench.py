@@ -41,7 +41,9 @@ def parse():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--dp", type=int, default=1)
-    ap.add_argument("--v", type=int, default=None, help="virtual stages per rank (interleaved)")
+    # (not "--v": torch.distributed.run's argparse would take it for an abbreviation of
+    # its --virtual-local-rank even after the script name)
+    ap.add_argument("--vstages", type=int, default=None, help="virtual stages per rank (interleaved)")
     ap.add_argument("--recompute", action="store_true")
     ap.add_argument("--graphs", type=int, default=None,
                     help="replay per-microbatch stage compute as HIP graphs (default: on for 1 GPU)")
@@ -81,7 +83,7 @@ def main():
     if a.graphs is None:
         a.graphs = 1 if world == 1 else 0
     trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m,
-                              mbs=a.mbs, seq_len=a.seq, v=a.v, device=device, recompute=a.recompute, seed=0,
+                              mbs=a.mbs, seq_len=a.seq, v=a.vstages, device=device, recompute=a.recompute, seed=0,
                               split_head=False if a.no_split_head else None, graphs=bool(a.graphs))
     gb = dp * m * a.mbs
     g = torch.Generator(device=device).manual_seed(1234 + trainer.mesh.dp_rank)
