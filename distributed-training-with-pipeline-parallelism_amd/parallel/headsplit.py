@@ -58,21 +58,25 @@ def head_token_split(T: int, rank_load: Sequence[float], head_load: float, align
     return [c * align for c in cnt]
 
 
-def _lag_last_stage(order: List[Action], last: int, lag: int) -> List[Action]:
-    """Delay the last stage's backward (B/I/W) of microbatch i until after its forward
-    of i+lag (the slack that lets the other ranks fit their head chunks in).  A stable
-    re-sort: relative orders of forwards and of backwards are unchanged."""
+def _lag_last_stage(order: List[Action], last, lag: int) -> List[Action]:
+    """Delay the backward (B/I/W) of microbatch i of stage(s) ``last`` (an index or a set)
+    until after that stage's forward of i+lag (the slack that lets the other ranks fit
+    their head chunks in).  A stable re-sort: relative orders of forwards and of
+    backwards are unchanged."""
     if lag <= 0:
         return list(order)
-    fpos = {a.mb: i for i, a in enumerate(order) if a.stage == last and a.op == Op.F}
+    stages = {last} if isinstance(last, int) else set(last)
+    fpos = {(a.stage, a.mb): i for i, a in enumerate(order) if a.stage in stages and a.op == Op.F}
     if not fpos:
         return list(order)
-    flast = max(fpos.values())
+    flast = {}
+    for (st, _), i in fpos.items():
+        flast[st] = max(flast.get(st, -1), i)
     keys = []
     for i, a in enumerate(order):
         k = float(i)
-        if a.stage == last and a.op in (Op.B, Op.I, Op.W):
-            k = max(k, fpos.get(a.mb + lag, flast) + 0.5)
+        if a.stage in stages and a.op in (Op.B, Op.I, Op.W):
+            k = max(k, fpos.get((a.stage, a.mb + lag), flast[a.stage]) + 0.5)
         keys.append(k)
     return [a for _, a in sorted(zip(keys, order), key=lambda t: t[0])]
 
@@ -91,11 +95,12 @@ def insert_head_ops(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: i
     base = {r: [a for a in orders.get(r, []) if a is not None and a.op.is_compute] for r in range(pp)}
     split = uses_split_backward(base)
     last_rank = s2r[S - 1]
-    if v == 1 and lag > 0:
+    if lag > 0:
         # every stage gets `lag` more warmup forwards (delaying only the last stage's
-        # backwards would starve the upstream ranks' steady state)
+        # backwards would starve the upstream ranks' steady state); with several
+        # virtual stages per rank, each of them does
         for r in range(pp):
-            base[r] = _lag_last_stage(base[r], r, lag)
+            base[r] = _lag_last_stage(base[r], {s for s in range(S) if s2r[s] == r}, lag)
     head = tuple(r for r in range(pp) if head_costs.get(r, 0.0) > 0.0)
     mbs = sorted({a.mb for a in base[last_rank] if a.op == Op.F and a.stage == S - 1})
 

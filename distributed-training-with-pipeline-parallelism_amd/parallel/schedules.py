@@ -311,4 +311,5 @@ def analytic_bubble(name: str, pp: int, m: int, v: int = 1) -> float:
     if name in ("Interleaved1F1B", "LoopedBFS"):
         return (pp - 1) / (v * m + pp - 1)
     from .simulate import simulate
-    return simulate(generate(name, pp, m, v), pp, v).bubble
+    style = REQUIRED_STYLE.get(name, "loop")
+    return simulate(generate(name, pp, m, v, style), pp, v, style).bubble
