@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
 // every SIMD one wave issues MFMAs while its partner issues ds_reads / DMA: the
 // cdna guide's 8-phase template (§5 "256^2 8-phase template"), with 32x32x16 MFMAs.
 // ---------------------------------------------------------------------------------------
-template <int EPI, bool ACC, bool M16>
+template <int EPI, bool ACC, bool M16, bool TT = false>
 __global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
 gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
              const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
@@ -534,12 +534,35 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
 
   // staging: this wave's two 1 KiB pieces (j = 0, 1) of every half-tile.  Piece rows
   // i = 64 j + 8 wave + (lane >> 3); swz8 reads row bits 1-3, i.e. i & 15 = 8 (wave & 1) + lr.
+  static_assert(!TT || M16, "the TT build exists with 16x16x32 MFMAs only");
   const int lr = lane >> 3;
   const int lc = (lane & 7) ^ (M16 ? swzq(8 * (wave & 1) + lr) : swz8(8 * (wave & 1) + lr));
   const bf16_t* pa[2];
   const bf16_t* pb[2];
+  // TT (both operands stored k-major: A^T [K][M], B [K][N], the dW GEMMs): a half-tile is a
+  // [64 k][128 col] image with 256-byte rows; piece p = wave + 8 j holds k-rows 4p..4p+3,
+  // lane l lands at k-row 4p + (l >> 4), physical chunk l & 15 = logical chunk ^ swz16(k-row)
+  // (swz16 of that row = ((l >> 4) << 2) | (wave & 3)).  Image column c of A0 is tile row
+  // c < 64 ? c : c + 64 (A1: + 64); of B0 tile column 64 (c / 32) + c % 32 (B1: + 32).
+  const bf16_t* ta1[2];
+  const bf16_t* tb1[2];
+  if constexpr (TT) {
+    const int kr = lane >> 4;
+    const int ic = 8 * ((lane & 15) ^ ((kr << 2) | (wave & 3)));
+    const int am = ic < 64 ? ic : ic + 64, bn = 64 * (ic >> 5) + (ic & 31);
+    auto cm = [&](int m) { return m < M ? m : M - 8; };
+    auto cn = [&](int n) { return n < N ? n : N - 8; };
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < 2; ++j) {
+      const int64_t krow = (int64_t)kt0 * BK + 4 * wave + 32 * j + kr;
+      pa[j] = A + krow * lda + cm(m0 + am);
+      ta1[j] = A + krow * lda + cm(m0 + am + 64);
+      pb[j] = B + krow * ldb + cn(n0 + bn);
+      tb1[j] = B + krow * ldb + cn(n0 + bn + 32);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2 && !TT; ++j) {
     int ra = m0 + 128 * j + 8 * wave + lr;          // A0 row; A1 = +64
     ra = ra < M ? ra : M - 1;
     int rb = n0 + 64 * ((wave >> 2) + 2 * j) + 8 * (wave & 3) + lr;   // B0 row (= output col); B1 = +32
@@ -557,6 +580,17 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   // half-tile h (0 = A0, 1 = B0, 2 = B1, 3 = A1: consumption order) of K-tile kt -> buffer kt & 1
   auto issue = [&](int h, int kt) {
     char* img = smem + (kt & 1) * BUF + (h == 0 ? 0 : h == 3 ? HALF : h == 1 ? 2 * HALF : 3 * HALF);
+    if constexpr (TT) {
+      const int64_t da = (int64_t)kt * BK * lda, db = (int64_t)kt * BK * ldb;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16_t* src = h == 0 ? pa[j] + da : h == 3 ? ta1[j] + da : h == 1 ? pb[j] + db : tb1[j] + db;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(img + (wave + 8 * j) * 1024), 16,
+                                         0, 0);
+      }
+      return;
+    }
     const int64_t dk = (int64_t)kt * BK;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -705,7 +739,8 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   const int rA = wr * 64 + (lane & 15);
   const int rB = wc * 32 + (lane & 15);
   auto fq = [&](const char* img, int row, int st) -> bf16x8 {
-    return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * ((4 * st + q) ^ swzq(row)));
+    if constexpr (TT) return frag16<true, 128>(img, row - (lane & 15), st);   // row = base + (lane & 15)
+    else return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * ((4 * st + q) ^ swzq(row)));
   };
 
 #define G4_MFMA(R0, BF, C0)                                                              \
@@ -780,7 +815,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   }
 }
 
-template <int EPI, bool ACC, bool M16>
+template <int EPI, bool ACC, bool M16, bool TT = false>
 static int launch3(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
                    int N, int K,
                    int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
@@ -788,7 +823,7 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
   constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
   constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
-  auto kern = gemm3_kernel<EPI, ACC, M16>;
+  auto kern = gemm3_kernel<EPI, ACC, M16, TT>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -874,6 +909,9 @@ static int dispatch(int cfg, const void* A, const void* B, void* C, const void* 
                     int M,
                     int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
                     int split, hipStream_t st) {
+  if constexpr (TA && TB && ACC && EPI == EPI_NONE) {
+    if (cfg == 6) return launch3<EPI, ACC, true, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+  }
   if constexpr (!TA && !TB) {
     if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
     if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
@@ -945,7 +983,7 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
                              int* split_out) {
   int split = 1;
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
-  if (force_cfg >= 0 && force_cfg < 6) cfg = force_cfg;
+  if (force_cfg >= 0 && force_cfg < 7) cfg = force_cfg;
   // the ping-pong 256x256 engine for both-K-contiguous operands (MIPIPE_GEMM3=0 disables;
   // MIPIPE_GEMM_M16=1 selects its 16x16x32-MFMA build)
   static const bool use3 = [] { const char* e = getenv("MIPIPE_GEMM3"); return !(e && e[0] == '0'); }();
@@ -958,7 +996,12 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
     const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 96) cfg = 5;
   }
-  if (cfg >= 4 && (transA || transB)) cfg = 0;
+  // the TT (dW) build of the ping-pong engine: 256x256 tiles, split-K f32 accumulate
+  // (MIPIPE_GEMM3T=0 keeps the 2-stage gemm2 TT engine)
+  static const bool use3t = [] { const char* e = getenv("MIPIPE_GEMM3T"); return !(e && e[0] == '0'); }();
+  if (cfg == 0 && transA && transB && c_f32_accum && use3t && force_cfg < 0 && M % 8 == 0 && N % 8 == 0) cfg = 6;
+  if (cfg == 6 && !(transA && transB && c_f32_accum)) cfg = 0;
+  if (cfg >= 4 && cfg != 6 && (transA || transB)) cfg = 0;
   if ((transA || transB) && cfg == 1) cfg = 2;
   // bf16-output split-K runs the f32-accumulate instantiation (NT or TT) into slabs
   if (!c_f32_accum && transA != transB) split = 1;

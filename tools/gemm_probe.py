@@ -1,6 +1,6 @@
 """Run one GEMM shape a few times (for rocprofv3 --pmc counter collection).
 
-    python tools/gemm_probe.py M N K [cfg] [layout: nt|tt] [iters]"""
+    python tools/gemm_probe.py M N K [cfg] [layout: nt|ntacc|tt] [iters]"""
 import os
 import sys
 
@@ -19,6 +19,11 @@ if layout == "nt":
     b = torch.randn(N, K, device="cuda").to(torch.bfloat16)
     c = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     fn = lambda: _k._gemm(a, b, c, cfg=cfg)
+elif layout == "ntacc":   # the dW problem with both operands K-contiguous (f32 accumulate, split-K)
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    b = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    c = torch.zeros(M, N, device="cuda", dtype=torch.float32)
+    fn = lambda: _k._gemm(a, b, c, accum=True, cfg=cfg)
 else:
     a = torch.randn(K, M, device="cuda").to(torch.bfloat16)
     b = torch.randn(K, N, device="cuda").to(torch.bfloat16)
