@@ -70,8 +70,20 @@ __global__ void __launch_bounds__(256) xent_kernel(bf16_t* __restrict__ logits, 
 // Register-resident variant: 512 threads hold the whole row (CPT 16-byte chunks each), so
 // the logits are read from HBM exactly once and the gradient written once; exp2 with
 // log2(e) folded into one fma.
-template <int CPT, bool WRITE_GRAD>
-__global__ void __launch_bounds__(512) xent_reg_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ target,
+// opaque to the optimizer: keeps the row as packed bf16 words between passes instead of
+// 8x as many live unpacked floats (which capped the kernel at 1 row in flight per CU)
+template <int CPT>
+__device__ __forceinline__ void keep_packed(u16x8 (&v)[CPT]) {
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    uint4 w = __builtin_bit_cast(uint4, v[i]);
+    asm volatile("" : "+v"(w.x), "+v"(w.y), "+v"(w.z), "+v"(w.w));
+    v[i] = __builtin_bit_cast(u16x8, w);
+  }
+}
+
+template <int CPT, bool WRITE_GRAD, int NTH = 512>
+__global__ void __launch_bounds__(NTH) xent_reg_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ target,
                                                        float* __restrict__ loss, int T, int V, int Vp,
                                                        float grad_scale, int64_t ignore_index) {
   __shared__ float red[16];
@@ -80,32 +92,45 @@ __global__ void __launch_bounds__(512) xent_reg_kernel(bf16_t* __restrict__ logi
   bf16_t* x = logits + (size_t)row * Vp;
   const int64_t tgt = target[row];
   const int nchunk = Vp >> 3;
+  const int nfull = V >> 3;  // chunks entirely inside the real vocabulary: no per-element checks
   u16x8 v[CPT];
   float m = -INFINITY;
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
-    const int c = threadIdx.x + 512 * i;
-    if (c < nchunk) {
-      v[i] = *reinterpret_cast<const u16x8*>(x + c * 8);
+    const int c = threadIdx.x + NTH * i;
+    if (c < nchunk) v[i] = *reinterpret_cast<const u16x8*>(x + c * 8);
+  }
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int c = threadIdx.x + NTH * i;
+    if (c < nfull) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) m = fmaxf(m, bf2f(v[i][e]));
+    } else if (c < nchunk) {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (c * 8 + e < V) m = fmaxf(m, bf2f(v[i][e]));
     }
   }
-  const float gm = block_max<512>(m, red);
+  keep_packed<CPT>(v);
+  const float gm = block_max<NTH>(m, red);
   const float mc = gm * L2E;
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
-    const int c = threadIdx.x + 512 * i;
-    if (c < nchunk) {
+    const int c = threadIdx.x + NTH * i;
+    if (c < nfull) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += __builtin_amdgcn_exp2f(__builtin_fmaf(bf2f(v[i][e]), L2E, -mc));
+    } else if (c < nchunk) {
 #pragma unroll
       for (int e = 0; e < 8; ++e)
         if (c * 8 + e < V) s += __builtin_amdgcn_exp2f(__builtin_fmaf(bf2f(v[i][e]), L2E, -mc));
     }
   }
+  keep_packed<CPT>(v);
   __syncthreads();
-  const float gs = block_sum<512>(s, red);
+  const float gs = block_sum<NTH>(s, red);
   const float lse = gm + __logf(gs);
   const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
   if (threadIdx.x == 0) loss[row] = valid ? lse - bf2f(x[tgt]) : 0.f;
@@ -115,8 +140,15 @@ __global__ void __launch_bounds__(512) xent_reg_kernel(bf16_t* __restrict__ logi
   const float lc = lse * L2E;
 #pragma unroll
   for (int i = 0; i < CPT; ++i) {
-    const int c = threadIdx.x + 512 * i;
-    if (c < nchunk) {
+    const int c = threadIdx.x + NTH * i;
+    if (c < nfull) {
+      u16x8 o;
+      const int te = tgt - 8 * c;   // target's slot in this chunk (usually out of range)
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        o[e] = f2bf((__builtin_amdgcn_exp2f(__builtin_fmaf(bf2f(v[i][e]), L2E, -lc)) - (e == te ? 1.f : 0.f)) * sc);
+      *reinterpret_cast<u16x8*>(x + c * 8) = o;
+    } else if (c < nchunk) {
       u16x8 o;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -144,8 +176,17 @@ extern "C" int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss,
                                                      ignore_index);                                             \
     return (int)hipGetLastError();                                                                               \
   }
-  MP_XR(4) MP_XR(16) MP_XR(32)
+  MP_XR(4) MP_XR(13) MP_XR(16)
 #undef MP_XR
+  if (nchunk <= 1024 * 16) {  // large vocabularies (Llama-3: 128256): 1024 threads, 16 chunks each
+    if (write_grad)
+      xent_reg_kernel<16, true, 1024><<<T, 1024, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,
+                                                         ignore_index);
+    else
+      xent_reg_kernel<16, false, 1024><<<T, 1024, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,
+                                                          ignore_index);
+    return (int)hipGetLastError();
+  }
   if (write_grad)
     xent_kernel<true><<<T, 256, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale, ignore_index);
   else

@@ -52,7 +52,7 @@ def test_norm_fwd_bwd(kind, D, branch):
             close(b, a, atol=3e-2, rtol=3e-2)
 
 
-@pytest.mark.parametrize("V,Vp", [(50257, 50304), (10000, 10000), (1000, 1024)])
+@pytest.mark.parametrize("V,Vp", [(50257, 50304), (10000, 10000), (1000, 1024), (128256, 128256)])
 def test_xent(V, Vp):
     torch.manual_seed(0)
     T = 64
