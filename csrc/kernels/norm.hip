@@ -133,18 +133,42 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
   }
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
+  // software pipeline over this wave's rows: row i+1's dy / s / dres loads are in flight
+  // while row i is reduced and written (one row at a time exposed the load latency)
+  u16x8 pdv[MAXJ], psv[MAXJ], prv[HAS_DRES ? MAXJ : 1];
+  auto fetch = [&](int row) {
+    const size_t b = (size_t)row * D;
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      const int c = lane + 64 * j;
+      if (c < nchunk) {
+        pdv[j] = *reinterpret_cast<const u16x8*>(dy + b + c * 8);
+        psv[j] = *reinterpret_cast<const u16x8*>(s + b + c * 8);
+        if constexpr (HAS_DRES) prv[j] = *reinterpret_cast<const u16x8*>(dres + b + c * 8);
+      }
+    }
+  };
+  if (r0 + wv < r1) fetch(r0 + wv);
   for (int row = r0 + wv; row < r1; row += 4) {
     const size_t base = (size_t)row * D;
     const float mean = RMS ? 0.f : mean_in[row];
     const float rstd = rstd_in[row];
+    u16x8 cdv[MAXJ], csv[MAXJ], crv[HAS_DRES ? MAXJ : 1];
+#pragma unroll
+    for (int j = 0; j < MAXJ; ++j) {
+      cdv[j] = pdv[j];
+      csv[j] = psv[j];
+      if constexpr (HAS_DRES) crv[j] = prv[j];
+    }
+    if (row + 4 < r1) fetch(row + 4);
     float xh[MAXJ][8], g[MAXJ][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
       const int c = lane + 64 * j;
       if (c < nchunk) {
-        u16x8 dv = *reinterpret_cast<const u16x8*>(dy + base + c * 8);
-        u16x8 sv = *reinterpret_cast<const u16x8*>(s + base + c * 8);
+        u16x8 dv = cdv[j];
+        u16x8 sv = csv[j];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float d = bf2f(dv[e]);
@@ -166,7 +190,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
       const int c = lane + 64 * j;
       if (c < nchunk) {
         u16x8 rv;
-        if (HAS_DRES) rv = *reinterpret_cast<const u16x8*>(dres + base + c * 8);
+        if constexpr (HAS_DRES) rv = crv[j];
         u16x8 out, bout;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
