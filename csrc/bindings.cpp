@@ -44,7 +44,7 @@ int mp_set_drop_step_elem(uint64_t v, hipStream_t st);
 int mp_set_drop_step_norm(uint64_t v, hipStream_t st);
 int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
              int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
-             int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, hipStream_t st);
+             int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, float* colsum, hipStream_t st);
 int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg, int* split_out);
 int mp_gemm(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
@@ -247,15 +247,20 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch
 
 // v2 engine (8 waves, glds staging).  Returns false if the combination is not provided
 // by v2 (the caller then uses gemm()).
-bool gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> bias,
-           c10::optional<torch::Tensor> residual, c10::optional<torch::Tensor> aux, bool transA, bool transB,
-           int64_t epilogue, bool accum, double alpha, int64_t force_cfg) {
+// returns 1 if done, 0 if the combination is not provided by v2 (caller uses gemm()),
+// 2 if done WITHOUT the requested fused column sums (caller sums separately)
+int64_t gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> bias,
+              c10::optional<torch::Tensor> residual, c10::optional<torch::Tensor> aux, bool transA, bool transB,
+              int64_t epilogue, bool accum, double alpha, int64_t force_cfg, c10::optional<torch::Tensor> colsum) {
   const int M = C.size(0), N = C.size(1);
   const int K = transA ? A.size(0) : A.size(1);
   TORCH_CHECK((transA ? A.size(1) : A.size(0)) == M, "gemm2: A/M mismatch");
   TORCH_CHECK((transB ? B.size(0) : B.size(1)) == K && (transB ? B.size(1) : B.size(0)) == N, "gemm2: B mismatch");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm2: inner dims must be contiguous");
   TORCH_CHECK(!accum || C.scalar_type() == torch::kFloat32, "gemm2: accumulate needs f32 C");
+  TORCH_CHECK(!colsum.has_value() || (colsum->scalar_type() == torch::kFloat32 && colsum->is_contiguous() &&
+                                      colsum->numel() >= N),
+              "gemm2: colsum must be a contiguous f32 [N] tensor");
   // split-K slabs (plain stores + one reduce pass instead of f32 atomics)
   int split = 1;
   mp_gemm2_plan(M, N, K, transA, transB, accum, (int)force_cfg, &split);
@@ -265,10 +270,21 @@ bool gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torc
                           mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),
                           residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
                           transA, transB, epilogue, accum, (float)alpha, (int)force_cfg,
-                          ws.defined() ? ws.data_ptr<float>() : nullptr, cur_stream());
-  if (rc == -2 || rc == -1) return false;
+                          ws.defined() ? ws.data_ptr<float>() : nullptr,
+                          colsum.has_value() ? colsum->data_ptr<float>() : nullptr, cur_stream());
+  if (rc == -3) {
+    const int rc2 = mp_gemm2(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual),
+                             mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),
+                             residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
+                             transA, transB, epilogue, accum, (float)alpha, (int)force_cfg,
+                             ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream());
+    if (rc2 == -2 || rc2 == -1) return 0;
+    check(rc2, "gemm2");
+    return 2;
+  }
+  if (rc == -2 || rc == -1) return 0;
   check(rc, "gemm2");
-  return true;
+  return 1;
 }
 
 void transpose(torch::Tensor in, torch::Tensor out) {

@@ -212,6 +212,13 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
   constexpr int RG = BM / WM;      // rows per group
   constexpr int CP = BN + 4;       // f32 pitch
   float* ct = reinterpret_cast<float*>(smem);
+  // bf16 outputs with WS != nullptr: also accumulate the column sums of the final values
+  // into WS[N] (f32; the bias gradient of the next layer).  Every thread keeps the same 8
+  // columns over all its rows (NTH is a multiple of BN / 8), so the sums stay in registers
+  // until one LDS reduction and BN atomics per tile.
+  constexpr bool CS_OK = !ACC && (NTH % (BN / 8) == 0);
+  const bool cs = CS_OK && WS != nullptr;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
   for (int pass = 0; pass < WM; ++pass) {
     if (wr == pass) stage(ct, CP);
@@ -265,9 +272,28 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
         *reinterpret_cast<float4*>(cp + 4) = c1;
       } else {
         epi_store8<EPI>(v, gr, gc, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, AUX, ldx);
+        if (cs) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) csum[e] += v[e];
+        }
       }
     }
     __syncthreads();
+  }
+  if constexpr (CS_OK) {
+    if (cs) {
+      float* red = ct;   // [NTH][8]
+#pragma unroll
+      for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = csum[e];
+      __syncthreads();
+      constexpr int CH = BN / 8, GRP = NTH / CH;   // column chunks; threads per chunk
+      for (int c = threadIdx.x; c < BN; c += NTH) {
+        float t = 0.f;
+#pragma unroll 4
+        for (int g = 0; g < GRP; ++g) t += red[(g * CH + c / 8) * 8 + (c & 7)];
+        if (n0 + c < N) atomicAdd(WS + n0 + c, t);
+      }
+    }
   }
 }
 
@@ -1016,11 +1042,17 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
 extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux,
                         int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux,
                         int transA, int transB, int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws,
-                        hipStream_t st) {
+                        float* colsum, hipStream_t st) {
   if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
   int split = 1;
   const int cfg = mp_gemm2_plan(M, N, K, transA, transB, c_f32_accum, force_cfg, &split);
-  float* wsp = split > 1 ? ws : nullptr;
+  if (colsum != nullptr) {
+    // fused output column sums: bf16 outputs, one pass (no split-K), tiles whose width
+    // divides the 512-thread epilogue (not 256x192); -3 tells the caller to sum separately
+    if (c_f32_accum || split > 1 || cfg == 1) return -3;
+    ws = colsum;
+  }
+  float* wsp = (split > 1 || colsum != nullptr) ? ws : nullptr;
   int rc = -2;
   if (!c_f32_accum && split > 1) {
     // bf16 output, split-K: partial products into f32 slabs (alpha applied there), then
@@ -1058,7 +1090,7 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   MP_G(true, true, EPI_NONE, true)
   MP_G(false, false, EPI_NONE, true)
 #undef MP_G
-  if (rc == 0 && wsp != nullptr) {
+  if (rc == 0 && wsp != nullptr && split > 1) {
     const int64_t n4 = (int64_t)M * N / 4;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 4096);
     splitk_reduce_kernel<<<blocks, 256, 0, st>>>(wsp, reinterpret_cast<float*>(C), M, N, ldc, split);

@@ -319,11 +319,11 @@ class Block:
                 dh2 = ops.linear_dx(dgu, self.w("ffn.w13.weight"), wt=self.wt("ffn.w13.weight"))
             else:
                 gact, a, h2 = st["g"], st["a"], st["h2"]
+                # the fc1 bias gradient (column sums of da) is accumulated by the dX GEMM's
+                # epilogue instead of a second pass over da
                 da = ops.linear_dx(dy, self.w("ffn.w2.weight"), act_input=a, act=cfg.activation,
-                                   wt=self.wt("ffn.w2.weight"))
+                                   wt=self.wt("ffn.w2.weight"), colsum=self.g("ffn.w1.bias") if cfg.bias else None)
                 wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
-                if cfg.bias:
-                    wjobs.append(lambda da=da: ops.colsum(da, self.g("ffn.w1.bias")))
                 wjobs.append(lambda da=da, h2=h2: ops.linear_dw(da, h2, self.g("ffn.w1.weight")))
                 dh2 = ops.linear_dx(da, self.w("ffn.w1.weight"), wt=self.wt("ffn.w1.weight"))
             fuse_cs = cfg.bias and kind == "layernorm"

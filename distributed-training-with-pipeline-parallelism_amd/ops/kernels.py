@@ -221,12 +221,20 @@ def embed_bwd(idx: torch.Tensor, dout: torch.Tensor, dwte: torch.Tensor, dwpe: O
 # GEMMs (linear layers)
 # ======================================================================================
 def _gemm(A, B, C, bias=None, residual=None, aux=None, transA=False, transB=False, epi=EPI_NONE, accum=False,
-          alpha=1.0, cfg: int = -1):
+          alpha=1.0, cfg: int = -1, colsum=None):
+    """``colsum`` (f32 [N]): also accumulate the column sums of the bf16 output (fused in
+    the GEMM epilogue where the engine supports it, else one extra pass)."""
     e = _ext()
-    if GEMM_V >= 2 and e.gemm2(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum),
-                               float(alpha), int(cfg)):
-        return C
+    if GEMM_V >= 2:
+        rc = e.gemm2(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum), float(alpha),
+                     int(cfg), colsum)
+        if rc:
+            if rc == 2 and colsum is not None:
+                e.colsum(C, colsum)
+            return C
     e.gemm(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum), float(alpha))
+    if colsum is not None:
+        e.colsum(C, colsum)
     return C
 
 
@@ -300,7 +308,7 @@ def _act_grad_cpu(x, act):
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tensor] = None, act: str = "none",
               out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
-              wt: Optional[torch.Tensor] = None):
+              wt: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None):
     """dx = dy @ w  (w [N,K]), optionally times act'(act_input) (the previous layer's
     pre-activation) and plus ``residual``.  With ``wt`` (= w^T, [K,N], kept by the param
     arena) the GEMM runs in the both-K-contiguous form on the v2 engine."""
@@ -317,11 +325,11 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
             out.copy_(acc)
             return out
         if act != "none":
-            _gemm(dy, wt, out, aux=act_input, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU)
+            _gemm(dy, wt, out, aux=act_input, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU, colsum=colsum)
         elif residual is not None:
-            _gemm(dy, wt, out, residual=residual, epi=EPI_RES)
+            _gemm(dy, wt, out, residual=residual, epi=EPI_RES, colsum=colsum)
         else:
-            _gemm(dy, wt, out)
+            _gemm(dy, wt, out, colsum=colsum)
         return out
     if _gpu(dy):
         if act != "none":
@@ -332,6 +340,8 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
             torch.mm(dy, w, out=out)
         else:
             _gemm(dy, w, out, transB=True)
+        if colsum is not None:
+            _ext().colsum(out, colsum)
         return out
     g = dy.float() @ w.float()
     if act != "none":
@@ -339,6 +349,8 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
     if residual is not None:
         g = g + residual.float()
     out.copy_(g.to(out.dtype))
+    if colsum is not None:
+        colsum += out.float().sum(0)
     return out
 
 

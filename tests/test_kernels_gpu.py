@@ -336,3 +336,21 @@ def test_native_rccl_engine_self_transfer():
     with open("/proc/self/maps") as f:
         libs = {line.split()[-1] for line in f if "librccl" in line}
     assert len(libs) == 1, libs
+
+
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 5])
+@pytest.mark.parametrize("epi", ["dgelu", "none", "res"])
+def test_gemm_fused_colsum(cfg, epi):
+    """Output column sums accumulated in the GEMM epilogue (the next layer's bias grad);
+    configs without the fused path (256x192) fall back to a separate pass."""
+    from mipipe.ops import kernels as _k
+    torch.manual_seed(1)
+    M, N, K = 1024, 768, 512
+    x, w, r, aux = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(M, N), rnd(M, N)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    cs = torch.full((N,), 0.5, device=DEV)
+    epi_id = dict(none=0, res=5, dgelu=6)[epi]
+    _k._gemm(x.to(DEV), w.to(DEV), y, residual=r.to(DEV) if epi == "res" else None,
+             aux=aux.to(DEV) if epi == "dgelu" else None, epi=epi_id, cfg=cfg, colsum=cs)
+    ref = y.float().cpu().sum(0) + 0.5
+    close(cs, ref, atol=0.05 * (M ** 0.5), rtol=2e-2)
