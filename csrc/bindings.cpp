@@ -37,7 +37,7 @@ int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, cons
                 float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int Hkv, int D,
                 int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride, int64_t dq_stride,
                 int64_t dk_stride, int64_t dv_stride, int causal, float scale, float p_drop, uint64_t seed,
-                hipStream_t st);
+                float* csq, float* csk, float* csv, hipStream_t st);
 int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st);
 int mp_set_drop_step_attn(uint64_t v, hipStream_t st);
 int mp_set_drop_step_elem(uint64_t v, hipStream_t st);
@@ -219,12 +219,21 @@ void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o
 void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o, torch::Tensor dout,
               torch::Tensor lse, torch::Tensor delta, torch::Tensor dq, torch::Tensor dk, torch::Tensor dv,
               int64_t B, int64_t Sq, int64_t Sk, int64_t H, int64_t Hkv, int64_t D, bool causal,
-              double scale, double p, int64_t seed) {
+              double scale, double p, int64_t seed, c10::optional<torch::Tensor> dbias) {
   TORCH_CHECK(o.stride(0) == dout.stride(0), "o and dout must share a row stride");
+  // dbias: f32 [(H + 2 Hkv) D] QKV bias gradient, accumulated by the kernels (q | k | v)
+  float* cs = nullptr;
+  if (dbias.has_value()) {
+    TORCH_CHECK(dbias->scalar_type() == torch::kFloat32 && dbias->is_contiguous() &&
+                    dbias->numel() == (H + 2 * Hkv) * D,
+                "attn_bwd: dbias must be a contiguous f32 [(H + 2 Hkv) D] tensor");
+    cs = dbias->data_ptr<float>();
+  }
   check(mp_attn_bwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), dout.data_ptr(), lse.data_ptr<float>(),
                     delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(), B,
                     Sq, Sk, H, Hkv, D, q.stride(0), k.stride(0), v.stride(0), o.stride(0), dq.stride(0), dk.stride(0),
-                    dv.stride(0), causal, (float)scale, (float)p, (uint64_t)seed, cur_stream()),
+                    dv.stride(0), causal, (float)scale, (float)p, (uint64_t)seed, cs,
+                    cs ? cs + H * D : nullptr, cs ? cs + (H + Hkv) * D : nullptr, cur_stream()),
         "attn_bwd");
 }
 

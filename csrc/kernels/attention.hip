@@ -307,6 +307,30 @@ struct GTile {
   }
 };
 
+// Column sums over a workgroup's 128 token rows of a [rows][D] f32 register tile (lane =
+// row 32 w + l32, register 4g + e of acc[d] = column 32d + 8g + 4hl + e), times `mul`,
+// atomically added to out[0 .. D): the bias gradient of the QKV projection, fused into the
+// attention backward instead of a second pass over dQKV.  Sums over the 32 lanes of each
+// half by xor-shuffles, over the 4 waves through LDS (`red`, >= 4 * DP floats; the caller
+// has synchronised so it is free), then one atomic per column per workgroup.
+template <int DP>
+__device__ __forceinline__ void wg_colsum_atomic(const f32x16 (&acc)[DP / 32], float mul, bool valid, float* red,
+                                                 float* __restrict__ out, int D) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      float x = valid ? acc[d][r] * mul : 0.f;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) x += __shfl_xor(x, o, 64);
+      if (l32 == 0) red[w * DP + 32 * d + 8 * (r >> 2) + 4 * hl + (r & 3)] = x;
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < DP; c += 256)
+    if (c < D) atomicAdd(out + c, red[c] + red[DP + c] + red[2 * DP + c] + red[3 * DP + c]);
+}
+
 template <int N>
 __device__ __forceinline__ void attn_wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | (((N >> 4) & 3) << 14));
@@ -324,7 +348,8 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
     bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs,
-    int64_t ks, int64_t vs, int64_t os, int64_t dks, int64_t dvs, float scale, float p_drop, uint64_t seed) {
+    int64_t ks, int64_t vs, int64_t os, int64_t dks, int64_t dvs, float scale, float p_drop, uint64_t seed,
+    float* __restrict__ CSK, float* __restrict__ CSV) {
   if (p_drop > 0.f) seed = step_seed(seed);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE = 64 * DP * 2;
@@ -466,6 +491,14 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
       }
     }
   }
+  // ---- fused bias-gradient column sums of dK (scaled) and dV
+  if (CSK != nullptr) {
+    __syncthreads();   // the Q / dO ring is free
+    float* red = reinterpret_cast<float*>(smem);
+    wg_colsum_atomic<DP>(dk, scale, kvalid, red, CSK + (int64_t)hk * D, D);
+    __syncthreads();
+    wg_colsum_atomic<DP>(dv, 1.f, kvalid, red, CSV + (int64_t)hk * D, D);
+  }
   // ---- epilogue: lane = key, registers = d
   if (kvalid) {
     bf16_t* dkrow = dK + ((int64_t)b * Sk + key) * dks + (int64_t)hk * D;
@@ -499,7 +532,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
     const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     float* __restrict__ DELTA,
     bf16_t* __restrict__ dQ, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
-    int64_t os, int64_t dqs, float scale, float p_drop, uint64_t seed) {
+    int64_t os, int64_t dqs, float scale, float p_drop, uint64_t seed, float* __restrict__ CSQ) {
   if (p_drop > 0.f) seed = step_seed(seed);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE = 64 * DP * 2;
@@ -613,6 +646,10 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
       vst.store(vbuf(cur ^ 1));
     }
   }
+  if (CSQ != nullptr) {
+    __syncthreads();   // K / V tiles no longer read
+    wg_colsum_atomic<DP>(dq, scale, qvalid, reinterpret_cast<float*>(smem), CSQ + (int64_t)h * D, D);
+  }
   if (qvalid) {
     bf16_t* drow = dQ + ((int64_t)b * Sq + qrow) * dqs + (int64_t)h * D;
 #pragma unroll
@@ -653,7 +690,7 @@ template <int DP, bool CAUSAL, bool DROP>
 static int launch_bwd(const void* q, const void* k, const void* v, const void* o, const void* dout, const float* lse,
                       float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int Hkv, int D,
                       int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs, int64_t dks, int64_t dvs,
-                      float scale, float p, uint64_t seed, hipStream_t st) {
+                      float scale, float p, uint64_t seed, float* csq, float* csk, float* csv, hipStream_t st) {
   {
     const size_t lds = 4 * 64 * DP * 2;
     auto kern = attn_bwd_dq_kernel<DP, CAUSAL, DROP>;
@@ -661,7 +698,7 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
     dim3 grid((Sq + 127) / 128, B * H);
     kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
                                  (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os,
-                                 dqs, scale, p, seed);
+                                 dqs, scale, p, seed, csq);
   }
   {
     const size_t lds = (DP <= 128 ? 3 : 2) * (2 * 64 * DP * 2 + 512);
@@ -670,7 +707,7 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
     dim3 grid((Sk + 127) / 128, B * Hkv);
     kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)dout, lse,
                                  delta, (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, dks, dvs,
-                                 scale, p, seed);
+                                 scale, p, seed, csk, csv);
   }
   return (int)hipGetLastError();
 }
@@ -703,14 +740,15 @@ extern "C" int mp_attn_bwd(const void* q, const void* k, const void* v, const vo
                            const float* lse, float* delta, void* dq, void* dk, void* dv, int B, int Sq,
                            int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs,
                            int64_t dks, int64_t dvs, int causal, float scale, float p_drop, uint64_t seed,
-                           hipStream_t st) {
+                           float* csq, float* csk, float* csv, hipStream_t st) {
   const int DP = pick_dp(D);
+  if ((csq == nullptr) != (csk == nullptr) || (csk == nullptr) != (csv == nullptr)) return -1;
   if (DP < 0 || D % 8 || H % Hkv) return -1;
   const bool drop = p_drop > 0.f;
 #define MP_B(DPV, C, DR)                                                                                             \
   if (DP == DPV && (bool)causal == C && drop == DR)                                                                  \
     return launch_bwd<DPV, C, DR>(q, k, v, o, dout, lse, delta, dq, dk, dv, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os, dqs, \
-                                  dks, dvs, scale, p_drop, seed, st);
+                                  dks, dvs, scale, p_drop, seed, csq, csk, csv, st);
   MP_B(64, true, false) MP_B(64, false, false) MP_B(64, true, true) MP_B(64, false, true)
   MP_B(128, true, false) MP_B(128, false, false) MP_B(128, true, true) MP_B(128, false, true)
   MP_B(256, true, false) MP_B(256, false, false) MP_B(256, true, true) MP_B(256, false, true)

@@ -17,6 +17,7 @@ so checkpoints are per-stage shards that re-split to any PP degree (SURVEY §2.7
 from __future__ import annotations
 
 import hashlib
+import os
 import math
 from dataclasses import dataclass
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -163,6 +164,13 @@ class MBContext:
         self.seed = seed
         self.layers: Dict[int, dict] = {}
         self.misc: dict = {}
+
+
+# MIPIPE_FUSE_QKV_BIAS=1: the attention backward kernels sum the QKV bias gradient
+# themselves.  Off by default: measured 2 % slower end to end (same-box A/B, GPT-2 small:
+# 740K vs 754K tok/s) than the separate colsum pass -- the cross-lane reductions and the
+# contended per-column atomics in the attention epilogue cost more than re-reading dQKV
+_FUSE_QKV_BIAS = os.environ.get("MIPIPE_FUSE_QKV_BIAS", "0") == "1"
 
 
 def _seed(base: int, *parts: int) -> int:
@@ -343,13 +351,17 @@ class Block:
             q, k, v = qkv[:, : H * Dh], qkv[:, H * Dh:(H + KV) * Dh], qkv[:, (H + KV) * Dh:]
             dqkv = torch.empty_like(qkv)
             dq, dk, dv = dqkv[:, : H * Dh], dqkv[:, H * Dh:(H + KV) * Dh], dqkv[:, (H + KV) * Dh:]
+            # the QKV bias gradient is summed by the attention backward kernels themselves
+            # (no second pass over dQKV), unless RoPE still has to rotate dQ/dK afterwards
+            fuse_qkv_bias = cfg.bias and cfg.pos != "rope" and _FUSE_QKV_BIAS
             ops.attn_bwd(q, k, v, o, do, st["lse"], dq, dk, dv, B, S, S, H, KV, Dh, cfg.causal,
-                         p_drop=cfg.dropout, seed=_seed(sd, 1))
+                         p_drop=cfg.dropout, seed=_seed(sd, 1),
+                         dbias=self.g("attn.wqkv.bias") if fuse_qkv_bias else None)
             if cfg.pos == "rope":
                 ops.rope_(dqkv, self.rope[0], self.rope[1], S, H, KV, Dh, inverse=True)
             h1 = st["h1"]
             wjobs.append(lambda dqkv=dqkv, h1=h1: ops.linear_dw(dqkv, h1, self.g("attn.wqkv.weight")))
-            if cfg.bias:
+            if cfg.bias and not fuse_qkv_bias:
                 wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, self.g("attn.wqkv.bias")))
             dh1 = ops.linear_dx(dqkv, self.w("attn.wqkv.weight"), wt=self.wt("attn.wqkv.weight"))
             dx, _ = ops.norm_bwd(dh1, st["x"], self.w("attn_norm.weight"), st["mu1"], st["rs1"], kind=kind,

@@ -510,14 +510,16 @@ def attn_fwd(q, k, v, o, lse, B: int, Sq: int, Sk: int, H: int, Hkv: int, D: int
 
 
 def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B: int, Sq: int, Sk: int, H: int, Hkv: int, D: int, causal: bool,
-             scale: Optional[float] = None, p_drop: float = 0.0, seed: int = 0, delta=None):
-    """Writes dq, dk, dv (token-major views like the inputs)."""
+             scale: Optional[float] = None, p_drop: float = 0.0, seed: int = 0, delta=None,
+             dbias: Optional[torch.Tensor] = None):
+    """Writes dq, dk, dv (token-major views like the inputs).  ``dbias`` (f32
+    [(H + 2 Hkv) D]): also accumulate the QKV bias gradient (column sums of dq | dk | dv)."""
     scale = 1.0 / math.sqrt(D) if scale is None else scale
     if _gpu(q):
         if delta is None:
             delta = torch.empty(B * H * Sq, device=q.device, dtype=torch.float32)
         _ext().attn_bwd(q, k, v, o, do, lse, delta, dq, dk, dv, B, Sq, Sk, H, Hkv, D, bool(causal),
-                        float(scale), float(p_drop), int(seed))
+                        float(scale), float(p_drop), int(seed), dbias)
         return dq, dk, dv
     rep = H // Hkv
     Q, K, V = _heads(q, B, Sq, H, D), _heads(k, B, Sk, Hkv, D), _heads(v, B, Sk, Hkv, D)
@@ -543,6 +545,10 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B: int, Sq: int, Sk: int, H: int, 
     dq[:, : H * D].copy_(dQ.permute(0, 2, 1, 3).reshape(B * Sq, H * D).to(dq.dtype))
     dk[:, : Hkv * D].copy_(dK.permute(0, 2, 1, 3).reshape(B * Sk, Hkv * D).to(dk.dtype))
     dv[:, : Hkv * D].copy_(dV.permute(0, 2, 1, 3).reshape(B * Sk, Hkv * D).to(dv.dtype))
+    if dbias is not None:
+        dbias[: H * D] += dq[:, : H * D].float().sum(0)
+        dbias[H * D:(H + Hkv) * D] += dk[:, : Hkv * D].float().sum(0)
+        dbias[(H + Hkv) * D:] += dv[:, : Hkv * D].float().sum(0)
     return dq, dk, dv
 
 

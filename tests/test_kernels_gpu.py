@@ -188,11 +188,15 @@ def test_attention_fwd_bwd(B, S, H, Hkv, D, causal):
         ops.attn_fwd(qq, kk, vv, o, lse, B, S, S, H, Hkv, D, causal)
         dqkv = torch.zeros_like(Q)
         dq, dk, dv = dqkv[:, : H * D], dqkv[:, H * D:(H + Hkv) * D], dqkv[:, (H + Hkv) * D:]
-        ops.attn_bwd(qq, kk, vv, o, do.to(dev), lse, dq, dk, dv, B, S, S, H, Hkv, D, causal)
-        res[dev] = (o, lse, dqkv)
+        dbias = torch.full(((H + 2 * Hkv) * D,), 0.25, device=dev)   # fused QKV bias grad (accumulates)
+        ops.attn_bwd(qq, kk, vv, o, do.to(dev), lse, dq, dk, dv, B, S, S, H, Hkv, D, causal, dbias=dbias)
+        res[dev] = (o, lse, dqkv, dbias)
     close(res[DEV][0], res["cpu"][0], atol=2e-2, rtol=2e-2)
     close(res[DEV][1], res["cpu"][1], atol=2e-2, rtol=1e-3)
     close(res[DEV][2], res["cpu"][2], atol=5e-2, rtol=5e-2)
+    # the kernels' column sums agree with the sums of the gradients they wrote
+    close(res[DEV][3], res[DEV][2].float().sum(0).cpu() + 0.25, atol=0.05 * T ** 0.5, rtol=2e-2)
+    close(res[DEV][3], res["cpu"][3], atol=0.1 * T ** 0.5, rtol=5e-2)
 
 
 def test_attention_dropout_consistency():
