@@ -171,6 +171,8 @@ class MBContext:
 # 740K vs 754K tok/s) than the separate colsum pass -- the cross-lane reductions and the
 # contended per-column atomics in the attention epilogue cost more than re-reading dQKV
 _FUSE_QKV_BIAS = os.environ.get("MIPIPE_FUSE_QKV_BIAS", "0") == "1"
+# MIPIPE_FUSE_FC1_BIAS=0: the fc1 bias gradient in a separate pass instead of the dX GEMM's epilogue
+_FUSE_FC1_BIAS = os.environ.get("MIPIPE_FUSE_FC1_BIAS", "1") != "0"
 
 
 def _seed(base: int, *parts: int) -> int:
@@ -329,9 +331,12 @@ class Block:
                 gact, a, h2 = st["g"], st["a"], st["h2"]
                 # the fc1 bias gradient (column sums of da) is accumulated by the dX GEMM's
                 # epilogue instead of a second pass over da
+                fuse_b1 = cfg.bias and _FUSE_FC1_BIAS
                 da = ops.linear_dx(dy, self.w("ffn.w2.weight"), act_input=a, act=cfg.activation,
-                                   wt=self.wt("ffn.w2.weight"), colsum=self.g("ffn.w1.bias") if cfg.bias else None)
+                                   wt=self.wt("ffn.w2.weight"), colsum=self.g("ffn.w1.bias") if fuse_b1 else None)
                 wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
+                if cfg.bias and not fuse_b1:
+                    wjobs.append(lambda da=da: ops.colsum(da, self.g("ffn.w1.bias")))
                 wjobs.append(lambda da=da, h2=h2: ops.linear_dw(da, h2, self.g("ffn.w1.weight")))
                 dh2 = ops.linear_dx(da, self.w("ffn.w1.weight"), wt=self.wt("ffn.w1.weight"))
             fuse_cs = cfg.bias and kind == "layernorm"
