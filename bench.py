@@ -155,6 +155,7 @@ def main():
                    "parallelism": f"pp{pp}" + (f"_dp{dp}" if dp > 1 else ""),
                    "layer_split": trainer.layer_ranges, "optimizer": "AdamW(fused, clip 1.0)",
                    "hip_graphs": bool(a.graphs),
+                   "native_runner": trainer.runtime.native_runner is not None,
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
                    else "last stage",
                    "head_lag": getattr(trainer, "head_lag", None),

@@ -318,9 +318,13 @@ void set_dropout_step(int64_t step) {
 namespace mipipe_comm {
 void register_rccl(pybind11::module& m);
 }
+namespace mipipe_runtime {
+void register_runner(pybind11::module& m);
+}
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mipipe_comm::register_rccl(m);
+  mipipe_runtime::register_runner(m);
   m.doc() = "mipipe gfx950 HIP kernels";
   m.def("norm_fwd", &norm_fwd);
   m.def("norm_bwd", &norm_bwd);

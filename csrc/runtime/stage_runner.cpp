@@ -1,0 +1,184 @@
+// Native stage runner: replays one rank's pipeline step from C++ (SURVEY §7.1
+// runtime/stage_runner; the executor role of torch's _PipelineScheduleRuntime,
+// schedules.py:2037-2284, which the reference drives from Python).
+//
+// Once every compute action of the rank's lowered program has been captured as a HIP
+// graph (parallel/graphs.py) and every buffer the program touches is persistent (static
+// receive buffers, graph-pool outputs), a step is a fixed instruction tape:
+//
+//   GRAPH  g         hipGraphLaunch(g) on the compute stream
+//   COPY   d, s, n   hipMemcpyAsync device -> device (a static graph input refreshed)
+//   POST   e, ops    one grouped ncclSend/ncclRecv on the RCCL engine's comm stream,
+//                    ordered after the compute stream (RcclP2P::post_raw); fills a slot
+//   WAIT   slot      the compute stream waits for that group's completion event
+//   CALL   fn        a Python callable (anything not expressible above: gloo transfers,
+//                    DP all-reduce through torch.distributed) -- the GIL is taken only here
+//
+// parallel/native_runner.py records the tape from one instrumented Python step and
+// `run()` replays it with the GIL released: no per-action Python, no allocator calls, no
+// host synchronisation -- the host issues the whole step in tens of microseconds and the
+// GPU streams run ahead of it.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime.h>
+
+#include <vector>
+
+#include "../comm/rccl_p2p.h"
+
+namespace py = pybind11;
+
+namespace mipipe_runtime {
+
+using mipipe_comm::RcclP2P;
+
+#define MP_HIPCHK(x)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    TORCH_CHECK(e_ == hipSuccess, "stage runner: ", hipGetErrorString(e_), " at ", #x);      \
+  } while (0)
+
+class StageRunner {
+ public:
+  enum Kind { GRAPH = 0, COPY = 1, POST = 2, WAIT = 3, CALL = 4 };
+
+  explicit StageRunner(int device) : device_(device) {}
+
+  void add_graph(int64_t graph_exec) {
+    TORCH_CHECK(graph_exec != 0, "stage runner: null graph exec");
+    Instr i;
+    i.kind = GRAPH;
+    i.a = graph_exec;
+    tape_.push_back(std::move(i));
+  }
+
+  void add_copy(int64_t dst, int64_t src, int64_t nbytes) {
+    Instr i;
+    i.kind = COPY;
+    i.a = dst;
+    i.b = src;
+    i.c = nbytes;
+    tape_.push_back(std::move(i));
+  }
+
+  // sends / recvs: (device pointer, element count, dtype code, peer); dtype codes follow
+  // torch (bf16 15, f32 6, f16 5, i64 4, i32 3, u8 0, f64 7).  Returns the slot a WAIT names.
+  int64_t add_post(py::object engine, const std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t>>& sends,
+                   const std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t>>& recvs) {
+    Instr i;
+    i.kind = POST;
+    i.engine = engine.cast<RcclP2P*>();
+    i.keep = engine;
+    for (const auto& [p, n, t, peer] : sends) i.sends.push_back({reinterpret_cast<void*>(p), (size_t)n, nccl(t), (int)peer});
+    for (const auto& [p, n, t, peer] : recvs) i.recvs.push_back({reinterpret_cast<void*>(p), (size_t)n, nccl(t), (int)peer});
+    i.slot = nslots_++;
+    tape_.push_back(std::move(i));
+    return tape_.back().slot;
+  }
+
+  void add_wait(int64_t slot) {
+    TORCH_CHECK(slot >= 0 && slot < nslots_, "stage runner: bad slot ", slot);
+    Instr i;
+    i.kind = WAIT;
+    i.slot = slot;
+    tape_.push_back(std::move(i));
+  }
+
+  void add_call(py::function fn) {
+    Instr i;
+    i.kind = CALL;
+    i.fn = std::move(fn);
+    tape_.push_back(std::move(i));
+  }
+
+  // one step on the current HIP stream of `device`
+  void run() {
+    hipStream_t st = c10::hip::getCurrentHIPStream(device_).stream();
+    std::vector<int64_t> handles(nslots_, -1);
+    std::vector<RcclP2P*> engines(nslots_, nullptr);
+    py::gil_scoped_release nogil;
+    for (const Instr& i : tape_) {
+      switch (i.kind) {
+        case GRAPH:
+          MP_HIPCHK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(i.a), st));
+          break;
+        case COPY:
+          MP_HIPCHK(hipMemcpyAsync(reinterpret_cast<void*>(i.a), reinterpret_cast<const void*>(i.b), (size_t)i.c,
+                                   hipMemcpyDeviceToDevice, st));
+          break;
+        case POST:
+          handles[i.slot] = i.engine->post_raw(i.sends, i.recvs, st);
+          engines[i.slot] = i.engine;
+          break;
+        case WAIT:
+          TORCH_CHECK(handles[i.slot] >= 0, "stage runner: WAIT before its POST (slot ", i.slot, ")");
+          engines[i.slot]->wait_raw(handles[i.slot], st);
+          handles[i.slot] = -2;  // consumed
+          break;
+        case CALL: {
+          py::gil_scoped_acquire gil;
+          i.fn();
+          break;
+        }
+      }
+    }
+    // groups whose completion nobody consumed (sends): order them before the next step
+    for (int64_t s = 0; s < nslots_; ++s)
+      if (handles[s] >= 0) engines[s]->wait_raw(handles[s], st);
+    ++runs_;
+  }
+
+  int64_t size() const { return (int64_t)tape_.size(); }
+  int64_t runs() const { return runs_; }
+  std::vector<int64_t> kinds() const {
+    std::vector<int64_t> k;
+    for (const auto& i : tape_) k.push_back(i.kind);
+    return k;
+  }
+
+ private:
+  struct Instr {
+    int kind = GRAPH;
+    int64_t a = 0, b = 0, c = 0;
+    int64_t slot = -1;
+    RcclP2P* engine = nullptr;
+    py::object keep;  // keeps the engine alive
+    std::vector<RcclP2P::RawOp> sends, recvs;
+    py::function fn;
+  };
+
+  static ncclDataType_t nccl(int64_t code) {
+    switch (code) {
+      case 15: return ncclBfloat16;
+      case 6: return ncclFloat32;
+      case 5: return ncclFloat16;
+      case 4: return ncclInt64;
+      case 3: return ncclInt32;
+      case 0: return ncclUint8;
+      case 7: return ncclFloat64;
+      default: TORCH_CHECK(false, "stage runner: unsupported dtype code ", code);
+    }
+    return ncclFloat32;
+  }
+
+  int device_;
+  std::vector<Instr> tape_;
+  int64_t nslots_ = 0;
+  int64_t runs_ = 0;
+};
+
+void register_runner(py::module& m) {
+  py::class_<StageRunner>(m, "StageRunner")
+      .def(py::init<int>(), py::arg("device"))
+      .def("add_graph", &StageRunner::add_graph)
+      .def("add_copy", &StageRunner::add_copy)
+      .def("add_post", &StageRunner::add_post)
+      .def("add_wait", &StageRunner::add_wait)
+      .def("add_call", &StageRunner::add_call)
+      .def("run", &StageRunner::run)
+      .def("kinds", &StageRunner::kinds)
+      .def_property_readonly("size", &StageRunner::size)
+      .def_property_readonly("runs", &StageRunner::runs);
+}
+
+}  // namespace mipipe_runtime

@@ -129,8 +129,8 @@ class NativeStage(StageBase):
         if self.is_last and not self.split_head:
             if not last_loss:
                 return (out,), None
-            loss = out.clone()
-            return (loss.detach(),), loss
+            # the runtime copies it into a persistent loss slot (runtime._loss_slot)
+            return (out.detach(),), out
         return (out,), None
 
     def _backward_graphed(self, op, mb, grad_outputs, weight_grads):

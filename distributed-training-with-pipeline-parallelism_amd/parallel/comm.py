@@ -51,13 +51,17 @@ class _StagedSend:
 
 class _NativeWork:
     """Handle of one grouped transfer on the native RCCL engine; ``wait`` makes the
-    current stream wait (no host block), like torch's NCCL Work."""
+    current stream wait (no host block), like torch's NCCL Work.  Under a recording step
+    (:mod:`.native_runner`) the wait is also put on the tape."""
 
-    def __init__(self, engine, handle: int):
-        self.engine, self.handle = engine, handle
+    def __init__(self, engine, handle: int, rec=None, slot: int = -1):
+        self.engine, self.handle, self.rec, self.slot = engine, handle, rec, slot
 
     def wait(self):
         self.engine.wait(self.handle)
+        if self.rec is not None:
+            self.rec.native_wait(self.slot)
+            self.rec = None     # one WAIT per handle, however often it is waited on
         return True
 
 
@@ -113,12 +117,27 @@ class P2P:
 
     def post(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
         """Post one group; returns (send_works, recv_works) aligned with the inputs."""
+        from . import native_runner
+        rec = native_runner.active()
         if self.engine is not None:
             if not sends and not recvs:
                 return [], []
             h = self.engine.post([(t, p) for t, p in sends], [(t, p) for t, p in recvs])
-            w = _NativeWork(self.engine, h)
+            slot = rec.native_post(self.engine, sends, recvs) if rec is not None else -1
+            w = _NativeWork(self.engine, h, rec, slot)
             return [w] * len(sends), [w] * len(recvs)
+        if rec is not None:
+            # transfers through torch.distributed replay as CALLs on the same tensors
+            ns = len(sends)
+            works = native_runner.record_issue(rec, lambda: self._post_torch(sends, recvs))
+            return works[:ns], works[ns:]
+        return self._post_torch_split(sends, recvs)
+
+    def _post_torch_split(self, sends, recvs):
+        works = self._post_torch(sends, recvs)
+        return works[: len(sends)], works[len(sends):]
+
+    def _post_torch(self, sends, recvs) -> list:
         ops = []
         staged = []
         for t, peer in sends:
@@ -134,13 +153,13 @@ class P2P:
                 t = h
             ops.append(dist.P2POp(dist.irecv, t, self.global_rank(peer), self.group))
         if not ops:
-            return [], []
+            return []
         works = dist.batch_isend_irecv(ops)
         sw, rw = works[: len(sends)], works[len(sends):]
         if self.host_staged:
             sw = [_StagedSend(w, h) for w, h in zip(sw, staged)]
             rw = [_StagedRecv(w, h, d) for w, (h, d) in zip(rw, host_recv)]
-        return sw, rw
+        return list(sw) + list(rw)
 
     # -------------------------------------------------------------- spec exchange
     def _pack(self, specs: Sequence[Spec]) -> torch.Tensor:

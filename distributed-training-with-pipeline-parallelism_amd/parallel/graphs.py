@@ -55,8 +55,12 @@ class GraphCache:
             keep: Callable[[], Any] = None) -> Any:
         """Replay the graph captured for ``key`` (capturing it on first use).  ``keep``
         returns objects whose tensors must outlive the capture (saved activations)."""
+        from . import native_runner
+        rec = native_runner.active()
         entry = self.graphs.get(key)
         if entry is None:
+            if rec is not None:
+                rec.invalidate(f"graph {key!r} captured during the recording step")
             g = torch.cuda.CUDAGraph()
             torch.cuda.synchronize()
             # thread-local capture: the RCCL watchdog thread may query events meanwhile
@@ -71,8 +75,12 @@ class GraphCache:
             for s, t in zip(static_in, inputs):
                 if s.data_ptr() != t.data_ptr():
                     s.copy_(t)
+                    if rec is not None:
+                        rec.copy(s, t)
             self.replays += 1
         entry[0].replay()
+        if rec is not None:
+            rec.graph(entry[0])
         return entry[2]
 
     def clear(self) -> None:

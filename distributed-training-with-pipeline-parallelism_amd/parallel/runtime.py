@@ -155,6 +155,14 @@ class PipelineRuntime:
         self.deps: Optional[DepTracker] = DepTracker(pp_rank, lvl) if lvl > 0 else None
         # roctx / torch.profiler ranges per action ("PP:<action>", as torch schedules.py:2245)
         self.ranges = os.environ.get("MIPIPE_RANGES", "0") == "1"
+        # native step replay (parallel/native_runner.py, csrc/runtime/stage_runner.cpp): once
+        # every action is a captured HIP graph, one step is recorded and later steps run in C++
+        self.native_enabled = os.environ.get("MIPIPE_NATIVE_RUNNER", "1") != "0"
+        self.native_runner = None
+        self.native_reason = "not recorded yet"
+        self._in_bufs: Dict[int, Tuple[torch.Tensor, ...]] = {}
+        self._tgt_bufs: Dict[int, torch.Tensor] = {}
+        self._loss_bufs: Dict[tuple, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ init
     def _needs_inference(self) -> bool:
@@ -231,12 +239,94 @@ class PipelineRuntime:
             self._recv_bufs[key] = buf
         return buf
 
+    # ------------------------------------------------------------------ native replay
+    def _native_possible(self, return_outputs: bool) -> bool:
+        if not self.native_enabled or return_outputs or self.device.type != "cuda":
+            return False
+        if self.deps is not None or self.profile or self.ranges:
+            return False
+        if any(getattr(st, "graphs", None) is None for st in self.stages.values()):
+            return False
+        if self.head is not None and self.head.graphs is None:
+            return False
+        # step 1 eager, step 2 captures, step 3 (and later) replays every action
+        return self._steps >= 2 and all(getattr(st, "step_id", 0) >= 2 for st in self.stages.values())
+
+    def _loss_slot(self, key: tuple, like: torch.Tensor) -> torch.Tensor:
+        buf = self._loss_bufs.get(key)
+        if buf is None or buf.shape != like.shape or buf.dtype != like.dtype:
+            buf = torch.empty_like(like)
+            self._loss_bufs[key] = buf
+        return buf
+
+    def _persist_inputs(self, inputs, targets):
+        """Copy the step's user inputs / targets into persistent per-microbatch buffers (so a
+        recorded tape never points at a caller's tensor).  Runs in Python every step."""
+        if inputs is not None:
+            out = []
+            for mb, args in enumerate(inputs):
+                bufs = self._in_bufs.get(mb)
+                if bufs is None or any(b.shape != a.shape for b, a in zip(bufs, args)):
+                    bufs = tuple(torch.empty_like(a) for a in args)
+                    self._in_bufs[mb] = bufs
+                for b, a in zip(bufs, args):
+                    b.copy_(a)
+                out.append(bufs)
+            inputs = out
+        if targets is not None:
+            out = []
+            for mb, t in enumerate(targets):
+                b = self._tgt_bufs.get(mb)
+                if b is None or b.shape != t.shape:
+                    b = torch.empty_like(t)
+                    self._tgt_bufs[mb] = b
+                b.copy_(t)
+                out.append(b)
+            targets = out
+        return inputs, targets
+
+    def _step_native(self, inputs, targets, losses):
+        for st in self.stages.values():
+            st.clear_runtime_states()
+        self._steps += 1
+        self._persist_inputs(inputs, targets)
+        self.native_runner.run()
+        for st in self.stages.values():
+            st.post_step()
+        mb_losses = {k[1]: t for k, t in self._loss_bufs.items() if k[0] == "L"}
+        self.head_losses = {k[1]: t for k, t in self._loss_bufs.items() if k[0] == "H"}
+        if losses is not None and mb_losses:
+            losses.extend(mb_losses[i] for i in sorted(mb_losses))
+        self._last_losses = mb_losses
+        return None
+
     # ------------------------------------------------------------------ step
     def step(self, inputs: Optional[Sequence[Tuple[torch.Tensor, ...]]] = None,
              targets: Optional[Sequence[torch.Tensor]] = None, losses: Optional[list] = None,
              return_outputs: bool = True) -> Optional[List[Tuple[torch.Tensor, ...]]]:
         if not self._initialized:
             self._initialize(inputs[0] if inputs is not None else None)
+        possible = self._native_possible(return_outputs)
+        if possible and self.native_runner is not None:
+            return self._step_native(inputs, targets, losses)
+        rec = None
+        if possible:
+            from .native_runner import TapeRecorder
+            inputs, targets = self._persist_inputs(inputs, targets)
+            rec = TapeRecorder(self.device)
+        with (rec if rec is not None else contextlib.nullcontext()):
+            out = self._step_python(inputs, targets, losses, return_outputs, rec)
+        if rec is not None:
+            if rec.valid:
+                self.native_runner = rec.runner
+                self.native_reason = f"recorded {rec.runner.size} instructions"
+            else:
+                self.native_enabled = False
+                self.native_reason = "disabled: " + rec.reason
+                log.warning("native stage runner not used: %s", rec.reason)
+        return out
+
+    def _step_python(self, inputs, targets, losses, return_outputs, rec):
         for st in self.stages.values():
             st.clear_runtime_states()
         recv_works: Dict[tuple, List] = {}
@@ -302,6 +392,14 @@ class PipelineRuntime:
                 a = e
                 st = self.stages.get(a.stage)
                 if a.op == Op.REDUCE_GRAD:
+                    if rec is not None:
+                        from .native_runner import record_issue
+
+                        def _rg(st=st):
+                            w_ = st.reduce_grad(self.m, scaled_in_loss=self.scale_grads)
+                            return [w_] if w_ is not None else []
+                        reduce_works.extend(record_issue(rec, _rg))
+                        continue
                     w = st.reduce_grad(self.m, scaled_in_loss=self.scale_grads)
                     if w is not None:
                         reduce_works.append(w)
@@ -359,6 +457,10 @@ class PipelineRuntime:
                 if return_outputs:
                     outputs[a.mb] = out
                 if loss is not None:
+                    if getattr(st, "_graphed", lambda: False)():
+                        # graph output -> persistent loss slot (a recorded COPY on the tape)
+                        from .native_runner import copy_into
+                        loss = copy_into(self._loss_slot(("L", a.mb), loss), loss)
                     mb_losses[a.mb] = loss
             else:
                 produce(("F", a.stage + 1, a.mb), out, a, self.s2r[a.stage + 1] == self.rank)
@@ -378,7 +480,8 @@ class PipelineRuntime:
                     d = self._dh_buf(mb)[rows] if local_last else torch.empty_like(ins[0])
                     return d, head.runner(ins[0], ins[1], d, scale)
                 dh, loss = head.graphs.run(("H", a.mb), (h_in, tgt), fn)
-                self.head_losses[a.mb] = loss.clone()
+                from .native_runner import copy_into
+                self.head_losses[a.mb] = copy_into(self._loss_slot(("H", a.mb), loss), loss)
             else:
                 dh = self._dh_buf(a.mb)[rows] if local_last else torch.empty_like(h_in)
                 self.head_losses[a.mb] = head.runner(h_in, tgt, dh, scale)

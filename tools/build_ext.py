@@ -64,11 +64,13 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
         if force or _newer([k] + headers, o):
             jobs_list.append(base + ["-c", k, "-o", o])
     incs, tlib, abi = _torch_paths()
-    # translation units that include torch: the pybind module and the native RCCL engine
-    for bsrc in (os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "comm", "rccl_p2p.cpp")):
+    # translation units that include torch: the pybind module, the native RCCL engine, the stage runner
+    host_hdrs = glob.glob(os.path.join(CSRC, "comm", "*.h"))
+    for bsrc in (os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "comm", "rccl_p2p.cpp"),
+                 os.path.join(CSRC, "runtime", "stage_runner.cpp")):
         bobj = os.path.join(OBJ, os.path.basename(bsrc) + ".o")
         objs.append(bobj)
-        if force or _newer([bsrc], bobj):
+        if force or _newer([bsrc] + host_hdrs, bobj):
             cmd = base + [f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_API_INCLUDE_EXTENSION_H",
                           "-DTORCH_EXTENSION_NAME=_C", "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1",
                           "-isystem", "/opt/rocm/include"]

@@ -42,7 +42,9 @@ def main():
             dist.all_reduce(v)
         losses.append(float(v.item()))
     if rank == 0:
-        print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses}), flush=True)
+        print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses,
+                          "native_runner": tr.runtime.native_runner is not None,
+                          "native_reason": tr.runtime.native_reason}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
