@@ -354,7 +354,11 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int TILE = 64 * DP * 2;
   constexpr int BUFB = 2 * TILE + 512;               // Q, dO, lse[64], delta[64]
-  constexpr int NBUF = DP <= 128 ? 3 : 2;
+  // ring depth: MIPIPE-tunable at build time (MP_DKDV_NBUF); 4 buffers keep 3 tiles in flight
+#ifndef MP_DKDV_NBUF
+#define MP_DKDV_NBUF 4
+#endif
+  constexpr int NBUF = DP <= 128 ? MP_DKDV_NBUF : 2;
   constexpr int LOOK = NBUF - 1;                     // tiles issued ahead
   using GT = GTile<DP>;
 
@@ -416,8 +420,11 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     const int hq = hk * grp + it / ntq;
     const int q0 = q_begin + (it % ntq) * 64;
     const int bhq = b * H + hq;
-    // tile `it` landed (LOOK-1 younger tiles may stay in flight), then publish to all waves
-    if (LOOK == 2 && it + 1 < total) {
+    // tile `it` landed (up to LOOK-1 younger tiles may stay in flight), then publish to all
+    // waves; wave 0 issues 2 extra DMAs per tile (the row stats)
+    if (LOOK >= 3 && it + 2 < total) {
+      if (w == 0) attn_wait_vmcnt<2 * (PER_TILE + 2)>(); else attn_wait_vmcnt<2 * PER_TILE>();
+    } else if (LOOK >= 2 && it + 1 < total) {
       if (w == 0) attn_wait_vmcnt<PER_TILE + 2>(); else attn_wait_vmcnt<PER_TILE>();
     } else {
       attn_wait_vmcnt<0>();
@@ -701,7 +708,7 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
                                  dqs, scale, p, seed, csq);
   }
   {
-    const size_t lds = (DP <= 128 ? 3 : 2) * (2 * 64 * DP * 2 + 512);
+    const size_t lds = (DP <= 128 ? MP_DKDV_NBUF : 2) * (2 * 64 * DP * 2 + 512);
     auto kern = attn_bwd_dkdv_kernel<DP, CAUSAL, DROP>;
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     dim3 grid((Sk + 127) / 128, B * Hkv);
