@@ -587,23 +587,38 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
   int n_end = Sk;
   if (CAUSAL) n_end = min(Sk, m0 + 128 + shift);
   const int ntiles = (n_end + 63) / 64;
-  Stage64<DP> kst, vst;
-  kst.load(Kb, ks, 0, Sk, D);
-  vst.load(Vb, vs, 0, Sk, D);
-  kst.store(kbuf(0));
-  vst.store(vbuf(0));
+  // K / V tiles stream through an NBUF-deep LDS ring by LDS-DMA (the dK/dV kernel's
+  // scheme): LOOK tiles in flight, counted vmcnt, one raw barrier per tile
+  constexpr int NBUF = DP <= 128 ? 4 : 2;
+  constexpr int LOOK = NBUF - 1;
+  constexpr int BUFB = 2 * TILE;
+  using GT = GTile<DP>;
+  constexpr int PER_TILE = 2 * GT::PPW;
+  GT gt;
+  gt.init();
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+  auto issue = [&](int t) {
+    char* buf = smem + (t % NBUF) * BUFB;
+    gt.issue(Kb, ks, t * 64, Sk, D, buf, wv);
+    gt.issue(Vb, vs, t * 64, Sk, D, buf + TILE, wv);
+  };
+#pragma unroll
+  for (int i = 0; i < LOOK; ++i)
+    if (i < ntiles) issue(i);
   const int wave_last_q = m0 + 32 * w + 31 + shift;
   for (int t = 0; t < ntiles; ++t) {
-    const int cur = t & 1;
     const int n0 = t * 64;
-    if (t + 1 < ntiles) {
-      kst.load(Kb, ks, n0 + 64, Sk, D);
-      vst.load(Vb, vs, n0 + 64, Sk, D);
-    }
-    __syncthreads();
+    if (LOOK >= 3 && t + 2 < ntiles) attn_wait_vmcnt<2 * PER_TILE>();
+    else if (LOOK >= 2 && t + 1 < ntiles) attn_wait_vmcnt<PER_TILE>();
+    else attn_wait_vmcnt<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // every wave is done with tile t-1: its buffer takes tile t+LOOK
+    if (t + LOOK < ntiles) issue(t + LOOK);
     if (!(CAUSAL && n0 > wave_last_q)) {
-      const char* kb = kbuf(cur);
-      const char* vb = vbuf(cur);
+      const char* kb = smem + (t % NBUF) * BUFB;
+      const char* vb = kb + TILE;
       f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
 #pragma unroll
       for (int s = 0; s < DP / 16; ++s) {
@@ -647,10 +662,6 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
         a = cat44(lds_tr4<DP>(kb, 48 + 4 * hl, c0), lds_tr4<DP>(kb, 56 + 4 * hl, c0));
         dq[d] = mfma32(a, d11, dq[d]);
       }
-    }
-    if (t + 1 < ntiles) {
-      kst.store(kbuf(cur ^ 1));
-      vst.store(vbuf(cur ^ 1));
     }
   }
   if (CSQ != nullptr) {
@@ -699,7 +710,7 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
                       int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs, int64_t dks, int64_t dvs,
                       float scale, float p, uint64_t seed, float* csq, float* csk, float* csv, hipStream_t st) {
   {
-    const size_t lds = 4 * 64 * DP * 2;
+    const size_t lds = (DP <= 128 ? 4 : 2) * 2 * 64 * DP * 2;
     auto kern = attn_bwd_dq_kernel<DP, CAUSAL, DROP>;
     if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     dim3 grid((Sq + 127) / 128, B * H);
