@@ -44,7 +44,8 @@ def parse():
     # (not "--v": torch.distributed.run's argparse would take it for an abbreviation of
     # its --virtual-local-rank even after the script name)
     ap.add_argument("--vstages", type=int, default=None, help="virtual stages per rank (interleaved)")
-    ap.add_argument("--recompute", action="store_true")
+    ap.add_argument("--recompute", nargs="?", const="1", default="0", choices=["0", "1", "auto"],
+                    help="activation recompute: 1 (on), 0 (off), auto (HBM plan: only if the stash does not fit)")
     ap.add_argument("--graphs", type=int, default=None,
                     help="replay per-microbatch stage compute as HIP graphs (default: on for 1 GPU)")
     ap.add_argument("--no-split-head", action="store_true",
@@ -83,7 +84,7 @@ def main():
     if a.graphs is None:
         a.graphs = 1 if world == 1 else 0
     trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m,
-                              mbs=a.mbs, seq_len=a.seq, v=a.vstages, device=device, recompute=a.recompute, seed=0,
+                              mbs=a.mbs, seq_len=a.seq, v=a.vstages, device=device, recompute=a.recompute if a.recompute == "auto" else a.recompute == "1", seed=0,
                               split_head=False if a.no_split_head else None, graphs=bool(a.graphs))
     gb = dp * m * a.mbs
     g = torch.Generator(device=device).manual_seed(1234 + trainer.mesh.dp_rank)
@@ -155,6 +156,7 @@ def main():
                    "parallelism": f"pp{pp}" + (f"_dp{dp}" if dp > 1 else ""),
                    "layer_split": trainer.layer_ranges, "optimizer": "AdamW(fused, clip 1.0)",
                    "hip_graphs": bool(a.graphs),
+                   "recompute": trainer.recompute,
                    "native_runner": trainer.runtime.native_runner is not None,
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
                    else "last stage",

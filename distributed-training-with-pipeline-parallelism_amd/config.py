@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import json
 from dataclasses import asdict, dataclass, field, fields, is_dataclass
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Union
 
 
 @dataclass
@@ -44,7 +44,7 @@ class TrainSection:
     lr_schedule: str = "cosine"         # cosine | constant
     weight_decay: float = 0.1
     max_grad_norm: float = 1.0
-    recompute: bool = False
+    recompute: Union[bool, str] = False   # True, False or "auto" (engine.plan_recompute: HBM plan)
     seed: int = 0
     data: str = "synthetic"             # synthetic | path to a uint16/int32 token file (memory-mapped)
     log_every: int = 10

@@ -136,6 +136,22 @@ class NativeConfig:
             p += self.vocab_size * d + (self.vocab_size if self.bias and self.cross_attn else 0)
         return p
 
+    def stash_bytes_per_layer(self, tokens: int, recompute: bool = False) -> int:
+        """bf16 activations one layer keeps for its backward, per microbatch of ``tokens``
+        (models/native.py Block.forward stash): layer input, norm outputs, QKV, attention
+        output, FFN pre-activation / gate tensors.  With full recompute only the input."""
+        d, f = self.d_model, self.d_ff
+        if recompute:
+            return 2 * tokens * d
+        if self.activation == "swiglu":
+            ffn = 3 * f                    # gate|up (2f) + activated (f)
+        else:
+            ffn = 2 * f                    # pre-activation + activated
+        per_tok = 5 * d + self.qkv_dim + ffn
+        if self.cross_attn:                # second attention block: q/kv projections, output, norm
+            per_tok += 3 * d + 2 * d
+        return 2 * tokens * per_tok
+
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs per token (fwd+bwd = 3x fwd), incl. attention and the LM head."""
         d = self.d_model

@@ -99,3 +99,33 @@ def test_pp2_zbv_matches_pp1(split_head):
         for k, v in r["sd"].items():
             torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref["sd"][k]), atol=1e-4, rtol=1e-4,
                                        msg=lambda m: f"{k}: {m}")
+
+
+def test_recompute_auto_plan():
+    """recompute="auto": the HBM plan keeps the whole stash when it fits (Llama-3 8B at
+    seq 8192 on one 288 GB MI355X, PP=1: ~203 GB planned, 186 GB measured) and recomputes
+    when it does not (a hypothetical 64 GB device)."""
+    import torch
+    from mipipe.engine import max_inflight_microbatches, plan_recompute
+    from mipipe.models.config import NativeConfig
+    from mipipe.models.native import balanced_layer_ranges
+    from mipipe.parallel.schedules import generate
+    import mipipe.engine as E
+
+    cfg = NativeConfig.llama3("8b")
+    lr = balanced_layer_ranges(cfg, 1, 8192, head_on_last=True)
+    order = generate("1F1B", 1, 2, 1, "loop")[0]
+    assert max_inflight_microbatches(order, {0}) == 1
+    orig = E.torch.cuda.get_device_properties
+    try:
+        for gb, want in ((288, False), (64, True)):
+            E.torch.cuda.get_device_properties = lambda d, gb=gb: type("P", (), {"total_memory": gb * 2 ** 30})()
+            plan = plan_recompute(cfg, lr, [0], order, 1, 8192, torch.device("cuda", 0), head_tokens=8192)
+            assert plan["recompute"] is want, plan
+        assert 180e9 < plan["bytes_no_recompute"] < 230e9
+    finally:
+        E.torch.cuda.get_device_properties = orig
+    # 1F1B PP=4: rank 0 holds 4 microbatches in flight, the last rank 1; GPipe holds all m
+    o4 = generate("1F1B", 4, 8, 1, "loop")
+    assert max_inflight_microbatches(o4[0], {0}) == 4 and max_inflight_microbatches(o4[3], {3}) == 1
+    assert max_inflight_microbatches(generate("GPipe", 4, 8, 1, "loop")[0], {0}) == 8
