@@ -45,6 +45,7 @@ class TrainSection:
     weight_decay: float = 0.1
     max_grad_norm: float = 1.0
     recompute: Union[bool, str] = False   # True, False or "auto" (engine.plan_recompute: HBM plan)
+    graphs: Optional[bool] = None       # HIP-graph replay + native stage runner (None: on for GPU)
     seed: int = 0
     data: str = "synthetic"             # synthetic | path to a uint16/int32 token file (memory-mapped)
     log_every: int = 10

@@ -87,7 +87,8 @@ def main():
                               max_grad_norm=t.max_grad_norm, recompute=t.recompute, seed=t.seed, style=p.style,
                               layer_ranges=[tuple(r) for r in p.layer_ranges] if p.layer_ranges else None,
                               split_head=p.split_head,
-                              dtype=torch.bfloat16 if device.type == "cuda" else torch.float32)
+                              dtype=torch.bfloat16 if device.type == "cuda" else torch.float32,
+                              graphs=(device.type == "cuda") if t.graphs is None else bool(t.graphs))
     start = 0
     if t.resume:
         man = trainer.load_checkpoint(t.resume)
@@ -95,6 +96,11 @@ def main():
         if rank == 0:
             print(f"resumed from {t.resume} at step {start} (saved at pp={man['pp']})", flush=True)
     data = TokenData(t.data, ncfg.vocab_size, m * t.micro_batch, t.seq_len, device, trainer.mesh.dp_rank, t.seed)
+    if start < t.steps:
+        # HIP graphs: two setup passes on the first batch capture every per-microbatch
+        # action (gradients discarded, weights untouched); later steps replay them, from
+        # the native stage runner once one step has been recorded
+        trainer.capture_graphs(*data.batch(start))
     log = MetricsLogger(t.metrics_file, rank, device)
     grid = lambda: format_compute_grid({r: [e for e in es if isinstance(e, Action)]
                                         for r, es in trainer.runtime.program_all.items()})
