@@ -39,6 +39,8 @@ int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, cons
                 int64_t dk_stride, int64_t dv_stride, int causal, float scale, float p_drop, uint64_t seed,
                 float* csq, float* csk, float* csv, hipStream_t st);
 int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st);
+int mp_transpose_batched(const void* src, void* dst, const int64_t* desc, const int* tile0, int n, int total_tiles,
+                         hipStream_t st);
 int mp_set_drop_step_attn(uint64_t v, hipStream_t st);
 int mp_set_drop_step_elem(uint64_t v, hipStream_t st);
 int mp_set_drop_step_norm(uint64_t v, hipStream_t st);
@@ -304,6 +306,18 @@ void transpose(torch::Tensor in, torch::Tensor out) {
         "transpose");
 }
 
+// every W^T copy of an arena in one launch: desc int64 [n, 4] = (src off, dst off, R, C),
+// tile0 int32 [n] = first 64x64 tile of each matrix
+void transpose_batched(torch::Tensor src, torch::Tensor dst, torch::Tensor desc, torch::Tensor tile0,
+                       int64_t total_tiles) {
+  TORCH_CHECK(desc.scalar_type() == torch::kInt64 && tile0.scalar_type() == torch::kInt32 && desc.is_cuda() &&
+                  tile0.is_cuda() && desc.size(0) == tile0.size(0),
+              "transpose_batched: bad descriptors");
+  check(mp_transpose_batched(src.data_ptr(), dst.data_ptr(), desc.data_ptr<int64_t>(), tile0.data_ptr<int>(),
+                             (int)desc.size(0), (int)total_tiles, cur_stream()),
+        "transpose_batched");
+}
+
 // training-step counter the dropout kernels mix into their seeds (mp_common.h
 // step_seed): stream-ordered, issued before a step's first replay, never captured
 void set_dropout_step(int64_t step) {
@@ -346,4 +360,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2", &gemm2);
   m.def("transpose", &transpose);
   m.def("set_dropout_step", &set_dropout_step);
+  m.def("transpose_batched", &transpose_batched);
 }

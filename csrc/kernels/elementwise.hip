@@ -174,6 +174,55 @@ __global__ void __launch_bounds__(256) transpose_kernel(const bf16_t* __restrict
   }
 }
 
+// All W^T copies of a parameter arena in ONE launch (refreshed after every optimizer step).
+// desc[i] = {src offset, dst offset, R, C} (elements, into the w16 / wt16 arenas); block b
+// transposes 64x64 tile (b - tile0[i]) of matrix i, found by binary search over the tile
+// prefix.  16-byte global loads and stores (C and R are multiples of 8), LDS tile in between.
+__global__ void __launch_bounds__(256) transpose_batched_kernel(const bf16_t* __restrict__ src,
+                                                                bf16_t* __restrict__ dst,
+                                                                const int64_t* __restrict__ desc,
+                                                                const int* __restrict__ tile0, int n) {
+  __shared__ bf16_t tile[64][72];   // 144-byte rows: 16-byte aligned, rows spread over banks
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {  // last i with tile0[i] <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (tile0[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const int64_t so = desc[4 * lo], dof = desc[4 * lo + 1];
+  const int R = (int)desc[4 * lo + 2], C = (int)desc[4 * lo + 3];
+  const int t = b - tile0[lo], tcols = (C + 63) / 64;
+  const int r0 = (t / tcols) * 64, c0 = (t % tcols) * 64;
+  const int tid = threadIdx.x;
+  // load: 64 rows x 8 chunks of 8 columns = 512 chunks, 2 per thread
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + 256 * k, rr = idx >> 3, cc = (idx & 7) * 8;
+    u16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (r0 + rr < R && c0 + cc < C) v = *reinterpret_cast<const u16x8*>(src + so + (int64_t)(r0 + rr) * C + c0 + cc);
+    *reinterpret_cast<u16x8*>(&tile[rr][cc]) = v;
+  }
+  __syncthreads();
+  // store: output row = input column (64 of them), 8 chunks of 8 input rows each
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int idx = tid + 256 * k, oc = idx >> 3, orr = (idx & 7) * 8;   // output row oc, cols orr..orr+7
+    if (c0 + oc < C && r0 + orr < R) {
+      u16x8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = tile[orr + e][oc];
+      *reinterpret_cast<u16x8*>(dst + dof + (int64_t)(c0 + oc) * R + r0 + orr) = v;
+    }
+  }
+}
+
+extern "C" int mp_transpose_batched(const void* src, void* dst, const int64_t* desc, const int* tile0, int n,
+                                    int total_tiles, hipStream_t st) {
+  if (n <= 0 || total_tiles <= 0) return 0;
+  transpose_batched_kernel<<<total_tiles, 256, 0, st>>>((const bf16_t*)src, (bf16_t*)dst, desc, tile0, n);
+  return (int)hipGetLastError();
+}
+
 static int grid_n8(int64_t n) {
   int64_t b = (n / 8 + 255) / 256;
   return (int)(b < 4096 ? (b < 1 ? 1 : b) : 4096);

@@ -107,6 +107,25 @@ class ParamArena:
         self.refresh_transposes()
 
     def refresh_transposes(self) -> None:
+        """W^T copies from the bf16 weights: one batched launch on GPU (a 16-byte-vector
+        tile transpose over a static descriptor table), per-matrix on CPU."""
+        if not self.t_offsets:
+            return
+        if self.w16.is_cuda and all(self.specs[n].shape[0] % 8 == 0 and self.specs[n].shape[1] % 8 == 0
+                                    and self.offsets[n] % 8 == 0 and o % 8 == 0
+                                    for n, o in self.t_offsets.items()):
+            if getattr(self, "_tdesc", None) is None:
+                rows, t0, tiles = [], [], 0
+                for name, o in self.t_offsets.items():
+                    r, c = self.specs[name].shape
+                    rows.append([self.offsets[name], o, r, c])
+                    t0.append(tiles)
+                    tiles += ((r + 63) // 64) * ((c + 63) // 64)
+                self._tdesc = torch.tensor(rows, dtype=torch.int64, device=self.w16.device)
+                self._ttile0 = torch.tensor(t0, dtype=torch.int32, device=self.w16.device)
+                self._ttiles = tiles
+            ops.load_ext().transpose_batched(self.w16, self.wt16, self._tdesc, self._ttile0, self._ttiles)
+            return
         for name in self.t_offsets:
             ops.transpose(self.w(name), self.wt(name))
 

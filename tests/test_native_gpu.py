@@ -99,7 +99,11 @@ def test_hip_graph_replay_matches_eager(recompute):
             assert tr.stages[0].graphs.captures >= 4
         res[graphs] = ([float(tr.train_step(x, y)) for _ in range(3)], tr.stages[0].arena.master.clone())
         if graphs:
-            assert tr.stages[0].graphs.replays >= 6
+            # step 1 after capture replays through Python (and is recorded), later steps
+            # replay from the native stage runner's tape
+            nr = tr.runtime.native_runner
+            assert tr.stages[0].graphs.replays >= 4
+            assert nr is not None and nr.runs >= 2, tr.runtime.native_reason
     # split-K dW uses f32 atomics (summation order varies run to run), so equal up to rounding
     assert res[True][0] == pytest.approx(res[False][0], rel=1e-4)
     # (Adam turns atomics-order noise of near-zero grads into lr-sized steps)
@@ -144,3 +148,19 @@ def test_dropout_graphs_match_eager_and_refresh_masks():
                         return_outputs=False)
         ls.append(float(torch.stack(losses).sum()))
     assert len(set(ls)) == 3, ls
+
+
+@pytest.mark.parametrize("name", ["gpt2", "llama"])
+def test_arena_batched_transpose_refresh(name):
+    """All W^T copies of an arena refreshed in one batched launch equal the transposes."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    model = NativeModel(CFGS[name], 0, 1, "cuda", seed=2)
+    A = model.arena
+    assert A.t_offsets
+    A.w16.copy_(torch.randn(A.w16.numel(), device="cuda").to(A.w16.dtype))
+    A.wt16.zero_()
+    A.refresh_transposes()
+    torch.cuda.synchronize()
+    for n in A.t_offsets:
+        assert torch.equal(A.wt(n), A.w(n).t()), n
