@@ -132,8 +132,14 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
 #define vbuf(i) (smem + (2 + (i)) * TILE)
 
   const int nmb = (Sq + 127) / 128;
-  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;  // heavy blocks first
-  const int bh = blockIdx.y;
+  // causal: longest-first over the WHOLE grid (workgroups are dispatched in linear id
+  // order): every (b, h)'s last query block, then the second to last, ...  Heavy-first
+  // within each (b, h) row only interleaved heavy and light blocks and left a tail of
+  // late heavy blocks -- causal took as long as full attention at S = 1024
+  const int lin = (int)blockIdx.x + (int)gridDim.x * (int)blockIdx.y;
+  const int nbh = (int)gridDim.y;
+  const int mb = CAUSAL ? (nmb - 1 - lin / nbh) : (int)blockIdx.x;
+  const int bh = CAUSAL ? lin % nbh : (int)blockIdx.y;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
   const int m0 = mb * 128;
@@ -362,8 +368,11 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
   constexpr int LOOK = NBUF - 1;                     // tiles issued ahead
   using GT = GTile<DP>;
 
-  const int kb = (int)blockIdx.x;
-  const int bhk = blockIdx.y;
+  // causal: key block 0 sees every query -> longest-first over the whole grid (all (b, h)'s
+  // first key block, then the second, ...), as in the forward
+  const int lin = (int)blockIdx.x + (int)gridDim.x * (int)blockIdx.y;
+  const int kb = CAUSAL ? lin / (int)gridDim.y : (int)blockIdx.x;
+  const int bhk = CAUSAL ? lin % (int)gridDim.y : (int)blockIdx.y;
   const int b = bhk / Hkv, hk = bhk % Hkv;
   const int grp = H / Hkv;
   const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
@@ -546,8 +555,11 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
 #define kbuf(i) (smem + (i) * TILE)
 #define vbuf(i) (smem + (2 + (i)) * TILE)
   const int nmb = (Sq + 127) / 128;
-  const int mb = CAUSAL ? (nmb - 1 - (int)blockIdx.x) : (int)blockIdx.x;
-  const int bh = blockIdx.y;
+  // causal: longest-first over the whole grid (see attn_fwd_kernel)
+  const int lin = (int)blockIdx.x + (int)gridDim.x * (int)blockIdx.y;
+  const int nbh = (int)gridDim.y;
+  const int mb = CAUSAL ? (nmb - 1 - lin / nbh) : (int)blockIdx.x;
+  const int bh = CAUSAL ? lin % nbh : (int)blockIdx.y;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
   const int m0 = mb * 128;
