@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--graphs", type=int, default=0)
     ap.add_argument("--split-head", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--dp", type=int, default=1, help="data-parallel replicas (pp = world / dp)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -26,20 +27,29 @@ def main():
     rank, world, _, device = init_distributed()
     cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=4, n_heads=4, d_ff=1024, max_seq_len=256)
     m, mbs, S = 8, 2, 256   # same data for every world size
-    tr = PipelineTrainer(cfg, pp=world, schedule=a.schedule if world > 1 else "1F1B", n_microbatches=m, mbs=mbs,
+    dp = a.dp
+    pp = world // dp
+    tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m // dp,
+                         mbs=mbs,
                          seq_len=S, device=device, seed=3, graphs=bool(a.graphs),
                          split_head=bool(a.split_head), lr=1e-3)
     g = torch.Generator(device=device).manual_seed(11)
     x = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
     y = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
+    if dp > 1:   # each replica trains on its shard of the same global batch
+        n = x.shape[0] // dp
+        r = tr.mesh.dp_rank
+        x, y = x[r * n:(r + 1) * n].contiguous(), y[r * n:(r + 1) * n].contiguous()
     if a.graphs:
         tr.capture_graphs(x, y)
     losses = []
     for _ in range(a.steps):
         loss = tr.train_step(x, y)
         v = torch.tensor([float(loss) if loss is not None else 0.0], dtype=torch.float64, device=device)
-        if world > 1 and tr.head is None:
+        if world > 1:
             dist.all_reduce(v)
+            # the loss lives on one rank per replica (last stage) or on every rank (distributed head)
+            v /= dp * (pp if tr.head is not None else 1)
         losses.append(float(v.item()))
     if rank == 0:
         print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses,
