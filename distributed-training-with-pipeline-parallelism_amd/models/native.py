@@ -192,6 +192,58 @@ class MBContext:
 _FUSE_QKV_BIAS = os.environ.get("MIPIPE_FUSE_QKV_BIAS", "0") == "1"
 # MIPIPE_FUSE_FC1_BIAS=0: the fc1 bias gradient in a separate pass instead of the dX GEMM's epilogue
 _FUSE_FC1_BIAS = os.environ.get("MIPIPE_FUSE_FC1_BIAS", "1") != "0"
+# MIPIPE_WGRAD_STREAM=0: weight-gradient GEMMs inline on the compute stream (no overlap)
+_WGRAD_STREAM = os.environ.get("MIPIPE_WGRAD_STREAM", "1") != "0"
+_WGRAD_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+class WGradOverlap:
+    """Weight-gradient work of a full stage backward (``B``) on a second HIP stream.
+
+    The dX chain of a backward is the critical path (its result goes to the previous
+    stage); the dW GEMMs only feed the optimizer.  Issued on a side stream right after
+    their layer's dX work, they fill the CUs the dX GEMMs leave idle (an N = 768 output
+    is 192 256x256 tiles on 256 CUs) and overlap the memory-bound norm / attention
+    backward kernels.  Every job list stays referenced until the compute stream has
+    waited for it, so neither the caching allocator nor a HIP-graph capture's private
+    pool can hand its input blocks to a concurrent writer; at most ``depth`` layers are
+    in flight (bounded extra activation lifetime).  :meth:`join` closes the fork, so a
+    captured backward graph is self-contained.
+    """
+
+    def __init__(self, device: torch.device, depth: int = 2):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        side = _WGRAD_SIDE.get(idx)
+        if side is None:
+            side = _WGRAD_SIDE[idx] = torch.cuda.Stream(device=idx)
+        self.side = side
+        self.main = torch.cuda.current_stream(idx)
+        self.depth = depth
+        self.inflight: List[tuple] = []   # (completion event, job list)
+
+    @staticmethod
+    def make(device: torch.device, weight_grads: bool = True) -> Optional["WGradOverlap"]:
+        if not (_WGRAD_STREAM and weight_grads and device.type == "cuda"):
+            return None
+        return WGradOverlap(device)
+
+    def run(self, jobs: List[Callable[[], None]]) -> None:
+        if not jobs:
+            return
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            for j in jobs:
+                j()
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        self.inflight.append((ev, jobs))
+        while len(self.inflight) > self.depth:
+            self.main.wait_event(self.inflight.pop(0)[0])
+
+    def join(self) -> None:
+        if self.inflight:
+            self.main.wait_stream(self.side)
+            self.inflight.clear()
 
 
 def _seed(base: int, *parts: int) -> int:
@@ -326,9 +378,9 @@ class Block:
         return ctx.layers[self.i]
 
     def backward(self, dy: torch.Tensor, B: int, S: int, ctx: MBContext, weight_grads: bool = True,
-                 defer: Optional[list] = None):
+                 defer: Optional[list] = None, ov: Optional[WGradOverlap] = None):
         """Returns dx.  If ``weight_grads`` is False the dW GEMMs are appended to ``defer``
-        (zero-bubble split: I now, W later)."""
+        (zero-bubble split: I now, W later); with an ``ov`` they run on its side stream."""
         st = self._ensure(B, S, ctx)
         cfg = self.cfg
         sd = _seed(ctx.seed, self.i)
@@ -390,7 +442,9 @@ class Block:
             dh1 = ops.linear_dx(dqkv, self.w("attn.wqkv.weight"), wt=self.wt("attn.wqkv.weight"))
             dx, _ = ops.norm_bwd(dh1, st["x"], self.w("attn_norm.weight"), st["mu1"], st["rs1"], kind=kind,
                                  dres=dx2, dw=self.g("attn_norm.weight"), dbias=self.gb("attn_norm.bias"))
-        if weight_grads:
+        if ov is not None:
+            ov.run(wjobs)
+        elif weight_grads:
             for j in wjobs:
                 j()
         else:
@@ -722,6 +776,7 @@ class NativeModel:
     def backward(self, dy: Optional[torch.Tensor], ctx: MBContext, B: int, S: int, weight_grads: bool = True):
         cfg = self.cfg
         defer: List = []
+        ov = WGradOverlap.make(self.device, weight_grads)   # dW GEMMs on a side stream
         if self.last and self.split_head:
             # dy = dL/d(final-norm output), gathered from the head chunks
             if cfg.final_norm:
@@ -732,11 +787,15 @@ class NativeModel:
             dl = ctx.misc.pop("dlogits")
             hn = ctx.misc.pop("hn")
             W = self.head_weight()
-            dhn = ops.linear_dx(dl, W, wt=self.head_weight_t())
             jobs = [lambda dl=dl, hn=hn: ops.linear_dw(dl, hn, self.head_grad())]
             if self.arena.has("output.bias"):
                 jobs.append(lambda dl=dl: ops.colsum(dl, self.arena.g("output.bias")))
-            if weight_grads:
+            if ov is not None:
+                ov.run(jobs)    # the head dW runs beside the head dX GEMM
+            dhn = ops.linear_dx(dl, W, wt=self.head_weight_t())
+            if ov is not None:
+                pass    # already issued
+            elif weight_grads:
                 for j in jobs:
                     j()
             else:
@@ -748,7 +807,11 @@ class NativeModel:
             else:
                 dy = dhn
         for blk in reversed(self.blocks):
-            dy = blk.backward(dy, B, S, ctx, weight_grads=weight_grads, defer=defer)
+            dy = blk.backward(dy, B, S, ctx, weight_grads=weight_grads, defer=defer, ov=ov)
+        if ov is not None:
+            # close the fork before the embedding gradient: with tied weights it
+            # accumulates into the head's dW buffer
+            ov.join()
         if self.first:
             tokens = ctx.misc.pop("tokens")
             ea = self._emb_arena()
