@@ -318,6 +318,23 @@ void transpose_batched(torch::Tensor src, torch::Tensor dst, torch::Tensor desc,
         "transpose_batched");
 }
 
+// A private HIP stream (not from torch's round-robin pool, whose streams other users --
+// graph capture, process groups -- may also be handed).  Never destroyed: it lives as
+// long as the process, like the streams it is used beside.  priority: 0 = default,
+// -1 = the device's highest.
+int64_t create_stream(int64_t device, int64_t priority) {
+  int cur = 0;
+  TORCH_CHECK(hipGetDevice(&cur) == hipSuccess, "hipGetDevice");
+  TORCH_CHECK(hipSetDevice((int)device) == hipSuccess, "hipSetDevice");
+  int lo = 0, hi = 0;
+  TORCH_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess, "priority range");
+  hipStream_t s = nullptr;
+  const hipError_t e = hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority < 0 ? hi : lo);
+  hipSetDevice(cur);
+  TORCH_CHECK(e == hipSuccess, "hipStreamCreateWithPriority: ", hipGetErrorString(e));
+  return reinterpret_cast<int64_t>(s);
+}
+
 // training-step counter the dropout kernels mix into their seeds (mp_common.h
 // step_seed): stream-ordered, issued before a step's first replay, never captured
 void set_dropout_step(int64_t step) {
@@ -360,5 +377,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2", &gemm2);
   m.def("transpose", &transpose);
   m.def("set_dropout_step", &set_dropout_step);
+  m.def("create_stream", &create_stream, pybind11::arg("device"), pybind11::arg("priority") = 0);
   m.def("transpose_batched", &transpose_batched);
 }

@@ -1,19 +1,31 @@
-// Native RCCL point-to-point engine for the pipeline runtime (SURVEY §2.4 "P2P engine").
+// Native RCCL point-to-point engine for the pipeline runtime (SURVEY §2.4 "P2P engine",
+// §7.4-1 "separate communicators or streams per direction avoid head-of-line blocking").
 //
-// One RCCL communicator per pipeline group, created from a unique id that the Python side
-// broadcasts once over torch.distributed.  Every CommGroup of the lowered program becomes
-// one ncclGroupStart/End on a dedicated high-priority HIP comm stream:
+// Two RCCL communicators per pipeline group, one per traffic DIRECTION, each driven from
+// its own high-priority HIP stream:
 //
-//   post(sends, recvs):  event(current compute stream) -> comm stream waits on it (send
-//                        data produced, recv buffers free) -> grouped ncclSend/ncclRecv ->
-//                        "done" event recorded on the comm stream; returns a handle
-//   wait(handle):        the CURRENT stream waits on that event (no host block), exactly
-//                        where the runtime consumes a received buffer
+//   channel 0 ("fwd"):  activations flowing down the pipeline (F messages, and the last
+//                       stage's hidden rows to the distributed-head ranks, H messages)
+//   channel 1 ("bwd"):  gradients flowing back up (B messages, head input grads D)
 //
-// so transfers overlap compute and never stall the host.  Tensors touched by the comm
-// stream are registered with the caching allocator (recordStream), so their memory is not
-// reused before the transfer completes.  The order of groups is the globally consistent
-// order produced by parallel/lower.py, which is what RCCL's in-order semantics require.
+// RCCL runs the operations of one communicator in host-issue order and a large send
+// completes only when the peer's matching receive runs.  With ONE stream for both
+// directions an early-posted gradient receive (waiting on the downstream backward) holds
+// back every activation send queued after it, so the downstream rank starves.  With one
+// stream per direction the two flows never queue behind each other; parallel/simulate.py
+// (check_lowered(..., channels=2)) proves the per-channel order of a lowered program
+// cannot deadlock before the runtime uses it.  Each communicator is only ever used from
+// its own stream, in host order, so RCCL's per-communicator ordering rule holds.
+//
+//   post(ch, sends, recvs): event(current compute stream) -> channel stream waits on it
+//                           (send data produced, recv buffers free) -> grouped
+//                           ncclSend/ncclRecv -> "done" event; returns a handle
+//   wait(handle):           the CURRENT stream waits on that event (no host block)
+//
+// Tensors touched by a channel stream are registered with the caching allocator
+// (recordStream), so their memory is not reused before the transfer completes.
+// `abort()` (ncclCommAbort) tears both communicators down even with transfers in
+// flight -- the pre-flight ping uses it to back out of a link that does not answer.
 #pragma once
 #include <torch/extension.h>
 #include <c10/hip/HIPCachingAllocator.h>
@@ -23,6 +35,7 @@
 
 #include <dlfcn.h>
 
+#include <array>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -33,6 +46,8 @@ namespace py = pybind11;
 
 namespace mipipe_comm {
 
+constexpr int kChannels = 2;
+
 // RCCL entry points are resolved at run time from the librccl that PyTorch itself loaded
 // (torch/lib/librccl.so, shared with ProcessGroupNCCL): the extension does not link a second
 // RCCL into the process.  rccl.h only provides the types.
@@ -40,6 +55,8 @@ struct Rccl {
   decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
   decltype(&ncclCommInitRank) CommInitRank = nullptr;
   decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclCommAbort) CommAbort = nullptr;
+  decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
   decltype(&ncclSend) Send = nullptr;
   decltype(&ncclRecv) Recv = nullptr;
   decltype(&ncclGroupStart) GroupStart = nullptr;
@@ -58,8 +75,8 @@ inline void load_rccl(const std::string& path) {
 #define MP_SYM(f)                                                                      \
   r->f = reinterpret_cast<decltype(r->f)>(dlsym(h, "nccl" #f));                        \
   TORCH_CHECK(r->f != nullptr, "RcclP2P: missing symbol nccl" #f " in ", path);
-  MP_SYM(GetUniqueId) MP_SYM(CommInitRank) MP_SYM(CommDestroy) MP_SYM(Send) MP_SYM(Recv) MP_SYM(GroupStart)
-  MP_SYM(GroupEnd) MP_SYM(GetErrorString)
+  MP_SYM(GetUniqueId) MP_SYM(CommInitRank) MP_SYM(CommDestroy) MP_SYM(CommAbort) MP_SYM(CommGetAsyncError)
+  MP_SYM(Send) MP_SYM(Recv) MP_SYM(GroupStart) MP_SYM(GroupEnd) MP_SYM(GetErrorString)
 #undef MP_SYM
   g_rccl = r;
 }
@@ -99,64 +116,75 @@ class RcclP2P {
     MP_NCCL(g_rccl->GetUniqueId(&id));
     return py::bytes(id.internal, sizeof(id.internal));
   }
+  static int64_t id_bytes() { return (int64_t)sizeof(ncclUniqueId::internal); }
 
-  RcclP2P(const py::bytes& id, int nranks, int rank, int device) : nranks_(nranks), rank_(rank), device_(device) {
+  // ids: kChannels unique ids concatenated (one communicator per direction)
+  RcclP2P(const py::bytes& ids, int nranks, int rank, int device) : nranks_(nranks), rank_(rank), device_(device) {
     TORCH_CHECK(g_rccl != nullptr, "RcclP2P.load(<torch/lib/librccl.so>) first");
-    std::string s = id;
-    TORCH_CHECK(s.size() == sizeof(ncclUniqueId::internal), "RcclP2P: bad unique id size ", s.size());
-    ncclUniqueId uid;
-    std::memcpy(uid.internal, s.data(), s.size());
+    std::string s = ids;
+    const size_t n = sizeof(ncclUniqueId::internal);
+    TORCH_CHECK(s.size() == n * kChannels, "RcclP2P: expected ", kChannels, " unique ids (", n * kChannels,
+                " bytes), got ", s.size());
     MP_HIP(hipSetDevice(device));
-    MP_NCCL(g_rccl->CommInitRank(&comm_, nranks, uid, rank));
-    // high-priority stream from torch's pool: comm kernels are scheduled ahead of compute, and
-    // the stream outlives every tensor recordStream()-ed on it (the caching allocator records
-    // events on it when those tensors are freed, possibly after close())
-    comm_stream_ = c10::hip::getStreamFromPool(/*isHighPriority=*/true, device);
-    stream_ = comm_stream_.stream();
+    int lo = 0, hi = 0;
+    MP_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    for (int c = 0; c < kChannels; ++c) {
+      ncclUniqueId uid;
+      std::memcpy(uid.internal, s.data() + c * n, n);
+      MP_NCCL(g_rccl->CommInitRank(&comm_[c], nranks, uid, rank));
+      // A private high-priority stream per channel (not torch's round-robin pool, which
+      // could hand both channels -- or a compute user -- the same stream).  Never destroyed:
+      // the caching allocator may record events on it when recordStream()-ed tensors are
+      // freed after close().
+      MP_HIP(hipStreamCreateWithPriority(&stream_[c], hipStreamNonBlocking, hi));
+      hstream_[c] = c10::hip::getStreamFromExternal(stream_[c], device);
+    }
   }
 
   ~RcclP2P() { close(); }
 
   void close() {
-    if (stream_ != nullptr) {
-      hipStreamSynchronize(stream_);
-      for (auto& kv : pending_) hipEventDestroy(kv.second);
-      pending_.clear();
-      for (hipEvent_t e : pool_) hipEventDestroy(e);
-      pool_.clear();
-      stream_ = nullptr;
-    }
-    if (comm_ != nullptr) {
-      g_rccl->CommDestroy(comm_);
-      comm_ = nullptr;
+    if (open_) {
+      for (int c = 0; c < kChannels; ++c) hipStreamSynchronize(stream_[c]);
+      release_events();
+      for (int c = 0; c < kChannels; ++c)
+        if (comm_[c] != nullptr) g_rccl->CommDestroy(comm_[c]);
+      comm_ = {nullptr, nullptr};
+      open_ = false;
     }
   }
 
-  int64_t post(const std::vector<std::pair<torch::Tensor, int64_t>>& sends,
+  // Tear down with transfers possibly in flight (a peer that never answered).  Does not
+  // synchronise the channel streams: ncclCommAbort makes their kernels return.
+  void abort() {
+    if (!open_) return;
+    for (int c = 0; c < kChannels; ++c)
+      if (comm_[c] != nullptr) g_rccl->CommAbort(comm_[c]);
+    comm_ = {nullptr, nullptr};
+    pending_.clear();  // events leaked on purpose: their streams may still be unwinding
+    open_ = false;
+  }
+
+  // First asynchronous RCCL error of either communicator ("" if none).
+  std::string async_error() {
+    if (!open_) return "closed";
+    for (int c = 0; c < kChannels; ++c) {
+      ncclResult_t r = ncclSuccess;
+      if (g_rccl->CommGetAsyncError(comm_[c], &r) != ncclSuccess) return "ncclCommGetAsyncError failed";
+      if (r != ncclSuccess && r != ncclInProgress) return g_rccl->GetErrorString(r);
+    }
+    return "";
+  }
+
+  int64_t post(int channel, const std::vector<std::pair<torch::Tensor, int64_t>>& sends,
                const std::vector<std::pair<torch::Tensor, int64_t>>& recvs) {
-    TORCH_CHECK(comm_ != nullptr, "RcclP2P is closed");
-    hipStream_t cur = c10::hip::getCurrentHIPStream(device_).stream();
-    hipEvent_t ready = event();
-    MP_HIP(hipEventRecord(ready, cur));
-    MP_HIP(hipStreamWaitEvent(stream_, ready, 0));
-    pool_.push_back(ready);  // the wait above captured its state; reusable now
-    const c10::hip::HIPStream& cs = comm_stream_;
-    MP_NCCL(g_rccl->GroupStart());
-    for (const auto& [t, peer] : sends) {
-      TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RcclP2P: send tensors must be contiguous GPU tensors");
-      MP_NCCL(g_rccl->Send(t.data_ptr(), t.numel(), nccl_type(t), (int)peer, comm_, stream_));
-    }
-    for (const auto& [t, peer] : recvs) {
-      TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RcclP2P: recv tensors must be contiguous GPU tensors");
-      MP_NCCL(g_rccl->Recv(t.data_ptr(), t.numel(), nccl_type(t), (int)peer, comm_, stream_));
-    }
-    MP_NCCL(g_rccl->GroupEnd());
+    std::vector<RawOp> s, r;
+    for (const auto& [t, peer] : sends) s.push_back(raw(t, peer));
+    for (const auto& [t, peer] : recvs) r.push_back(raw(t, peer));
+    const int64_t h = post_raw(channel, s, r, c10::hip::getCurrentHIPStream(device_).stream());
+    const c10::hip::HIPStream& cs = hstream_[channel];
     for (const auto& p : sends) c10::hip::HIPCachingAllocator::recordStream(p.first.storage().data_ptr(), cs);
     for (const auto& p : recvs) c10::hip::HIPCachingAllocator::recordStream(p.first.storage().data_ptr(), cs);
-    hipEvent_t done = event();
-    MP_HIP(hipEventRecord(done, stream_));
-    const int64_t h = next_++;
-    pending_[h] = done;
     return h;
   }
 
@@ -169,18 +197,28 @@ class RcclP2P {
     ncclDataType_t type;
     int peer;
   };
-  int64_t post_raw(const std::vector<RawOp>& sends, const std::vector<RawOp>& recvs, hipStream_t compute) {
-    TORCH_CHECK(comm_ != nullptr, "RcclP2P is closed");
+  int64_t post_raw(int channel, const std::vector<RawOp>& sends, const std::vector<RawOp>& recvs,
+                   hipStream_t compute) {
+    TORCH_CHECK(open_, "RcclP2P is closed");
+    TORCH_CHECK(channel >= 0 && channel < kChannels, "RcclP2P: bad channel ", channel);
+    hipStream_t cs = stream_[channel];
+    ncclComm_t comm = comm_[channel];
     hipEvent_t ready = event();
     MP_HIP(hipEventRecord(ready, compute));
-    MP_HIP(hipStreamWaitEvent(stream_, ready, 0));
-    pool_.push_back(ready);
+    MP_HIP(hipStreamWaitEvent(cs, ready, 0));
+    pool_.push_back(ready);  // the wait above captured its state; reusable now
     MP_NCCL(g_rccl->GroupStart());
-    for (const auto& o : sends) MP_NCCL(g_rccl->Send(o.ptr, o.count, o.type, o.peer, comm_, stream_));
-    for (const auto& o : recvs) MP_NCCL(g_rccl->Recv(o.ptr, o.count, o.type, o.peer, comm_, stream_));
+    for (const auto& o : sends) {
+      TORCH_CHECK(o.peer >= 0 && o.peer < nranks_, "RcclP2P: bad send peer ", o.peer);
+      MP_NCCL(g_rccl->Send(o.ptr, o.count, o.type, o.peer, comm, cs));
+    }
+    for (const auto& o : recvs) {
+      TORCH_CHECK(o.peer >= 0 && o.peer < nranks_, "RcclP2P: bad recv peer ", o.peer);
+      MP_NCCL(g_rccl->Recv(o.ptr, o.count, o.type, o.peer, comm, cs));
+    }
     MP_NCCL(g_rccl->GroupEnd());
     hipEvent_t done = event();
-    MP_HIP(hipEventRecord(done, stream_));
+    MP_HIP(hipEventRecord(done, cs));
     const int64_t h = next_++;
     pending_[h] = done;
     return h;
@@ -194,28 +232,30 @@ class RcclP2P {
   }
 
   // make the current stream wait for a posted group (idempotent)
-  void wait(int64_t h) {
-    auto it = pending_.find(h);
-    if (it == pending_.end()) return;
-    hipStream_t cur = c10::hip::getCurrentHIPStream(device_).stream();
-    MP_HIP(hipStreamWaitEvent(cur, it->second, 0));
-    pool_.push_back(it->second);
-    pending_.erase(it);
-  }
+  void wait(int64_t h) { wait_raw(h, c10::hip::getCurrentHIPStream(device_).stream()); }
 
+  // host-side completion test (pre-flight ping polls it against a deadline)
   bool query(int64_t h) {
     auto it = pending_.find(h);
     return it == pending_.end() || hipEventQuery(it->second) == hipSuccess;
   }
 
   void synchronize() {
-    if (stream_ != nullptr) MP_HIP(hipStreamSynchronize(stream_));
+    if (open_)
+      for (int c = 0; c < kChannels; ++c) MP_HIP(hipStreamSynchronize(stream_[c]));
   }
 
   int rank() const { return rank_; }
   int nranks() const { return nranks_; }
+  int channels() const { return kChannels; }
+  int64_t stream_handle(int c) const { return reinterpret_cast<int64_t>(stream_[c]); }
 
  private:
+  RawOp raw(const torch::Tensor& t, int64_t peer) {
+    TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "RcclP2P: tensors must be contiguous GPU tensors");
+    return RawOp{t.data_ptr(), (size_t)t.numel(), nccl_type(t), (int)peer};
+  }
+
   hipEvent_t event() {
     if (!pool_.empty()) {
       hipEvent_t e = pool_.back();
@@ -227,9 +267,18 @@ class RcclP2P {
     return e;
   }
 
-  ncclComm_t comm_ = nullptr;
-  c10::hip::HIPStream comm_stream_{c10::hip::getDefaultHIPStream()};
-  hipStream_t stream_ = nullptr;
+  void release_events() {
+    for (auto& kv : pending_) hipEventDestroy(kv.second);
+    pending_.clear();
+    for (hipEvent_t e : pool_) hipEventDestroy(e);
+    pool_.clear();
+  }
+
+  std::array<ncclComm_t, kChannels> comm_{nullptr, nullptr};
+  std::array<hipStream_t, kChannels> stream_{nullptr, nullptr};
+  std::array<c10::hip::HIPStream, kChannels> hstream_{c10::hip::getDefaultHIPStream(),
+                                                      c10::hip::getDefaultHIPStream()};
+  bool open_ = true;
   int nranks_, rank_, device_;
   int64_t next_ = 1;
   std::unordered_map<int64_t, hipEvent_t> pending_;

@@ -900,15 +900,8 @@ static int choose(int M, int N, int K, bool acc, bool outer, int* split_out) {
   int best = 3, best_split = 1;
   float best_t = 3.0e38f;
   const int kt = K / BK;
-  // CUs an f32-accumulate (dW) GEMM plans for: it runs on the weight-gradient side stream
-  // beside the dX chain, so it may plan for a share of the chip (MIPIPE_DW_CUS, default 256)
-  static const int dw_cus = [] {
-    const char* e = getenv("MIPIPE_DW_CUS");
-    const int v = e ? atoi(e) : 256;
-    return v >= 16 && v <= 256 ? v : 256;
-  }();
   for (int c = 0; c < 4; ++c) {
-    const int cus = acc ? dw_cus : 256;
+    const int cus = 256;
     const int slots = c == 3 ? 2 * cus : cus;  // 128x128 tiles fit two workgroups per CU
     if (outer && CFGS[c].bn == 192) continue;  // outer-contig images need power-of-two widths
     const int tiles = ((M + CFGS[c].bm - 1) / CFGS[c].bm) * ((N + CFGS[c].bn - 1) / CFGS[c].bn);

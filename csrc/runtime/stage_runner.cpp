@@ -8,8 +8,10 @@
 //
 //   GRAPH  g         hipGraphLaunch(g) on the compute stream
 //   COPY   d, s, n   hipMemcpyAsync device -> device (a static graph input refreshed)
-//   POST   e, ops    one grouped ncclSend/ncclRecv on the RCCL engine's comm stream,
-//                    ordered after the compute stream (RcclP2P::post_raw); fills a slot
+//   POST   e, c, ops one grouped ncclSend/ncclRecv on channel c (0: activations down the
+//                    pipeline, 1: gradients up) of the RCCL engine -- that direction's own
+//                    communicator and stream, ordered after the compute stream
+//                    (RcclP2P::post_raw); fills a slot
 //   WAIT   slot      the compute stream waits for that group's completion event
 //   CALL   fn        a Python callable (anything not expressible above: gloo transfers,
 //                    DP all-reduce through torch.distributed) -- the GIL is taken only here
@@ -18,10 +20,19 @@
 // `run()` replays it with the GIL released: no per-action Python, no allocator calls, no
 // host synchronisation -- the host issues the whole step in tens of microseconds and the
 // GPU streams run ahead of it.
+//
+// Profiling (`set_profile(true)`): timing events are recorded on the compute stream at the
+// start of the step, around every GRAPH and at the end, so the measured pipeline bubble
+// (1 - busy / step) describes exactly the replayed execution that the benchmark times.
+// A graph launch completes only when all its nodes have (including the dW GEMMs it forks
+// onto the side stream), so its interval covers that work too.
 #include <torch/extension.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 
+#include <string>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "../comm/rccl_p2p.h"
@@ -44,11 +55,12 @@ class StageRunner {
 
   explicit StageRunner(int device) : device_(device) {}
 
-  void add_graph(int64_t graph_exec) {
+  void add_graph(int64_t graph_exec, const std::string& label) {
     TORCH_CHECK(graph_exec != 0, "stage runner: null graph exec");
     Instr i;
     i.kind = GRAPH;
     i.a = graph_exec;
+    i.label = label;
     tape_.push_back(std::move(i));
   }
 
@@ -63,12 +75,13 @@ class StageRunner {
 
   // sends / recvs: (device pointer, element count, dtype code, peer); dtype codes follow
   // torch (bf16 15, f32 6, f16 5, i64 4, i32 3, u8 0, f64 7).  Returns the slot a WAIT names.
-  int64_t add_post(py::object engine, const std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t>>& sends,
+  int64_t add_post(py::object engine, int channel, const std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t>>& sends,
                    const std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t>>& recvs) {
     Instr i;
     i.kind = POST;
     i.engine = engine.cast<RcclP2P*>();
     i.keep = engine;
+    i.channel = channel;
     for (const auto& [p, n, t, peer] : sends) i.sends.push_back({reinterpret_cast<void*>(p), (size_t)n, nccl(t), (int)peer});
     for (const auto& [p, n, t, peer] : recvs) i.recvs.push_back({reinterpret_cast<void*>(p), (size_t)n, nccl(t), (int)peer});
     i.slot = nslots_++;
@@ -91,23 +104,32 @@ class StageRunner {
     tape_.push_back(std::move(i));
   }
 
+  void set_profile(bool on) { profile_ = on; }
+
   // one step on the current HIP stream of `device`
   void run() {
     hipStream_t st = c10::hip::getCurrentHIPStream(device_).stream();
     std::vector<int64_t> handles(nslots_, -1);
     std::vector<RcclP2P*> engines(nslots_, nullptr);
+    const bool prof = profile_;
+    if (prof) prepare_events();
     py::gil_scoped_release nogil;
+    int ng = 0;
+    if (prof) MP_HIPCHK(hipEventRecord(ev_[0], st));
     for (const Instr& i : tape_) {
       switch (i.kind) {
         case GRAPH:
+          if (prof) MP_HIPCHK(hipEventRecord(ev_[2 + 2 * ng], st));
           MP_HIPCHK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(i.a), st));
+          if (prof) MP_HIPCHK(hipEventRecord(ev_[3 + 2 * ng], st));
+          ++ng;
           break;
         case COPY:
           MP_HIPCHK(hipMemcpyAsync(reinterpret_cast<void*>(i.a), reinterpret_cast<const void*>(i.b), (size_t)i.c,
                                    hipMemcpyDeviceToDevice, st));
           break;
         case POST:
-          handles[i.slot] = i.engine->post_raw(i.sends, i.recvs, st);
+          handles[i.slot] = i.engine->post_raw(i.channel, i.sends, i.recvs, st);
           engines[i.slot] = i.engine;
           break;
         case WAIT:
@@ -125,7 +147,31 @@ class StageRunner {
     // groups whose completion nobody consumed (sends): order them before the next step
     for (int64_t s = 0; s < nslots_; ++s)
       if (handles[s] >= 0) engines[s]->wait_raw(handles[s], st);
+    if (prof) {
+      MP_HIPCHK(hipEventRecord(ev_[1], st));
+      profiled_ = true;
+    }
     ++runs_;
+  }
+
+  // Last profiled step: (label, start_ms, end_ms) per GRAPH relative to the step start,
+  // and the step's total time on the compute stream.  Blocks until the step finished.
+  std::pair<std::vector<std::tuple<std::string, double, double>>, double> timeline() {
+    std::vector<std::tuple<std::string, double, double>> out;
+    TORCH_CHECK(profiled_, "stage runner: no profiled step (set_profile(True) and run())");
+    MP_HIPCHK(hipEventSynchronize(ev_[1]));
+    float total = 0.f;
+    MP_HIPCHK(hipEventElapsedTime(&total, ev_[0], ev_[1]));
+    int ng = 0;
+    for (const Instr& i : tape_) {
+      if (i.kind != GRAPH) continue;
+      float s = 0.f, e = 0.f;
+      MP_HIPCHK(hipEventElapsedTime(&s, ev_[0], ev_[2 + 2 * ng]));
+      MP_HIPCHK(hipEventElapsedTime(&e, ev_[0], ev_[3 + 2 * ng]));
+      out.emplace_back(i.label, (double)s, (double)e);
+      ++ng;
+    }
+    return {out, (double)total};
   }
 
   int64_t size() const { return (int64_t)tape_.size(); }
@@ -135,12 +181,31 @@ class StageRunner {
     for (const auto& i : tape_) k.push_back(i.kind);
     return k;
   }
+  std::vector<int64_t> channels() const {
+    std::vector<int64_t> k;
+    for (const auto& i : tape_)
+      if (i.kind == POST) k.push_back(i.channel);
+    return k;
+  }
 
  private:
+  void prepare_events() {
+    int64_t ng = 0;
+    for (const auto& i : tape_) ng += i.kind == GRAPH;
+    const size_t need = (size_t)(2 + 2 * ng);
+    while (ev_.size() < need) {
+      hipEvent_t e;
+      MP_HIPCHK(hipEventCreate(&e));  // timing enabled
+      ev_.push_back(e);
+    }
+  }
+
   struct Instr {
     int kind = GRAPH;
     int64_t a = 0, b = 0, c = 0;
     int64_t slot = -1;
+    int channel = 0;
+    std::string label;
     RcclP2P* engine = nullptr;
     py::object keep;  // keeps the engine alive
     std::vector<RcclP2P::RawOp> sends, recvs;
@@ -165,18 +230,24 @@ class StageRunner {
   std::vector<Instr> tape_;
   int64_t nslots_ = 0;
   int64_t runs_ = 0;
+  bool profile_ = false;
+  bool profiled_ = false;
+  std::vector<hipEvent_t> ev_;
 };
 
 void register_runner(py::module& m) {
   py::class_<StageRunner>(m, "StageRunner")
       .def(py::init<int>(), py::arg("device"))
-      .def("add_graph", &StageRunner::add_graph)
+      .def("add_graph", &StageRunner::add_graph, py::arg("graph_exec"), py::arg("label") = "")
       .def("add_copy", &StageRunner::add_copy)
       .def("add_post", &StageRunner::add_post)
       .def("add_wait", &StageRunner::add_wait)
       .def("add_call", &StageRunner::add_call)
       .def("run", &StageRunner::run)
+      .def("set_profile", &StageRunner::set_profile)
+      .def("timeline", &StageRunner::timeline)
       .def("kinds", &StageRunner::kinds)
+      .def("channels", &StageRunner::channels)
       .def_property_readonly("size", &StageRunner::size)
       .def_property_readonly("runs", &StageRunner::runs);
 }

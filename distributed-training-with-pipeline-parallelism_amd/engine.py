@@ -36,11 +36,18 @@ class FlatAdamW:
     across the pipeline group (a 4-byte all-reduce) -- no host synchronisation."""
 
     def __init__(self, arenas: List[ParamArena], lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
-                 weight_decay: float = 0.1, max_grad_norm: float = 1.0, pp_group=None, norm_skip=()):
+                 weight_decay: float = 0.1, max_grad_norm: float = 1.0, pp_group=None, norm_skip=(),
+                 norm_exclude=None, grad_scale: float = 1.0):
         self.arenas = arenas
         # arenas replicated across the pipeline group (distributed head) count in the
         # global grad norm on one rank only
         self.norm_skip = set(norm_skip)
+        # {arena index: [(offset, numel), ...]}: slices left out of the norm (a tied
+        # embedding's second copy on the last stage holds the same summed gradient)
+        self.norm_exclude = {i: sorted(r) for i, r in (norm_exclude or {}).items()}
+        # gradients arrive DP-summed (the all-reduces skip a separate divide pass); the
+        # 1/dp factor is applied inside the AdamW kernel (and to the clip norm)
+        self.grad_scale = float(grad_scale)
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_norm = max_grad_norm
         self.pp_group = pp_group
@@ -57,14 +64,21 @@ class FlatAdamW:
         if use_clip:
             self.sumsq.zero_()
             for i, a in enumerate(self.arenas):
-                if i not in self.norm_skip:
-                    ops.sumsq(a.grad, self.sumsq)
+                if i in self.norm_skip:
+                    continue
+                lo = 0
+                for off, n in self.norm_exclude.get(i, ()):
+                    if off > lo:
+                        ops.sumsq(a.grad[lo:off], self.sumsq)
+                    lo = max(lo, off + n)
+                if lo < a.grad.numel():
+                    ops.sumsq(a.grad[lo:] if lo else a.grad, self.sumsq)
             if self.pp_group is not None and dist.get_world_size(self.pp_group) > 1:
                 dist.all_reduce(self.sumsq, group=self.pp_group)
         for a, m, v in zip(self.arenas, self.m, self.v):
             ops.adamw_(a.master, a.grad, m, v, a.w16, a.n_decay, lr, self.betas[0], self.betas[1], self.eps, self.wd,
-                       self.step_count, self.sumsq if use_clip else None, self.max_norm if use_clip else 0.0, 1.0,
-                       zero_grad=True)
+                       self.step_count, self.sumsq if use_clip else None, self.max_norm if use_clip else 0.0,
+                       self.grad_scale, zero_grad=True)
             a.refresh_transposes()
 
     def state_dict(self):
@@ -122,7 +136,8 @@ class PipelineTrainer:
                  device=None, lr: float = 3e-4, weight_decay: float = 0.1, max_grad_norm: float = 1.0,
                  recompute: bool = False, profile: bool = False, seed: int = 0, style: str = "loop",
                  mesh: Optional[Mesh] = None, layer_ranges=None, dtype=torch.bfloat16,
-                 split_head: Optional[bool] = None, head_align: Optional[int] = None, graphs: bool = False):
+                 split_head: Optional[bool] = None, head_align: Optional[int] = None, graphs: bool = False,
+                 adam_eps: float = 1e-8):
         self.cfg = cfg
         self.schedule = canonical_name(schedule)
         style = REQUIRED_STYLE.get(self.schedule, style)
@@ -172,7 +187,7 @@ class PipelineTrainer:
             head_plan = HeadPlan(chunks, cfg.d_model, runner=self.head.run, dtype=dtype)
             if graphs and self.device.type == "cuda":
                 from .parallel.graphs import GraphCache
-                head_plan.graphs = GraphCache()
+                head_plan.graphs = GraphCache(f"{self.mesh.pp_rank}")
             self.head_chunks = chunks
         # recompute="auto": HBM plan from the schedule's in-flight microbatches (288 GB per
         # MI355X usually holds the whole stash, and recompute costs a forward per layer)
@@ -193,18 +208,33 @@ class PipelineTrainer:
             egroup = self.mesh.embed_group if (tied_pp and (s == 0 or s == num_stages - 1)) else None
             self.stages.append(NativeStage(model, mbs, seq_len, dp_group=self.mesh.dp_group, embed_group=egroup,
                                            seed=seed + 1000 * self.mesh.dp_rank, graphs=graphs))
-        p2p = P2P(self.mesh.pp_group, self.mesh.pipe_ranks, self.device)
+        p2p = P2P(self.mesh.pp_group, self.mesh.pipe_ranks, self.device, ctrl_group=self.mesh.ctrl_group)
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
                                        scale_grads=True, style=style, profile=profile, orders=orders,
                                        head=head_plan, head_costs=head_costs, stage_costs=stage_costs)
         arenas = [st.arena for st in self.stages]
         norm_skip = []
+        norm_exclude = {}
+        if (tied_pp or self._tie_local) and (num_stages - 1) in my_stages:
+            # the last stage's copy of the tied embedding holds the same (summed) gradient
+            # as stage 0's after post_step: count it once in the global norm
+            i = [st.stage_index for st in self.stages].index(num_stages - 1)
+            a = self.stages[i].arena
+            g = a.g("tok_embeddings.weight")
+            norm_exclude[i] = [(g.storage_offset() - a.grad.storage_offset(), g.numel())]
         if self.head is not None:
             arenas.append(self.head.arena)
             if self.mesh.pp_rank != 0:
                 norm_skip.append(len(arenas) - 1)
-        self.optimizer = FlatAdamW(arenas, lr=lr, weight_decay=weight_decay, max_grad_norm=max_grad_norm,
-                                   pp_group=self.mesh.pp_group if pp > 1 else None, norm_skip=norm_skip)
+            if dist.is_initialized() and dist.get_world_size() > 1:
+                # replicated head: gradient all-reduce (SUM) over every rank (pipeline x DP),
+                # issued asynchronously right after this rank's last head-arena write
+                hgrad = self.head.arena.grad
+                self.runtime.head_reduce = lambda: dist.all_reduce(hgrad, async_op=True)
+                self.runtime.head_reduce_after_stage0 = bool(cfg.tie_embeddings)
+        self.optimizer = FlatAdamW(arenas, lr=lr, eps=adam_eps, weight_decay=weight_decay, max_grad_norm=max_grad_norm,
+                                   pp_group=self.mesh.pp_group if pp > 1 else None, norm_skip=norm_skip,
+                                   norm_exclude=norm_exclude, grad_scale=1.0 / self.mesh.dp)
         self.last_losses: List[torch.Tensor] = []
 
     @property
@@ -236,9 +266,7 @@ class PipelineTrainer:
             g0.add_(gl)      # both copies were already DP-reduced with their stage arenas
             gl.copy_(g0)
         if self.head is not None:
-            # replicated head: one gradient all-reduce over every rank (pipeline x DP)
-            if dist.is_initialized() and dist.get_world_size() > 1:
-                dist.all_reduce(self.head.arena.grad)
+            # (the head gradient all-reduce was issued and waited on inside the step)
             parts = torch.stack([self.runtime.head_losses.get(i, torch.zeros((), device=self.device))
                                  for i in range(self.m)]).float()
             if self.mesh.pp_group is not None and dist.get_world_size(self.mesh.pp_group) > 1:

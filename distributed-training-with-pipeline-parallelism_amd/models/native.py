@@ -215,9 +215,23 @@ class WGradOverlap:
         idx = device.index if device.index is not None else torch.cuda.current_device()
         side = _WGRAD_SIDE.get(idx)
         if side is None:
-            side = _WGRAD_SIDE[idx] = torch.cuda.Stream(device=idx)
+            # Which stream (hence which hardware queue: HIP maps streams onto
+            # GPU_MAX_HW_QUEUES=4 queues per priority) carries the dW work matters a lot.
+            # Measured, GPT-2 small bench on one MI355X (profiles/r2_wgrad_stream_ab.txt):
+            # torch's normal-priority pool stream 831K tok/s; a private stream (normal or
+            # high priority) or the high-priority pool 725K; dW inline 800K.  Default: the
+            # pool stream; MIPIPE_WGRAD_POOL=high|0 selects the alternatives for A/B runs.
+            pool = os.environ.get("MIPIPE_WGRAD_POOL", "1")
+            if pool in ("1", "high"):
+                side = torch.cuda.Stream(device=idx, priority=-1 if pool == "high" else 0)
+            else:
+                side = torch.cuda.ExternalStream(ops.load_ext().create_stream(idx, 0),
+                                                 device=torch.device("cuda", idx))
+            _WGRAD_SIDE[idx] = side
         self.side = side
         self.main = torch.cuda.current_stream(idx)
+        if self.side.cuda_stream == self.main.cuda_stream:
+            raise RuntimeError("weight-gradient side stream is the compute stream: no overlap possible")
         self.depth = depth
         self.inflight: List[tuple] = []   # (completion event, job list)
 

@@ -54,7 +54,7 @@ class NativeStage(StageBase):
         # seeds, ops.set_dropout_step, so replays draw fresh masks)
         if graphs and model.device.type != "cuda":
             graphs = False
-        self.graphs = GraphCache() if graphs else None
+        self.graphs = GraphCache(str(self.stage_index)) if graphs else None
         self._gctx = {}
 
     def _graphed(self) -> bool:
@@ -151,8 +151,12 @@ class NativeStage(StageBase):
         if not scaled_in_loss:
             self.arena.grad.div_(n_microbatches)
         if self.dp_group is not None and dist.get_world_size(self.dp_group) > 1:
-            return allreduce_flat(self.arena.grad, self.dp_group)
+            # SUM: the 1/dp average is folded into the AdamW kernel (engine.FlatAdamW)
+            return allreduce_flat(self.arena.grad, self.dp_group, average=False)
         return None
+
+    def has_grad_reduction(self, scaled_in_loss):
+        return (not scaled_in_loss) or (self.dp_group is not None and dist.get_world_size(self.dp_group) > 1)
 
     def post_step(self):
         if self.embed_group is not None and self.cfg.tie_embeddings and self.arena.has("tok_embeddings.weight"):

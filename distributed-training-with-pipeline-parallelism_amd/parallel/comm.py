@@ -1,11 +1,13 @@
 """Point-to-point transport between pipeline stages.
 
-On MI355X the backend is RCCL (``torch.distributed`` backend ``"nccl"``) over the
-point-to-point xGMI links; on CPU it is gloo (reference plumbing config,
-helper:175).  The executor hands this module :class:`~.ir.CommGroup` s whose
-per-peer order is already globally consistent (:mod:`.lower`), so each group is
-posted as one ``batch_isend_irecv`` (= one RCCL group: both directions of a link
-progress together) and nothing here needs to sort or retry.
+On MI355X the transport is the native RCCL engine (csrc/comm/rccl_p2p.h) over the
+point-to-point xGMI links: one communicator and one high-priority HIP stream per
+traffic direction (activations down, gradients up), grouped ``ncclSend``/``ncclRecv``,
+pre-flight pinged at construction with an in-process fallback to torch p2p if any
+pipeline rank fails.  On CPU it is gloo (reference plumbing config, helper:175).  The
+executor hands this module :class:`~.ir.CommGroup` s whose per-peer order is already
+globally consistent (:mod:`.lower`) and proven hang-free for the channel split in use
+(:func:`.simulate.check_lowered`), so nothing here needs to sort or retry.
 
 Static shapes: unlike the dependency's runtime shape inference with pickled
 meta-tensors (stage.py:1410-1519, C4 in SURVEY §2.6), stages declare their tensor
@@ -14,11 +16,15 @@ as small int64 tensors once at init (no pickling).
 """
 from __future__ import annotations
 
+import logging
 import os
+import time
 from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+
+log = logging.getLogger("mipipe.comm")
 
 _DTYPES = [torch.float32, torch.bfloat16, torch.float16, torch.int64, torch.int32, torch.float64, torch.uint8,
            torch.bool, torch.int8]
@@ -70,18 +76,24 @@ def load_native_rccl(ext) -> None:
     ext.RcclP2P.load(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
 
 
+# message kind -> engine channel: 0 = activations down the pipeline (F, and the last
+# stage's hidden rows to the head ranks, H), 1 = gradients back up (B, head grads D)
+CHANNEL_OF_KIND = {"F": 0, "H": 0, "B": 1, "D": 1}
+
+
 def make_native_engine(group, ranks: Sequence[int], my_pipe_rank: int, device: torch.device):
-    """Collective over the pipeline group: pipeline rank 0 draws an RCCL unique id, the
-    group broadcasts it, every rank joins the communicator (csrc/comm/rccl_p2p.cpp)."""
+    """Collective over the pipeline group: pipeline rank 0 draws one RCCL unique id per
+    channel, the group broadcasts them, every rank joins both communicators
+    (csrc/comm/rccl_p2p.h)."""
     from ..ops.kernels import load_ext
     ext = load_ext()
     if ext is None or not hasattr(ext, "RcclP2P"):
-        raise RuntimeError("MIPIPE_P2P=native needs the built extension (_C.so)")
+        raise RuntimeError("the native RCCL engine needs the built extension (_C.so)")
     load_native_rccl(ext)
-    n = 128
-    buf = torch.zeros(n, dtype=torch.uint8, device=device)
+    nb = int(ext.RcclP2P.id_bytes()) * 2
+    buf = torch.zeros(nb, dtype=torch.uint8, device=device)
     if my_pipe_rank == 0:
-        uid = ext.RcclP2P.unique_id()
+        uid = ext.RcclP2P.unique_id() + ext.RcclP2P.unique_id()
         buf.copy_(torch.frombuffer(bytearray(uid), dtype=torch.uint8))
     if len(ranks) > 1:
         dist.broadcast(buf, src=ranks[0], group=group)
@@ -89,43 +101,149 @@ def make_native_engine(group, ranks: Sequence[int], my_pipe_rank: int, device: t
     return ext.RcclP2P(uid, len(ranks), my_pipe_rank, device.index if device.index is not None else 0)
 
 
-class P2P:
-    """Thin wrapper around ``torch.distributed`` p2p for one pipeline group.
+def preflight(engine, peers: Sequence[int], me: int, device: torch.device, timeout_s: float) -> Tuple[bool, str]:
+    """Ping every peer on every channel of a native engine (one grouped send+recv per
+    channel) and poll for completion against a host deadline.  Also establishes the RCCL
+    connections up front (the role of torch's p2p warm-up, stage.py:925-979).
+    Returns (ok, reason)."""
+    peers = sorted(set(p for p in peers if p != me))
+    if not peers:
+        return True, ""
+    handles, recvs = [], []
+    for ch in range(engine.channels):
+        s = [(torch.full((1,), float(me * 16 + ch), device=device), p) for p in peers]
+        r = [(torch.full((1,), -1.0, device=device), p) for p in peers]
+        handles.append(engine.post(ch, s, r))
+        recvs.append(r)
+    deadline = time.monotonic() + timeout_s
+    while not all(engine.query(h) for h in handles):
+        err = engine.async_error()
+        if err:
+            return False, f"RCCL async error: {err}"
+        if time.monotonic() > deadline:
+            return False, f"no answer from peers {peers} within {timeout_s:.0f}s"
+        time.sleep(0.002)
+    for h in handles:
+        engine.wait(h)
+    torch.cuda.current_stream(device).synchronize()
+    for ch, r in enumerate(recvs):
+        for t, p in r:
+            if float(t.item()) != float(p * 16 + ch):
+                return False, f"channel {ch}: wrong ping payload from peer {p}: {float(t.item())}"
+    return True, ""
 
-    ``ranks[i]`` is the global rank of pipeline rank ``i``.  With the gloo backend and
-    GPU tensors (``MIPIPE_DIST_BACKEND=gloo``: several ranks sharing one GPU, used to
-    test the whole multi-process GPU stack on a single-GPU box) transfers are staged
-    through host memory; with RCCL they go device to device over xGMI.
+
+def agree(ok: bool, group, device: torch.device) -> bool:
+    """True iff every rank of ``group`` reports ok (control plane: a gloo group when
+    available, so a wedged RCCL channel cannot block the vote)."""
+    if group is None or not dist.is_initialized():
+        return ok
+    backend = dist.get_backend(group)
+    dev = torch.device("cpu") if backend == "gloo" else device
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()) == 1)
+
+
+class P2P:
+    """Point-to-point transport of one pipeline group.
+
+    ``ranks[i]`` is the global rank of pipeline rank ``i``.  Modes (``mode`` argument or
+    ``MIPIPE_P2P``):
+
+    * ``auto`` (default) / ``native`` -- on GPUs with the RCCL backend, the C++ engine
+      (csrc/comm/rccl_p2p.h): one communicator + stream per direction, grouped
+      ncclSend/ncclRecv, posts replayed natively by the stage runner.  It is created and
+      pinged (:func:`preflight`) at construction; if any rank of the pipeline fails, every
+      rank agrees (:func:`agree`) to fall back to torch p2p in-process -- ``auto`` logs
+      ``fallback_reason``, ``native`` raises.
+    * ``torch`` -- ``torch.distributed.batch_isend_irecv`` (ProcessGroupNCCL = RCCL, or gloo).
+
+    With the gloo backend and GPU tensors (``MIPIPE_DIST_BACKEND=gloo``: several ranks
+    sharing one GPU, used to test the whole multi-process GPU stack on a single-GPU box)
+    transfers are staged through host memory.
     """
 
-    def __init__(self, group: Optional[dist.ProcessGroup], ranks: Sequence[int], device: torch.device):
+    def __init__(self, group: Optional[dist.ProcessGroup], ranks: Sequence[int], device: torch.device,
+                 mode: Optional[str] = None, ctrl_group=None, preflight_timeout: Optional[float] = None):
         self.group = group
         self.ranks = list(ranks)
         self.device = device
         self.host_staged = (device.type == "cuda" and dist.is_initialized()
                             and dist.get_backend(group) == "gloo")
-        # MIPIPE_P2P=native: grouped ncclSend/ncclRecv from the C++ engine on its own comm
-        # stream instead of torch.distributed.batch_isend_irecv
+        mode = (mode or os.environ.get("MIPIPE_P2P", "auto")).lower()
+        if mode not in ("auto", "native", "torch"):
+            raise ValueError(f"MIPIPE_P2P={mode}: expected auto, native or torch")
         self.engine = None
-        if (os.environ.get("MIPIPE_P2P", "torch") == "native" and device.type == "cuda" and dist.is_initialized()
-                and not self.host_staged and len(self.ranks) > 1):
+        self.channels = 1
+        self.fallback_reason = ""
+        capable = (device.type == "cuda" and dist.is_initialized() and not self.host_staged and len(self.ranks) > 1)
+        if mode != "torch" and capable:
+            timeout = preflight_timeout if preflight_timeout is not None else \
+                float(os.environ.get("MIPIPE_P2P_PREFLIGHT_S", "60"))
             me = self.ranks.index(dist.get_rank())
-            self.engine = make_native_engine(group, self.ranks, me, device)
+            eng, ok, why = None, False, ""
+            try:
+                eng = make_native_engine(group, self.ranks, me, device)
+                ok, why = preflight(eng, range(len(self.ranks)), me, device, timeout)
+            except Exception as e:  # noqa: BLE001 - reported, then the whole pipeline falls back
+                ok, why = False, f"{type(e).__name__}: {e}"
+            all_ok = agree(ok, ctrl_group if ctrl_group is not None else group, device)
+            if all_ok:
+                self.engine = eng
+                self.channels = int(eng.channels)
+            else:
+                if eng is not None:
+                    eng.abort()
+                self.fallback_reason = why or "a peer's native engine failed its pre-flight"
+                if mode == "native":
+                    raise RuntimeError(f"MIPIPE_P2P=native: {self.fallback_reason}")
+                log.warning("native RCCL p2p engine not used (%s); torch p2p instead", self.fallback_reason)
+
+    @property
+    def kind(self) -> str:
+        """Transport actually in use: native | torch | gloo-staged | none."""
+        if self.engine is not None:
+            return "native"
+        if len(self.ranks) <= 1 or not dist.is_initialized():
+            return "none"
+        return "gloo-staged" if self.host_staged else "torch"
+
+    def use_single_channel(self) -> None:
+        """Post both directions on channel 0 (the lowered program's two-channel order was
+        not proven deadlock-free, see simulate.check_lowered)."""
+        self.channels = 1
 
     def global_rank(self, pipe_rank: int) -> int:
         return self.ranks[pipe_rank]
 
-    def post(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]]):
-        """Post one group; returns (send_works, recv_works) aligned with the inputs."""
+    def post(self, sends: Sequence[Tuple[torch.Tensor, int]], recvs: Sequence[Tuple[torch.Tensor, int]],
+             send_ch: Optional[Sequence[int]] = None, recv_ch: Optional[Sequence[int]] = None):
+        """Post one group; returns (send_works, recv_works) aligned with the inputs.
+        ``send_ch``/``recv_ch`` give each op's channel (native engine: the group is split
+        into one grouped call per channel; torch: ignored, one batch)."""
         from . import native_runner
         rec = native_runner.active()
         if self.engine is not None:
             if not sends and not recvs:
                 return [], []
-            h = self.engine.post([(t, p) for t, p in sends], [(t, p) for t, p in recvs])
-            slot = rec.native_post(self.engine, sends, recvs) if rec is not None else -1
-            w = _NativeWork(self.engine, h, rec, slot)
-            return [w] * len(sends), [w] * len(recvs)
+            sc = [0] * len(sends) if send_ch is None or self.channels == 1 else list(send_ch)
+            rc = [0] * len(recvs) if recv_ch is None or self.channels == 1 else list(recv_ch)
+            works_s: List = [None] * len(sends)
+            works_r: List = [None] * len(recvs)
+            for ch in sorted(set(sc) | set(rc)):
+                s_ = [sends[i] for i in range(len(sends)) if sc[i] == ch]
+                r_ = [recvs[i] for i in range(len(recvs)) if rc[i] == ch]
+                h = self.engine.post(ch, s_, r_)
+                slot = rec.native_post(self.engine, ch, s_, r_) if rec is not None else -1
+                w = _NativeWork(self.engine, h, rec, slot)
+                for i in range(len(sends)):
+                    if sc[i] == ch:
+                        works_s[i] = w
+                for i in range(len(recvs)):
+                    if rc[i] == ch:
+                        works_r[i] = w
+            return works_s, works_r
         if rec is not None:
             # transfers through torch.distributed replay as CALLs on the same tensors
             ns = len(sends)
@@ -201,6 +319,8 @@ class P2P:
         Pairs are exchanged in ascending (low, high) order on both sides so the
         first RCCL p2p on each link cannot cross-wait.
         """
+        if self.engine is not None:
+            return      # every link of both channels was pinged by preflight()
         for peer in sorted(set(peers)):
             if peer == my_rank:
                 continue

@@ -43,10 +43,18 @@ def _tensors(obj, out: List[torch.Tensor]) -> List[torch.Tensor]:
 
 
 class GraphCache:
-    def __init__(self):
+    def __init__(self, name: str = ""):
+        self.name = name
         self.graphs: Dict[Hashable, tuple] = {}
         self.captures = 0
         self.replays = 0
+
+    def label(self, key) -> str:
+        """Action label of a graph key on the tape, e.g. ('F', 3) -> 'F3' (prefixed by
+        ``self.name``, the stage index or 'H')."""
+        if isinstance(key, tuple) and len(key) == 2:
+            return f"{self.name}{key[0]}{key[1]}"
+        return f"{self.name}{key}"
 
     def __contains__(self, key) -> bool:
         return key in self.graphs
@@ -80,7 +88,7 @@ class GraphCache:
             self.replays += 1
         entry[0].replay()
         if rec is not None:
-            rec.graph(entry[0])
+            rec.graph(entry[0], self.label(key))
         return entry[2]
 
     def clear(self) -> None:

@@ -22,8 +22,14 @@ import torch
 import torch.distributed as dist
 
 
-def init_distributed(backend: Optional[str] = None, timeout_s: float = 600.0) -> tuple:
-    """Initialise the default process group from env; returns (rank, world, local_rank, device)."""
+def init_distributed(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> tuple:
+    """Initialise the default process group from env; returns (rank, world, local_rank, device).
+
+    ``timeout_s`` (default ``MIPIPE_PG_TIMEOUT_S`` or 300 s) bounds every collective and
+    p2p wait of the process group -- well under a launcher's own limit, so a hung peer
+    ends the job with an error instead of running into an external kill."""
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("MIPIPE_PG_TIMEOUT_S", "300"))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -63,6 +69,7 @@ class Mesh:
     pp_group: Optional[object]
     dp_group: Optional[object]
     embed_group: Optional[object]   # first + last stage of my pipeline (tied embeddings)
+    ctrl_group: Optional[object] = None   # gloo group of my pipeline: control-plane votes
 
     @property
     def is_first(self) -> bool:
@@ -81,9 +88,20 @@ def build_mesh(pp: int, dp: int = 1, backend_device: Optional[torch.device] = No
     if pp * dp != world:
         raise ValueError(f"pp({pp}) x dp({dp}) != world size {world}")
     dp_rank, pp_rank = divmod(rank, pp)
-    pp_group = dp_group = embed_group = None
+    pp_group = dp_group = embed_group = ctrl_group = None
     pipe_ranks = [dp_rank * pp + i for i in range(pp)]
     if world > 1:
+        # host-side (gloo) group per pipeline for control-plane agreement (the native p2p
+        # engine's pre-flight vote): it cannot be blocked by a wedged GPU communicator
+        gloo_default = dist.get_backend() == "gloo"
+        for d in range(dp):
+            ranks = [d * pp + i for i in range(pp)]
+            if gloo_default:
+                g = None
+            else:
+                g = dist.new_group(ranks, backend="gloo") if pp > 1 else None
+            if d == dp_rank:
+                ctrl_group = g
         # every rank must create every group, in the same order
         for d in range(dp):
             ranks = [d * pp + i for i in range(pp)]
@@ -113,4 +131,6 @@ def build_mesh(pp: int, dp: int = 1, backend_device: Optional[torch.device] = No
             dist.all_reduce(t, group=embed_group)
         if dev.type == "cuda":
             torch.cuda.synchronize()
-    return Mesh(rank, world, pp, dp, pp_rank, dp_rank, pipe_ranks, pp_group, dp_group, embed_group)
+    if ctrl_group is None and world > 1 and dist.get_backend() == "gloo":
+        ctrl_group = pp_group
+    return Mesh(rank, world, pp, dp, pp_rank, dp_rank, pipe_ranks, pp_group, dp_group, embed_group, ctrl_group)

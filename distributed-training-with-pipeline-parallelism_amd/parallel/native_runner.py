@@ -8,8 +8,8 @@ point-to-point transfers and waits.  :class:`TapeRecorder` observes one real Pyt
 a ``StageRunner`` (csrc/runtime/stage_runner.cpp) that replays the step with the GIL
 released: no per-action Python, no allocator traffic, no host synchronisation.
 
-Transfers on the native RCCL engine (``MIPIPE_P2P=native``) become native POST/WAIT
-instructions; transfers through ``torch.distributed`` (RCCL via ProcessGroupNCCL, or gloo)
+Transfers on the native RCCL engine (the default p2p transport on GPUs) become native
+POST/WAIT instructions (one per direction channel); transfers through ``torch.distributed`` (RCCL via ProcessGroupNCCL, or gloo)
 and DP all-reduces become CALL instructions that re-issue the same Python call on the same
 persistent tensors, so the runner is exact for every backend.  Anything that would break
 replay (a graph captured during the recording step, a dependency tracker or profiler
@@ -41,7 +41,8 @@ class TapeRecorder:
         ext = load_ext()
         if ext is None or not hasattr(ext, "StageRunner"):
             raise RuntimeError("the native stage runner needs the built extension (_C.so)")
-        self.runner = ext.StageRunner(device.index if device.index is not None else torch.cuda.current_device())
+        idx = device.index if device.index is not None else (torch.cuda.current_device() if device.type == "cuda" else 0)
+        self.runner = ext.StageRunner(idx)
         self.valid = True
         self.reason = ""
         self._holders: Dict[int, list] = {}
@@ -65,8 +66,8 @@ class TapeRecorder:
             self.valid, self.reason = False, why
 
     # ------------------------------------------------------------------ instructions
-    def graph(self, g: torch.cuda.CUDAGraph) -> None:
-        self.runner.add_graph(int(g.raw_cuda_graph_exec()))
+    def graph(self, g: torch.cuda.CUDAGraph, label: str = "") -> None:
+        self.runner.add_graph(int(g.raw_cuda_graph_exec()), str(label))
 
     def copy(self, dst: torch.Tensor, src: torch.Tensor) -> None:
         if not (dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype
@@ -75,7 +76,7 @@ class TapeRecorder:
             return
         self.runner.add_copy(dst.data_ptr(), src.data_ptr(), dst.numel() * dst.element_size())
 
-    def native_post(self, engine, sends, recvs) -> int:
+    def native_post(self, engine, channel: int, sends, recvs) -> int:
         def ops(lst):
             out = []
             for t, peer in lst:
@@ -85,7 +86,7 @@ class TapeRecorder:
                     code = 6
                 out.append((t.data_ptr(), t.numel(), code, int(peer)))
             return out
-        return self.runner.add_post(engine, ops(sends), ops(recvs))
+        return self.runner.add_post(engine, int(channel), ops(sends), ops(recvs))
 
     def native_wait(self, slot: int) -> None:
         self.runner.add_wait(slot)

@@ -40,6 +40,7 @@ from .headsplit import HeadPlan
 from .ir import Action, CommGroup, Entry, Op, format_compute_grid
 from .lower import lower
 from .schedules import canonical_name, generate, stage_to_rank
+from .simulate import message_channel
 from .stage import StageBase, specs_of
 from .validate import validate
 
@@ -141,11 +142,21 @@ class PipelineRuntime:
             self.orders = {r: [e for e in es if isinstance(e, Action) and e.op.is_compute] for r, es in program.items()}
         self.program_all = program
         self.program = program[pp_rank]
+        # the native engine posts each group split by direction (one RCCL communicator +
+        # stream per channel): use that only if the split order is proven hang-free
+        if getattr(p2p, "channels", 1) > 1:
+            from .simulate import check_lowered
+            try:
+                check_lowered(program, self.num_stages, channels=p2p.channels)
+            except RuntimeError as e:
+                log.warning("two-channel p2p order not provably safe (%s): single channel", e)
+                p2p.use_single_channel()
         self.device = any_stage.device
         self.profile = profile
         self.timer = _Timer(self.device)
         self.last_timeline: List[Tuple[str, float, float]] = []
         self.last_step_ms: float = 0.0
+        self.last_timeline_source = ""
         self._initialized = False
         self._recv_bufs: Dict[tuple, List[torch.Tensor]] = {}
         self._dh_full: Dict[int, torch.Tensor] = {}
@@ -160,6 +171,13 @@ class PipelineRuntime:
         self.native_enabled = os.environ.get("MIPIPE_NATIVE_RUNNER", "1") != "0"
         self.native_runner = None
         self.native_reason = "not recorded yet"
+        # distributed head: ``head_reduce()`` issues the async all-reduce of the replicated
+        # head gradient; it runs right after this rank's last action that writes the head
+        # arena (its last H; with tied embeddings also stage 0's last backward), so it
+        # overlaps the rest of the flush instead of following the step
+        self.head_reduce: Optional[Callable[[], object]] = None
+        self.head_reduce_after_stage0 = False
+        self._head_reduce_idx: Optional[int] = None
         self._in_bufs: Dict[int, Tuple[torch.Tensor, ...]] = {}
         self._tgt_bufs: Dict[int, torch.Tensor] = {}
         self._loss_bufs: Dict[tuple, torch.Tensor] = {}
@@ -243,7 +261,7 @@ class PipelineRuntime:
     def _native_possible(self, return_outputs: bool) -> bool:
         if not self.native_enabled or return_outputs or self.device.type != "cuda":
             return False
-        if self.deps is not None or self.profile or self.ranges:
+        if self.deps is not None or self.ranges:
             return False
         if any(getattr(st, "graphs", None) is None for st in self.stages.values()):
             return False
@@ -290,7 +308,19 @@ class PipelineRuntime:
             st.clear_runtime_states()
         self._steps += 1
         self._persist_inputs(inputs, targets)
-        self.native_runner.run()
+        prof = self.profile
+        if prof:
+            self.native_runner.set_profile(True)
+        try:
+            self.native_runner.run()
+        finally:
+            if prof:
+                self.native_runner.set_profile(False)
+        if prof:
+            # measured on the replayed tape itself: GRAPH intervals on the compute stream
+            tl, total = self.native_runner.timeline()
+            self.last_timeline, self.last_step_ms = [(str(a), float(s_), float(e)) for a, s_, e in tl], float(total)
+            self.last_timeline_source = "native tape"
         for st in self.stages.values():
             st.post_step()
         mb_losses = {k[1]: t for k, t in self._loss_bufs.items() if k[0] == "L"}
@@ -310,6 +340,8 @@ class PipelineRuntime:
         if possible and self.native_runner is not None:
             return self._step_native(inputs, targets, losses)
         rec = None
+        if possible and self.profile:
+            possible = False    # the recording step itself is not the profiled path
         if possible:
             from .native_runner import TapeRecorder
             inputs, targets = self._persist_inputs(inputs, targets)
@@ -367,24 +399,34 @@ class PipelineRuntime:
                 return contextlib.nullcontext()
             return _Range(f"PP:{a}")
 
+        hr_idx = self._head_reduce_index() if self.head_reduce is not None else None
         for idx, e in enumerate(self.program):
+            if hr_idx is not None and idx == hr_idx:
+                if rec is not None:
+                    from .native_runner import record_issue
+                    reduce_works.extend(record_issue(rec, lambda: [self.head_reduce()]))
+                else:
+                    reduce_works.append(self.head_reduce())
             try:
                 if isinstance(e, CommGroup):
-                    sends, recvs, rkeys = [], [], []
+                    sends, recvs, rkeys, sch, rch = [], [], [], [], []
                     for op in e.ops:
+                        ch = message_channel(op.key)
                         if op.action.op.is_send:
                             if deps is not None:
                                 deps.on_send(op.key, send_tensors)
                             ts = send_tensors.pop(op.key)
                             sends += [(t, op.peer) for t in ts]
+                            sch += [ch] * len(ts)
                             send_keep.append(ts)
                         else:
                             if deps is not None:
                                 deps.on_post_recv(op.key)
                             bufs = self._recv_buf(op.key)
                             recvs += [(t, op.peer) for t in bufs]
+                            rch += [ch] * len(bufs)
                             rkeys += [op.key] * len(bufs)
-                    sw, rw = self.p2p.post(sends, recvs)
+                    sw, rw = self.p2p.post(sends, recvs, sch, rch)
                     send_keep.extend(sw)
                     for k, w in zip(rkeys, rw):
                         recv_works.setdefault(k, []).append(w)
@@ -392,6 +434,8 @@ class PipelineRuntime:
                 a = e
                 st = self.stages.get(a.stage)
                 if a.op == Op.REDUCE_GRAD:
+                    if rec is not None and not st.has_grad_reduction(self.scale_grads):
+                        continue    # nothing to issue (no DP, scale folded into the loss): no CALL
                     if rec is not None:
                         from .native_runner import record_issue
 
@@ -413,6 +457,12 @@ class PipelineRuntime:
             except Exception:
                 self._report_failure(idx)
                 raise
+        if hr_idx is not None and hr_idx >= len(self.program):
+            if rec is not None:
+                from .native_runner import record_issue
+                reduce_works.extend(record_issue(rec, lambda: [self.head_reduce()]))
+            else:
+                reduce_works.append(self.head_reduce())
         if deps is not None:
             deps.finish(send_tensors, handoff)
         for w in send_keep:
@@ -424,12 +474,31 @@ class PipelineRuntime:
             st.post_step()
         if self.profile:
             self.last_timeline, self.last_step_ms = self.timer.finish()
+            self.last_timeline_source = "python executor"
         if losses is not None and mb_losses:
             losses.extend(mb_losses[i] for i in sorted(mb_losses))
         self._last_losses = mb_losses
         if self.stages.get(S - 1) is not None and return_outputs:
             return [outputs[i] for i in sorted(outputs)]
         return None
+
+    def _head_reduce_index(self) -> int:
+        """Program index right after this rank's last write to the head arena (and after
+        the sends that directly follow it, so the peer's transfers are not held back)."""
+        if self._head_reduce_idx is None:
+            last = -1
+            for i, e in enumerate(self.program):
+                if not isinstance(e, Action):
+                    continue
+                if e.op == Op.H or (self.head_reduce_after_stage0 and e.stage == 0 and
+                                    e.op in (Op.B, Op.I, Op.W)):
+                    last = i
+            j = last + 1
+            while j < len(self.program) and isinstance(self.program[j], CommGroup) and \
+                    all(op.action.op.is_send for op in self.program[j].ops):
+                j += 1
+            self._head_reduce_idx = j
+        return self._head_reduce_idx
 
     def _run_compute(self, a: Action, st, inputs, targets, return_outputs, loss_scale, handoff, outputs, mb_losses,
                      wait_recv, read_recv, produce) -> None:
@@ -510,12 +579,25 @@ class PipelineRuntime:
             st.backward_weight_mb(a.mb)
 
     # ------------------------------------------------------------------ diagnostics
-    def bubble(self) -> float:
-        """Measured bubble of the last profiled step on this rank: 1 - busy / step time."""
-        if not self.last_timeline or self.last_step_ms <= 0:
+    def busy_ms(self) -> float:
+        """Compute-stream busy time of the last profiled step (sum of action intervals)."""
+        return float(sum(e - s for _, s, e in self.last_timeline))
+
+    def bubble(self, step_ms: Optional[float] = None) -> float:
+        """Measured bubble of the last profiled step on this rank: 1 - busy / step time
+        (``step_ms``: a common step time, e.g. the max over ranks; default: this rank's)."""
+        step = self.last_step_ms if step_ms is None else step_ms
+        if not self.last_timeline or step <= 0:
             return float("nan")
-        busy = sum(e - s for _, s, e in self.last_timeline)
-        return max(0.0, 1.0 - busy / self.last_step_ms)
+        return max(0.0, 1.0 - self.busy_ms() / step)
+
+    def describe(self) -> str:
+        """Diagnostics for a hang report (utils/metrics.Watchdog): transport, tape state and
+        the compute grid of every rank's program."""
+        grid = {r: [e for e in es if isinstance(e, Action)] for r, es in self.program_all.items()}
+        head = (f"pipeline rank {self.rank}/{self.pp}: schedule {self.schedule}, m={self.m}, v={self.v}, "
+                f"p2p={getattr(self.p2p, 'kind', '?')}, native runner: {self.native_reason}, steps run: {self._steps}")
+        return head + "\n" + format_compute_grid(grid)
 
     def _report_failure(self, idx: int) -> None:
         grid = {r: [e for e in es if isinstance(e, Action)] for r, es in self.program_all.items()}

@@ -7,10 +7,11 @@
   also produces *time stamps*, which :mod:`.lower` uses to build a globally
   consistent p2p order.
 * :func:`check_lowered` models the executor on a GPU: per rank one in-order compute
-  stream and one in-order comm stream; a comm group starts after the previous group
-  completed and after every compute issued before it; a message completes when both
-  endpoint groups have started; a compute waits for the groups that carry its
-  inputs.  A fixpoint that does not finish means the lowered program can hang.
+  stream and one in-order comm stream per engine channel (1, or 2 = one per traffic
+  direction); a comm group starts after the previous group of its stream completed and
+  after every compute issued before it; a message completes when both endpoint groups
+  have started; a compute waits for the groups that carry its inputs.  A fixpoint that
+  does not finish means the lowered program can hang.
 """
 from __future__ import annotations
 
@@ -161,92 +162,93 @@ def to_grid(res: SimResult, pp: int) -> Dict[int, List[Optional[Action]]]:
 # ----------------------------------------------------------------------------------------
 
 
-def check_lowered(program: Dict[int, List[Entry]], num_stages: int) -> None:
-    """Raise RuntimeError if the lowered program can hang under RCCL semantics."""
+def message_channel(key: tuple) -> int:
+    """Engine channel of a message: 0 = activations down the pipeline (F, H), 1 =
+    gradients back up (B, D) -- one RCCL communicator + stream each (csrc/comm/rccl_p2p.h)."""
+    return 0 if key[0] in ("F", "H") else 1
+
+
+def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: int = 1) -> None:
+    """Raise RuntimeError if the lowered program can hang under RCCL semantics.
+
+    Model: per rank one in-order compute stream and ``channels`` in-order comm streams
+    (``channels=2``: each CommGroup is split by :func:`message_channel` and every part goes
+    to its direction's stream, as the native engine posts it).  A posted group starts
+    after the previous group of its stream completed and after every compute issued
+    before it; a message completes when both endpoint groups have started; a group
+    completes when all its messages have; a compute waits for the groups carrying its
+    inputs.  A fixpoint that does not finish means the program can hang."""
     comp_orders = {r: [e for e in es if isinstance(e, Action)] for r, es in program.items()}
     split = uses_split_backward(comp_orders)
     head = head_ranks_of(comp_orders)
     ranks = sorted(program)
-    # message key -> (sender group id, receiver group id)
-    msg_groups: Dict[tuple, List[Tuple[int, int]]] = {}
-    groups: Dict[Tuple[int, int], CommGroup] = {}
+    chan = (lambda key: 0) if channels <= 1 else message_channel
+    # posted (sub)groups per rank: (channel, ops, index of the last compute issued before it)
+    posts: Dict[int, List[Tuple[int, List, int]]] = {}
+    comp_list: Dict[int, List[Action]] = {}
     for r in ranks:
-        gi = 0
+        posts[r], comp_list[r] = [], []
         for e in program[r]:
             if isinstance(e, CommGroup):
-                groups[(r, gi)] = e
+                by_ch: Dict[int, List] = {}
                 for op in e.ops:
-                    msg_groups.setdefault(op.key, []).append((r, gi))
-                gi += 1
+                    by_ch.setdefault(chan(op.key), []).append(op)
+                for ch in sorted(by_ch):
+                    posts[r].append((ch, by_ch[ch], len(comp_list[r]) - 1))
+            else:
+                comp_list[r].append(e)
+    msg_groups: Dict[tuple, List[Tuple[int, int]]] = {}
+    recv_group_of: Dict[tuple, Tuple[int, int]] = {}
+    queues: Dict[Tuple[int, int], List[int]] = {}       # (rank, channel) -> post indices in order
+    for r in ranks:
+        for gi, (ch, ops, _) in enumerate(posts[r]):
+            queues.setdefault((r, ch), []).append(gi)
+            for op in ops:
+                msg_groups.setdefault(op.key, []).append((r, gi))
+                if op.action.op.is_recv:
+                    recv_group_of[(r,) + op.key] = (r, gi)
     for k, gs in msg_groups.items():
         if len(gs) != 2:
             raise RuntimeError(f"message {k} has {len(gs)} endpoints (expected send+recv)")
-    # recv-group needed by each compute (by message key of its inputs)
-    entries = {r: program[r] for r in ranks}
+    comp_waits: Dict[Tuple[int, int], List[Tuple[int, int]]] = {}
+    for r in ranks:
+        for ci, a in enumerate(comp_list[r]):
+            comp_waits[(r, ci)] = [recv_group_of[(r,) + key] for _, key in in_messages(a, num_stages, split, head)
+                                   if key is not None and (r,) + key in recv_group_of]
     comp_done: Dict[Tuple[int, int], bool] = {}
     grp_started: Dict[Tuple[int, int], bool] = {}
     grp_done: Dict[Tuple[int, int], bool] = {}
-    # compute index -> set of (rank, group) it must wait on
-    comp_waits: Dict[Tuple[int, int], List[Tuple[int, int]]] = {}
-    # group -> computes issued before it (last compute index)
-    grp_after_comp: Dict[Tuple[int, int], int] = {}
-    comp_list: Dict[int, List[Action]] = {}
-    recv_group_of: Dict[tuple, Tuple[int, int]] = {}
-    for r in ranks:
-        ci, gi = 0, 0
-        comp_list[r] = []
-        for e in entries[r]:
-            if isinstance(e, CommGroup):
-                grp_after_comp[(r, gi)] = ci - 1
-                for op in e.ops:
-                    if op.action.op.is_recv:
-                        recv_group_of[(r,) + op.key] = (r, gi)
-                gi += 1
-            else:
-                comp_list[r].append(e)
-                ci += 1
-    for r in ranks:
-        for ci, a in enumerate(comp_list[r]):
-            waits = []
-            for _, key in in_messages(a, num_stages, split, head):
-                if key is not None and (r,) + key in recv_group_of:
-                    waits.append(recv_group_of[(r,) + key])
-            comp_waits[(r, ci)] = waits
-    ncomp = {r: len(comp_list[r]) for r in ranks}
-    ngrp = {r: sum(1 for e in entries[r] if isinstance(e, CommGroup)) for r in ranks}
     cptr = {r: 0 for r in ranks}
-    gptr = {r: 0 for r in ranks}
+    qptr = {q: 0 for q in queues}
+    ncomp = {r: len(comp_list[r]) for r in ranks}
     changed = True
     while changed:
         changed = False
         for r in ranks:
-            # compute stream
             while cptr[r] < ncomp[r] and all(grp_done.get(g, False) for g in comp_waits[(r, cptr[r])]):
                 comp_done[(r, cptr[r])] = True
                 cptr[r] += 1
                 changed = True
-            # comm stream: start next group
-            g = gptr[r]
-            if g < ngrp[r] and (r, g) not in grp_started:
-                prev_ok = g == 0 or grp_done.get((r, g - 1), False)
-                last_c = grp_after_comp[(r, g)]
-                if prev_ok and (last_c < 0 or comp_done.get((r, last_c), False)):
-                    grp_started[(r, g)] = True
-                    changed = True
-        # group completion
-        for (r, g), grp in groups.items():
-            if grp_done.get((r, g)) or not grp_started.get((r, g)):
+        for q, lst in queues.items():
+            r = q[0]
+            # retire completed heads, then start the next group if its computes are done
+            while qptr[q] < len(lst) and grp_done.get((r, lst[qptr[q]]), False):
+                qptr[q] += 1
+                changed = True
+            if qptr[q] < len(lst):
+                gi = lst[qptr[q]]
+                if (r, gi) not in grp_started:
+                    last_c = posts[r][gi][2]
+                    if last_c < 0 or comp_done.get((r, last_c), False):
+                        grp_started[(r, gi)] = True
+                        changed = True
+        for (r, gi) in list(grp_started):
+            if grp_done.get((r, gi)):
                 continue
-            if all(all(grp_started.get(x, False) for x in msg_groups[op.key]) for op in grp.ops):
-                grp_done[(r, g)] = True
-                if gptr[r] == g:
-                    gptr[r] += 1
+            if all(all(grp_started.get(x, False) for x in msg_groups[op.key]) for op in posts[r][gi][1]):
+                grp_done[(r, gi)] = True
                 changed = True
-        for r in ranks:
-            while gptr[r] < ngrp[r] and grp_done.get((r, gptr[r]), False):
-                gptr[r] += 1
-                changed = True
-    stuck = {r: (cptr[r], ncomp[r], gptr[r], ngrp[r]) for r in ranks if cptr[r] < ncomp[r] or gptr[r] < ngrp[r]}
+    stuck = {r for r in ranks if cptr[r] < ncomp[r]} | {q[0] for q, lst in queues.items() if qptr[q] < len(lst)}
     if stuck:
-        detail = {r: (str(comp_list[r][cptr[r]]) if cptr[r] < ncomp[r] else "-") for r in stuck}
-        raise RuntimeError(f"lowered schedule can deadlock; stuck computes: {detail}")
+        detail = {r: (str(comp_list[r][cptr[r]]) if cptr[r] < ncomp[r] else "-") for r in sorted(stuck)}
+        raise RuntimeError(f"lowered schedule can deadlock ({channels} comm channel(s)); stuck computes: {detail}")

@@ -74,6 +74,11 @@ class StageBase:
         async work handle (DP all-reduce) that the runtime waits for at step end."""
         return None
 
+    def has_grad_reduction(self, scaled_in_loss: bool) -> bool:
+        """Whether ``reduce_grad`` issues any work (a recorded native tape skips the CALL
+        otherwise).  Conservative default: yes."""
+        return True
+
     def clear_runtime_states(self) -> None:
         pass
 

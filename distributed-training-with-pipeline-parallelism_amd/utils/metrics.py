@@ -60,6 +60,7 @@ class Watchdog:
         self.describe = describe
         self.exit_code = exit_code
         self._deadline: Optional[float] = None
+        self._limit = timeout_s
         self._lock = threading.Lock()
         self._stop = False
         self._thread = None
@@ -69,12 +70,12 @@ class Watchdog:
 
     def _run(self):
         while not self._stop:
-            time.sleep(min(1.0, self.timeout_s / 4))
+            time.sleep(min(1.0, max(0.05, self.timeout_s / 4)))
             with self._lock:
                 dl = self._deadline
             if dl is not None and time.monotonic() > dl:
                 rank = os.environ.get("RANK", "0")
-                sys.stderr.write(f"[mipipe watchdog] rank {rank}: step exceeded {self.timeout_s:.0f}s -- aborting\n")
+                sys.stderr.write(f"[mipipe watchdog] rank {rank}: step exceeded {self._limit:.0f}s -- aborting\n")
                 if self.describe is not None:
                     try:
                         sys.stderr.write(self.describe() + "\n")
@@ -84,13 +85,16 @@ class Watchdog:
                 sys.stderr.flush()
                 os._exit(self.exit_code)
 
-    def step(self):
+    def step(self, timeout_s: Optional[float] = None):
+        """Arm the watchdog for one phase (``timeout_s`` overrides the default limit)."""
         wd = self
+        limit = wd.timeout_s if timeout_s is None else float(timeout_s)
 
         class _Ctx:
             def __enter__(self_):
                 with wd._lock:
-                    wd._deadline = time.monotonic() + wd.timeout_s if wd._thread else None
+                    wd._deadline = time.monotonic() + limit if wd._thread else None
+                    wd._limit = limit
                 return self_
 
             def __exit__(self_, *exc):

@@ -1,0 +1,44 @@
+"""bench.py hang safety on CPU/gloo (2 ranks, tiny GPT-2): a rank that stops answering
+must end the run non-zero with the program grid printed (watchdog), and a stall confined
+to the first attempt must be retried by the supervisor into a valid JSON line
+(the reference's launcher joins with no timeout, nb:324-325)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from dist_utils import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ARGS = ["--model", "gpt2-tiny", "--vocab", "256", "--mbs", "1", "--seq", "32", "--steps", "3", "--warmup", "1",
+        "--step-timeout", "4"]
+
+
+def _bench(extra, stall, timeout=240):
+    env = dict(os.environ, MIPIPE_FAULT_STALL=stall, OMP_NUM_THREADS="1", MIPIPE_BENCH_ATTEMPT_S="90")
+    env.pop("WORLD_SIZE", None)
+    env.pop("RANK", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py")] + ARGS + extra
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd="/tmp")
+
+
+def test_stalled_rank_exits_nonzero_with_grid():
+    r = _bench(["--max-attempts", "1"], "1:2")
+    assert r.returncode != 0
+    assert "[mipipe watchdog]" in r.stderr
+    assert "Rank 0" in r.stderr and "Rank 1" in r.stderr and "Step 00:" in r.stderr   # the program grid
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_supervisor_retries_a_stalled_attempt():
+    r = _bench([], "1:2:0")     # only attempt 0 stalls
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    assert out["attempt"] == 1 and out["n_gpus"] == 2 and out["value"] > 0
+    assert out["config"]["parallelism"] == "pp2"
+    assert "attempt 0" in r.stderr

@@ -16,22 +16,30 @@ CFG = dict(gpt2=lambda: NativeConfig.gpt2("tiny", vocab_size=100, d_model=64, n_
 M, MBS, S = 4, 2, 16
 
 
-def _data(cfg, dp_rank=0):
-    g = torch.Generator().manual_seed(7 + dp_rank)
+def _data(cfg, dp_rank=0, step=0):
+    g = torch.Generator().manual_seed(7 + dp_rank + 100 * step)
     return (torch.randint(0, cfg.vocab_size, (M * MBS, S), generator=g),
             torch.randint(0, cfg.vocab_size, (M * MBS, S), generator=g))
 
 
-def _train(name, pp, dp, schedule, steps=2, split_head=None, layer_ranges="auto"):
+def _train(name, pp, dp, schedule, steps=2, split_head=None, layer_ranges="auto", max_grad_norm=1.0,
+           concat_dp=1, adam_eps=1e-8, lr=1e-3):
+    """concat_dp=k (PP=1, DP=1 only): train on the concatenation of k DP replicas' batches
+    (k*M microbatches) -- the single-process oracle of a DP=k run."""
     cfg = CFG[name]()
     if layer_ranges == "auto":
         layer_ranges = [(0, 2), (2, 4)] if pp == 2 else None
-    tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=schedule, n_microbatches=M, mbs=MBS, seq_len=S,
-                         device=torch.device("cpu"), dtype=torch.float32, lr=1e-3,
-                         layer_ranges=layer_ranges, split_head=split_head, head_align=8)
+    tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=schedule, n_microbatches=M * concat_dp, mbs=MBS, seq_len=S,
+                         device=torch.device("cpu"), dtype=torch.float32, lr=lr,
+                         layer_ranges=layer_ranges, split_head=split_head, head_align=8,
+                         max_grad_norm=max_grad_norm, adam_eps=adam_eps)
     losses = []
-    for _ in range(steps):
-        x, y = _data(cfg, tr.mesh.dp_rank)
+    for step in range(steps):
+        if concat_dp > 1:
+            parts = [_data(cfg, d, step) for d in range(concat_dp)]
+            x, y = torch.cat([p[0] for p in parts]), torch.cat([p[1] for p in parts])
+        else:
+            x, y = _data(cfg, tr.mesh.dp_rank, step)
         l = tr.train_step(x, y)
         if l is not None:
             losses.append(float(l))
@@ -39,8 +47,42 @@ def _train(name, pp, dp, schedule, steps=2, split_head=None, layer_ranges="auto"
     return dict(losses=losses, sd=sd)
 
 
-def _worker(rank, world, name, pp, dp, schedule, split_head=None, layer_ranges="auto"):
-    return _train(name, pp, dp, schedule, split_head=split_head, layer_ranges=layer_ranges)
+def _worker(rank, world, name, pp, dp, schedule, split_head=None, layer_ranges="auto", max_grad_norm=1.0,
+            adam_eps=1e-8, lr=1e-3):
+    return _train(name, pp, dp, schedule, split_head=split_head, layer_ranges=layer_ranges,
+                  max_grad_norm=max_grad_norm, adam_eps=adam_eps, lr=lr)
+
+
+@pytest.mark.parametrize("name,split_head", [("gpt2", True), ("gpt2", False), ("llama", True)])
+def test_dp2_pp2_matches_pp1_on_concatenated_batch_with_clipping(name, split_head):
+    """DP=2 x PP=2 must equal one process training on both replicas' batches, with the
+    grad-norm clip active (max_grad_norm 0.05): pins the 1/dp gradient scale of every
+    arena -- including the replicated distributed head, all-reduced over pipeline x DP --
+    and a tied embedding counted once in the global norm.  Adam eps = 1, lr = 1 makes the
+    update ~ the clipped gradient itself (Adam is otherwise blind to a gradient's scale)."""
+    ref = _train(name, 1, 1, "1F1B", max_grad_norm=0.05, concat_dp=2, adam_eps=1.0, lr=1.0)
+    res = run_world(_worker, 4, name, 2, 2, "1F1B", split_head, "auto", 0.05, 1.0, 1.0)
+    last = 1  # pipeline rank 1 of replica 0 holds the loss (every rank with a split head)
+    # per-replica losses average to the concatenated-batch loss
+    l0, l1 = res[last]["losses"], res[2 + last]["losses"]
+    assert [(a + b) / 2 for a, b in zip(l0, l1)] == pytest.approx(ref["losses"], rel=1e-5)
+    for r in res.values():
+        for k, v in r["sd"].items():
+            torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref["sd"][k]), atol=1e-4, rtol=1e-4,
+                                       msg=lambda m: f"{k}: {m}")
+
+
+@pytest.mark.parametrize("name", ["gpt2", "llama"])
+def test_pp2_matches_pp1_with_active_clipping(name):
+    """Clip active (0.05): the tied embedding's two copies (first and last stage) must
+    count once in the global grad norm (Adam eps = 1, lr = 1: scale-sensitive updates)."""
+    ref = _train(name, 1, 1, "1F1B", max_grad_norm=0.05, adam_eps=1.0, lr=1.0)
+    res = run_world(_worker, 2, name, 2, 1, "1F1B", False, "auto", 0.05, 1.0, 1.0)
+    assert res[1]["losses"] == pytest.approx(ref["losses"], rel=1e-5)
+    for r in res.values():
+        for k, v in r["sd"].items():
+            torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(ref["sd"][k]), atol=1e-4, rtol=1e-4,
+                                       msg=lambda m: f"{k}: {m}")
 
 
 @pytest.mark.parametrize("name", ["gpt2", "llama"])

@@ -326,16 +326,20 @@ def test_native_rccl_engine_self_transfer():
     from mipipe.parallel.comm import load_native_rccl
     ext = _k.load_ext()
     load_native_rccl(ext)
-    eng = ext.RcclP2P(ext.RcclP2P.unique_id(), 1, 0, torch.cuda.current_device())
+    eng = ext.RcclP2P(ext.RcclP2P.unique_id() + ext.RcclP2P.unique_id(), 1, 0, torch.cuda.current_device())
+    assert eng.channels == 2 and eng.stream_handle(0) != eng.stream_handle(1)
     src = torch.randn(1 << 20, device=DEV).to(torch.bfloat16)
     dst = torch.empty_like(src)
     src2 = torch.arange(1000, device=DEV, dtype=torch.int64)
     dst2 = torch.zeros_like(src2)
-    h = eng.post([(src, 0), (src2, 0)], [(dst, 0), (dst2, 0)])
+    h = eng.post(0, [(src, 0)], [(dst, 0)])          # channel 0 (activations)
+    h2 = eng.post(1, [(src2, 0)], [(dst2, 0)])       # channel 1 (gradients)
     eng.wait(h)
+    eng.wait(h2)
     torch.cuda.synchronize()
     assert torch.equal(dst, src) and torch.equal(dst2, src2)
-    assert eng.query(h)
+    assert eng.query(h) and eng.query(h2)
+    assert eng.async_error() == ""
     eng.close()
     with open("/proc/self/maps") as f:
         libs = {line.split()[-1] for line in f if "librccl" in line}

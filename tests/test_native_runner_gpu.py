@@ -70,3 +70,60 @@ def test_native_runner_virtual_stages_on_one_rank():
     _, l_python = _train(cfg, False, schedule="Interleaved1F1B", v=2)
     assert tr_n.runtime.native_runner is not None, tr_n.runtime.native_reason
     assert l_native == pytest.approx(l_python, rel=5e-4)
+
+
+def test_profiled_step_is_measured_on_the_tape():
+    """The bubble measurement replays the same native tape with timing events around
+    every graph: at PP=1 (no pipeline) the compute stream is busy the whole step."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    tr, _ = _train(CFGS["gpt2"], True, steps=4)
+    runs = tr.runtime.native_runner.runs
+    tr.runtime.profile = True
+    g = torch.Generator(device="cuda").manual_seed(7)
+    x = torch.randint(0, 1000, (8, 128), device="cuda", generator=g)
+    tr.train_step(x, x)
+    tr.runtime.profile = False
+    assert tr.runtime.native_runner.runs == runs + 1
+    assert tr.runtime.last_timeline_source == "native tape"
+    tl = tr.runtime.last_timeline
+    assert len(tl) == sum(1 for k in tr.runtime.native_runner.kinds() if k == 0)
+    assert all(e >= s >= 0 for _, s, e in tl)
+    assert {n[1:2] for n, _, _ in tl} >= {"F", "B"}
+    assert 0.0 <= tr.runtime.bubble() < 0.05, (tr.runtime.bubble(), tr.runtime.last_step_ms)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_wgrad_side_stream_matches_inline(graphs, monkeypatch):
+    """dW GEMMs on the private side stream (default) vs inline on the compute stream: the
+    gradients must agree (tied embedding: the fork joins before the embedding backward)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import mipipe.models.native as N
+
+    def grads(side):
+        monkeypatch.setattr(N, "_WGRAD_STREAM", side)
+        dev = torch.device("cuda", 0)
+        tr = PipelineTrainer(CFGS["gpt2"], pp=1, n_microbatches=2, mbs=4, seq_len=128, device=dev, seed=3,
+                             graphs=graphs)
+        gen = torch.Generator(device="cuda").manual_seed(5)
+        x = torch.randint(0, 1000, (8, 128), device=dev, generator=gen)
+        y = torch.randint(0, 1000, (8, 128), device=dev, generator=gen)
+        if graphs:
+            tr.capture_graphs(x, y)
+        for a in tr.optimizer.arenas:
+            a.grad.zero_()
+        tr.runtime.step([(c,) for c in torch.tensor_split(x, 2)], list(torch.tensor_split(y, 2)), [],
+                        return_outputs=False)
+        torch.cuda.synchronize()
+        side_streams = set(N._WGRAD_SIDE.values())
+        return [a.grad.clone() for a in tr.optimizer.arenas], side_streams
+
+    g_side, streams = grads(True)
+    g_inline, _ = grads(False)
+    for s in streams:
+        assert s.cuda_stream != torch.cuda.current_stream().cuda_stream
+    for a, b in zip(g_side, g_inline):
+        assert torch.isfinite(a).all()
+        err = (a - b).norm() / b.norm().clamp_min(1e-12)
+        assert err < 1e-5, float(err)

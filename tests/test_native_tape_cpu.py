@@ -1,0 +1,252 @@
+"""The native stage runner's tape at PP=4, on CPU/gloo with stand-ins for the GPU parts.
+
+On a GPU a step after graph capture is recorded into ``StageRunner``
+(csrc/runtime/stage_runner.cpp) as GRAPH / COPY / POST / WAIT / CALL instructions and
+replayed from C++.  Multi-rank RCCL cannot run on a one-GPU box, so this test swaps in:
+
+* ``FakeGraphCache`` -- "captures" an action by running it and replays it by re-running it
+  into the same persistent output tensors (what a HIP graph replay does);
+* ``FakeEngine`` -- the native RCCL engine's interface (two channels, post/wait), moving
+  data over one gloo group per channel;
+* ``FakeRunner`` -- ``StageRunner``'s interface; ``run()`` replays the tape in Python.
+
+It checks that a recorded PP=4 step holds only GRAPH/COPY/POST/WAIT plus CALLs for the
+collectives (the distributed head's gradient all-reduce, DP all-reduces), that both
+channels carry POSTs, and that replaying the tape trains exactly like the Python executor.
+"""
+import types
+
+import pytest
+import torch
+import torch.distributed as dist
+
+import mipipe  # noqa: F401
+from mipipe.engine import PipelineTrainer
+from mipipe.models.config import NativeConfig
+from mipipe.parallel import native_runner
+from mipipe.parallel.graphs import GraphCache
+from mipipe.parallel.runtime import PipelineRuntime
+
+from dist_utils import run_world
+
+GRAPH, COPY, POST, WAIT, CALL = range(5)
+
+
+def _nested_copy(dst, src):
+    if isinstance(dst, torch.Tensor):
+        dst.copy_(src)
+    elif isinstance(dst, (tuple, list)):
+        for d, s_ in zip(dst, src):
+            _nested_copy(d, s_)
+
+
+class FakeGraph:
+    reg = {}
+
+    def __init__(self, fn, static_in, out):
+        self.fn, self.static_in, self.out = fn, static_in, out
+        FakeGraph.reg[id(self)] = self
+
+    def raw_cuda_graph_exec(self):
+        return id(self)
+
+    def replay(self):
+        _nested_copy(self.out, self.fn(self.static_in))
+
+
+class FakeGraphCache(GraphCache):
+    def run(self, key, inputs, fn, keep=None):
+        rec = native_runner.active()
+        entry = self.graphs.get(key)
+        if entry is None:
+            if rec is not None:
+                rec.invalidate("capture during recording")
+            static_in = list(inputs)
+            out = fn(static_in)
+            g = FakeGraph(fn, static_in, out)
+            self.graphs[key] = entry = (g, static_in, out, [])
+            self.captures += 1
+            if rec is not None:
+                rec.graph(g, self.label(key))
+            return out
+        g, static_in, out, _ = entry
+        for s_, t in zip(static_in, inputs):
+            if s_.data_ptr() != t.data_ptr():
+                s_.copy_(t)
+                if rec is not None:
+                    rec.copy(s_, t)
+        self.replays += 1
+        g.replay()
+        if rec is not None:
+            rec.graph(g, self.label(key))
+        return out
+
+
+class FakeEngine:
+    """Native engine stand-in: channel c -> its own gloo group (independent matching)."""
+
+    def __init__(self, groups, ranks):
+        self.groups, self.ranks, self.channels = groups, ranks, len(groups)
+        self.reg, self.pending, self.next = {}, {}, 1
+        self.posts = [0] * len(groups)
+
+    def post(self, ch, sends, recvs):
+        ops = []
+        for t, p in sends:
+            self.reg[t.data_ptr()] = t
+            ops.append(dist.P2POp(dist.isend, t, self.ranks[p], self.groups[ch]))
+        for t, p in recvs:
+            self.reg[t.data_ptr()] = t
+            ops.append(dist.P2POp(dist.irecv, t, self.ranks[p], self.groups[ch]))
+        h = self.next
+        self.next += 1
+        self.pending[h] = dist.batch_isend_irecv(ops) if ops else []
+        self.posts[ch] += 1
+        return h
+
+    def wait(self, h):
+        for w in self.pending.pop(h, []):
+            w.wait()
+
+    def query(self, h):
+        return True
+
+    def abort(self):
+        pass
+
+
+class FakeRunner:
+    def __init__(self, device):
+        self.tape, self.nslots, self.runs = [], 0, 0
+
+    def add_graph(self, g, label=""):
+        self.tape.append((GRAPH, FakeGraph.reg[g]))
+
+    def add_copy_t(self, dst, src):
+        self.tape.append((COPY, (dst, src)))
+
+    def add_post(self, engine, ch, sends, recvs):
+        res = lambda lst: [(engine.reg[ptr], peer) for ptr, n, code, peer in lst]
+        self.tape.append((POST, (engine, ch, res(sends), res(recvs), self.nslots)))
+        self.nslots += 1
+        return self.nslots - 1
+
+    def add_wait(self, slot):
+        self.tape.append((WAIT, slot))
+
+    def add_call(self, fn):
+        self.tape.append((CALL, fn))
+
+    @property
+    def size(self):
+        return len(self.tape)
+
+    def kinds(self):
+        return [k for k, _ in self.tape]
+
+    def channels(self):
+        return [x[1] for k, x in self.tape if k == POST]
+
+    def set_profile(self, on):
+        pass
+
+    def run(self):
+        handles = {}
+        for k, x in self.tape:
+            if k == GRAPH:
+                x.replay()
+            elif k == COPY:
+                x[0].copy_(x[1])
+            elif k == POST:
+                eng, ch, s_, r_, slot = x
+                handles[slot] = (eng, eng.post(ch, s_, r_))
+            elif k == WAIT:
+                eng, h = handles.pop(x)
+                eng.wait(h)
+            else:
+                x()
+        for eng, h in handles.values():
+            eng.wait(h)
+        self.runs += 1
+
+
+def _patch(monkeypatch_like):
+    """Route the recorder to the fakes (runs inside each spawned rank)."""
+    import mipipe.ops.kernels as K
+    K.load_ext = lambda: types.SimpleNamespace(StageRunner=FakeRunner)
+    native_runner.TapeRecorder.copy = lambda self, dst, src: self.runner.add_copy_t(dst, src)
+
+    def possible(self, return_outputs):
+        if not self.native_enabled or return_outputs or self.deps is not None:
+            return False
+        if any(getattr(st, "graphs", None) is None for st in self.stages.values()):
+            return False
+        if self.head is not None and self.head.graphs is None:
+            return False
+        return self._steps >= 2 and all(getattr(st, "step_id", 0) >= 2 for st in self.stages.values())
+    PipelineRuntime._native_possible = possible
+
+
+CFG = lambda: NativeConfig.gpt2("tiny", vocab_size=96, d_model=64, n_layers=8, n_heads=4, d_ff=128, max_seq_len=16,
+                                dropout=0.0)
+M, MBS, S = 8, 2, 16
+
+
+def _worker(rank, world, pp, dp, schedule, v, native, steps):
+    torch.manual_seed(0)
+    if native:
+        _patch(None)
+    cfg = CFG()
+    tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=schedule, n_microbatches=M, mbs=MBS, seq_len=S, v=v,
+                         device=torch.device("cpu"), dtype=torch.float32, lr=1e-3, head_align=8)
+    eng = None
+    if native:
+        ranks = tr.mesh.pipe_ranks
+        groups = []
+        for d in range(dp):      # every rank creates every group, in the same order
+            rr = [d * pp + i for i in range(pp)]
+            gs = [dist.new_group(rr, backend="gloo") for _ in range(2)]
+            if d == tr.mesh.dp_rank:
+                groups = gs
+        eng = FakeEngine(groups, ranks)
+        tr.runtime.p2p.engine = eng
+        tr.runtime.p2p.channels = 2
+        for st in tr.stages:
+            st.graphs = FakeGraphCache(str(st.stage_index))
+        if tr.runtime.head is not None:
+            tr.runtime.head.graphs = FakeGraphCache(str(tr.mesh.pp_rank))
+    g = torch.Generator().manual_seed(11 + tr.mesh.dp_rank)
+    x = torch.randint(0, cfg.vocab_size, (M * MBS, S), generator=g)
+    y = torch.randint(0, cfg.vocab_size, (M * MBS, S), generator=g)
+    losses = [float(tr.train_step(x, y)) for _ in range(steps)]
+    out = dict(losses=losses, sd={k: v.numpy().copy() for k, v in tr.state_dict().items()})
+    r = tr.runtime.native_runner
+    if native:
+        out.update(recorded=r is not None, kinds=r.kinds() if r else [], channels=r.channels() if r else [],
+                   runs=r.runs if r else 0, reason=tr.runtime.native_reason,
+                   n_reduce_grad_calls=sum(1 for st in tr.stages if st.has_grad_reduction(True)),
+                   head=tr.runtime.head_reduce is not None)
+    return out
+
+
+@pytest.mark.parametrize("schedule,v,dp", [("1F1B", 1, 1), ("Interleaved1F1B", 2, 1), ("1F1B", 1, 2)])
+def test_pp4_tape_is_native_and_replays_exactly(schedule, v, dp):
+    world = 4 * dp
+    ref = run_world(_worker, world, 4, dp, schedule, v, False, 5)
+    res = run_world(_worker, world, 4, dp, schedule, v, True, 5)
+    for r in range(world):
+        o = res[r]
+        assert o["recorded"], o["reason"]
+        assert o["runs"] == 2                   # steps 4 and 5 replayed from the tape
+        kinds = o["kinds"]
+        assert set(kinds) <= {GRAPH, COPY, POST, WAIT, CALL}
+        assert kinds.count(POST) > 0 and kinds.count(GRAPH) > 0
+        # CALLs only for collectives (an issue + a stream-wait each): the head-gradient
+        # all-reduce and the per-stage DP all-reduces
+        assert kinds.count(CALL) == 2 * (int(o["head"]) + o["n_reduce_grad_calls"]), kinds
+        # both directions use their own channel
+        assert set(o["channels"]) == {0, 1}
+        assert o["losses"] == pytest.approx(ref[r]["losses"], rel=1e-6, abs=1e-6)
+        for k, w in o["sd"].items():
+            torch.testing.assert_close(torch.from_numpy(w), torch.from_numpy(ref[r]["sd"][k]), atol=1e-6,
+                                       rtol=1e-6)

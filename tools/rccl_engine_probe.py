@@ -31,13 +31,13 @@ say("loaded")
 torch.cuda.init()
 dev = torch.cuda.current_device()
 say("device", dev)
-uid = ext.RcclP2P.unique_id()
+uid = ext.RcclP2P.unique_id() + ext.RcclP2P.unique_id()
 say("uid", len(uid))
 eng = ext.RcclP2P(uid, 1, 0, dev)
 say("comm up")
 src = torch.randn(1 << 20, device="cuda").to(torch.bfloat16)
 dst = torch.empty_like(src)
-h = eng.post([(src, 0)], [(dst, 0)])
+h = eng.post(0, [(src, 0)], [(dst, 0)])
 say("posted", h)
 eng.wait(h)
 torch.cuda.synchronize()
