@@ -16,9 +16,11 @@
   free port per run instead of the reference's fixed 29500 + unbounded join
   (SURVEY §2.8 item 11).
 
-``engine='native'`` runs the same reference architecture on the MI355X HIP path
-(explicit backward, hand-written kernels); ``engine='torch'`` is the nn.Module /
-autograd path the reference uses.
+``engine='native'`` (the default whenever a GPU is present) runs the same reference
+architecture on the MI355X HIP path (explicit backward, hand-written kernels) and its
+last rank's ``step()`` returns the merged ``[B, S, vocab]`` logits like the reference's;
+``engine='torch'`` is the nn.Module / autograd path the reference uses (the CPU default).
+Every metrics dict also carries the measured and analytic pipeline bubble.
 """
 from __future__ import annotations
 
@@ -41,7 +43,11 @@ def _sync(device) -> None:
 
 
 def run_train_iterations(schedule, x: torch.Tensor, y: torch.Tensor, rank: int, world_size: int,
-                         num_iterations: int = 10, warmup: int = 2, device=None) -> Dict[str, float]:
+                         num_iterations: int = 10, warmup: int = 2, device=None,
+                         measure_bubble: bool = True) -> Dict[str, float]:
+    """Reference timed loop (helper:98-143) + one extra profiled step (untimed) for the
+    measured pipeline bubble ``1 - sum(busy_r) / (P * max step_r)`` over the schedule's
+    group, reported with the analytic (P-1)/(v*m+P-1) of the same schedule."""
     total_toks = x.shape[0] * x.shape[1] * num_iterations
     first = rank == 0
     last = rank == world_size - 1
@@ -65,7 +71,29 @@ def run_train_iterations(schedule, x: torch.Tensor, y: torch.Tensor, rank: int, 
         one()
     _sync(dev)
     elapsed = time.time() - start_t
-    return {"elapsed_time": elapsed, "throughput": total_toks / elapsed, "tokens_processed": total_toks}
+    out = {"elapsed_time": elapsed, "throughput": total_toks / elapsed, "tokens_processed": total_toks}
+    rt = getattr(schedule, "runtime", None)
+    if measure_bubble and rt is not None:
+        from ..parallel.schedules import analytic_bubble
+        if dist.is_initialized() and world_size > 1:
+            dist.barrier()
+        rt.profile = True
+        try:
+            one()
+        finally:
+            rt.profile = False
+        mine = torch.tensor([rt.busy_ms(), rt.last_step_ms], dtype=torch.float64)
+        if dist.is_initialized() and world_size > 1:
+            t = mine.to(dev) if dist.get_backend() == "nccl" else mine
+            allv = [torch.zeros_like(t) for _ in range(world_size)]
+            dist.all_gather(allv, t)
+            allv = [v.cpu() for v in allv]
+        else:
+            allv = [mine]
+        step = max(float(v[1]) for v in allv)
+        out["bubble_fraction"] = (1.0 - sum(float(v[0]) for v in allv) / (len(allv) * step)) if step > 0 else None
+        out["analytic_bubble"] = analytic_bubble(rt.schedule, rt.pp, rt.m, rt.v)
+    return out
 
 
 def stages_per_worker(schedule_type: str, n_layers: int, world_size: int) -> int:
@@ -75,7 +103,12 @@ def stages_per_worker(schedule_type: str, n_layers: int, world_size: int) -> int
 
 def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_size, seq_length, num_iterations,
                    results_queue, num_microbatches: int = 4, device: Optional[str] = None, port: int = 29500,
-                   engine: str = "torch", dropout: float = 0.1, seed: Optional[int] = None):
+                   engine: str = "auto", dropout: float = 0.1, seed: Optional[int] = None):
+    """Reference worker (helper:150-235).  ``engine='auto'`` (default): the MI355X HIP path
+    (``native``: hand-written kernels, explicit backward) when a GPU is present, the
+    reference's nn.Module / autograd path (``torch``) on CPU.  ``MIPIPE_DIST_BACKEND=gloo``
+    with GPUs: ranks share the visible devices and gloo carries the traffic (a test mode
+    for one-GPU boxes)."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -83,7 +116,13 @@ def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_siz
         os.environ["LOCAL_RANK"] = str(rank)
         os.environ["WORLD_SIZE"] = str(world_size)
         use_gpu = (device == "cuda") or (device is None and torch.cuda.is_available())
-        if use_gpu:
+        if engine == "auto":
+            engine = "native" if use_gpu else "torch"
+        if use_gpu and os.environ.get("MIPIPE_DIST_BACKEND") == "gloo":
+            dev = torch.device("cuda", rank % torch.cuda.device_count())
+            torch.cuda.set_device(dev)
+            dist.init_process_group(backend="gloo", rank=rank, world_size=world_size)
+        elif use_gpu:
             torch.cuda.set_device(rank)
             dev = torch.device("cuda", rank)
             dist.init_process_group(backend="nccl", rank=rank, world_size=world_size, device_id=dev)
@@ -165,7 +204,9 @@ def run_all_experiments(n_heads_list=(4, 8, 12), n_layers_list=(4, 8, 12), num_p
                         if "error" not in m:
                             rows.append(dict(n_layers=n_layers, n_heads=n_heads, num_processes=P, schedule=sched,
                                              throughput=m["throughput"], elapsed_time=m["elapsed_time"],
-                                             tokens_processed=m["tokens_processed"]))
+                                             tokens_processed=m["tokens_processed"],
+                                             bubble_fraction=m.get("bubble_fraction"),
+                                             analytic_bubble=m.get("analytic_bubble")))
                             print(f"L{n_layers} H{n_heads} P{P} {sched}: {m['throughput']:.1f} tok/s")
                         else:
                             print(f"L{n_layers} H{n_heads} P{P} {sched}: error {m['error']}")

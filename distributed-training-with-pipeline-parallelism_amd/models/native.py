@@ -751,9 +751,11 @@ class NativeModel:
 
     # ------------------------------------------------------------------ forward
     def forward(self, x: torch.Tensor, ctx: MBContext, B: int, S: int, target: Optional[torch.Tensor] = None,
-                loss_scale: float = 1.0):
+                loss_scale: float = 1.0, keep_logits: bool = False):
         """x: tokens [B,S] (stage 0) or hidden [B*S, D].  Last stage: returns the mean
-        loss (f32 scalar tensor) and keeps dlogits for the backward."""
+        loss (f32 scalar tensor) and keeps dlogits for the backward (the fused CE writes
+        the gradient over the logits; ``keep_logits`` saves a copy first, in
+        ``ctx.misc['logits_out']``, for callers that want the outputs too)."""
         cfg = self.cfg
         if self.first:
             tokens = x.reshape(-1)
@@ -782,6 +784,8 @@ class NativeModel:
         if target is None:
             ctx.misc.update(hn=hn, logits=logits)
             return logits
+        if keep_logits:
+            ctx.misc["logits_out"] = logits.clone()
         row_loss = ops.xent_fwd_bwd(logits, target.reshape(-1), cfg.vocab_size, grad_scale=loss_scale / T)
         ctx.misc.update(hn=hn, dlogits=logits)
         return row_loss.mean()

@@ -55,6 +55,7 @@ class NativeStage(StageBase):
         if graphs and model.device.type != "cuda":
             graphs = False
         self.graphs = GraphCache(str(self.stage_index)) if graphs else None
+        self.want_outputs = False   # set per step by the runtime (step(return_outputs=...))
         self._gctx = {}
 
     def _graphed(self) -> bool:
@@ -71,20 +72,31 @@ class NativeStage(StageBase):
             ops.set_dropout_step(self.step_id, self.model.device)
 
     def forward_mb(self, mb, args, target, loss_fn, loss_scale):
-        if self._graphed():
+        # compat step(return_outputs=True) on the last stage: also hand back the logits
+        want_logits = self.is_last and not self.split_head and self.want_outputs and target is not None
+        if self._graphed() and not want_logits:
             return self._forward_graphed(mb, args, target, loss_scale)
         # on the GPU the step enters through the device counter (set_dropout_step), so
         # eager and graph-replayed steps draw identical masks; the CPU ops see the seed only
         ctx = MBContext(mb, _seed(self.seed, 0 if self.model.device.type == "cuda" else self.step_id, mb))
         x = args[0]
         out = self.model.forward(x, ctx, self.mbs, self.S, target=target if self.is_last else None,
-                                 loss_scale=loss_scale)
+                                 loss_scale=loss_scale, keep_logits=want_logits)
         self._ctx[mb] = ctx
         if self.is_last and not self.split_head:
             if target is None:
-                return (out,), None
+                return (self._logits_view(out),), None
+            if want_logits:
+                # merged by the schedule into [B, S, vocab] like the reference's last-rank
+                # step() return value (helper:128, schedules.py:646-652)
+                return (self._logits_view(ctx.misc.pop("logits_out")),), out
             return (out.detach(),), out
         return (out,), None
+
+    def _logits_view(self, logits):
+        """[T, vocab_padded] -> [mbs, S, vocab] (the reference's output shape)."""
+        V = self.cfg.vocab_size
+        return logits[:, :V].reshape(self.mbs, self.S, V)
 
     def _dy(self, grad_outputs):
         if (self.is_last and not self.split_head) or not grad_outputs:
@@ -164,12 +176,16 @@ class NativeStage(StageBase):
 
 
 def build_reference_stage(args, stage_index: int, num_stages: int, device, mbs: int = 8, seq_len: int = 128,
-                          seed: int = 0) -> NativeStage:
-    """Reference architecture (helper:23-55) on the HIP path with the reference split rule."""
+                          seed: int = 0, dtype=None) -> NativeStage:
+    """Reference architecture (helper:23-55) on the HIP path with the reference split rule.
+    ``dtype`` default: bf16 on GPUs (the HIP kernels), f32 on CPU (the reference's own
+    precision, so CPU runs are numerically the reference module)."""
+    if dtype is None:
+        dtype = torch.bfloat16 if torch.device(device).type == "cuda" else torch.float32
     cfg = NativeConfig.reference(n_layers=args.n_layers, n_heads=args.n_heads, dim=args.dim,
                                  vocab_size=args.vocab_size, dropout=getattr(args, "dropout", 0.1),
                                  dim_feedforward=getattr(args, "dim_feedforward", 2048))
     from .native import balanced_layer_ranges
     rng = balanced_layer_ranges(cfg, num_stages, reference_rule=True)[stage_index]
-    model = NativeModel(cfg, stage_index, num_stages, device, layer_range=rng, seed=seed)
+    model = NativeModel(cfg, stage_index, num_stages, device, layer_range=rng, seed=seed, dtype=dtype)
     return NativeStage(model, mbs, seq_len)

@@ -87,9 +87,7 @@ class _PipelineSchedule:
         if outs is None or not has_last:
             return None
         if len(outs[0]) == 1:
-            if outs[0][0].dim() == 0:  # native stages return per-microbatch losses, not logits
-                return torch.stack([o[0] for o in outs])
-            return torch.cat([o[0] for o in outs], dim=0)
+            return torch.cat([o[0] for o in outs], dim=0)   # merged last-stage outputs (logits)
         return tuple(torch.cat([o[i] for o in outs], dim=0) for i in range(len(outs[0])))
 
     def eval(self, *args, target=None, losses=None):

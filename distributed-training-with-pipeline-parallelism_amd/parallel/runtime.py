@@ -361,6 +361,7 @@ class PipelineRuntime:
     def _step_python(self, inputs, targets, losses, return_outputs, rec):
         for st in self.stages.values():
             st.clear_runtime_states()
+            st.want_outputs = bool(return_outputs)
         recv_works: Dict[tuple, List] = {}
         send_keep: List = []
         send_tensors: Dict[tuple, Tuple[torch.Tensor, ...]] = {}
@@ -378,11 +379,17 @@ class PipelineRuntime:
 
         deps = self.deps
 
+        ready = [None]   # profiling: time the last receive of the current action completed
+
         def wait_recv(key):
             for w in recv_works.pop(key, []):
                 w.wait()
             if deps is not None:
                 deps.on_wait(key)
+            if self.profile:
+                # busy time starts once the inputs are there (a host-blocking gloo wait on
+                # CPU; on GPU an event after the stream wait)
+                ready[0] = self.timer.mark()
 
         def read_recv(key, action):
             if deps is not None:
@@ -449,11 +456,12 @@ class PipelineRuntime:
                         reduce_works.append(w)
                     continue
                 t_s = self.timer.mark() if self.profile else None
+                ready[0] = None
                 with rng(a):
                     self._run_compute(a, st, inputs, targets, return_outputs, loss_scale, handoff, outputs,
                                       mb_losses, wait_recv, read_recv, produce)
                 if self.profile:
-                    self.timer.add(a, t_s, self.timer.mark())
+                    self.timer.add(a, ready[0] if ready[0] is not None else t_s, self.timer.mark())
             except Exception:
                 self._report_failure(idx)
                 raise

@@ -162,3 +162,70 @@ def load_checkpoint(trainer, path: str, load_optimizer: bool = True, strict: boo
     handles.clear()
     _barrier()
     return man
+
+
+# ----------------------------------------------------------------------------------------
+# reference layout interop (helper:36-46, :78-91): global FQNs, unpadded vocabulary
+# ----------------------------------------------------------------------------------------
+VOCAB_ROWS = ("tok_embeddings.weight", "output.weight", "output.bias")
+
+
+def reference_state_dict(arenas, cfg) -> Dict[str, torch.Tensor]:
+    """f32 CPU ``state_dict`` of native arenas in the reference's layout: the FQNs of
+    ``nn.TransformerDecoderLayer`` / ``Transformer`` (the native reference block uses them
+    verbatim) and the vocabulary rows cut back from the kernel-friendly padding
+    (``vocab_padded``) to ``vocab_size`` -- what ``manual_model_split(...).submod.state_dict()``
+    holds for the same stage."""
+    out: Dict[str, torch.Tensor] = {}
+    for arena in arenas:
+        for name in arena.order:
+            t = arena.master_view(name).detach().float().cpu()
+            if name in VOCAB_ROWS:
+                t = t[: cfg.vocab_size]
+            out[name] = t.clone().contiguous()
+    return out
+
+
+def load_reference_state_dict(arenas, cfg, state_dict: Dict[str, torch.Tensor], strict: bool = True) -> List[str]:
+    """Copy a reference-layout ``state_dict`` (e.g. a split stage's, or a full
+    ``Transformer``'s) into native arenas; padded vocabulary rows are zeroed.  Keys the
+    arenas do not own are ignored (a full model's dict loads into any stage); with
+    ``strict`` every arena tensor must be present.  Returns the keys that were loaded."""
+    loaded, missing = [], []
+    for arena in arenas:
+        for name in arena.order:
+            src = state_dict.get(name)
+            if src is None:
+                missing.append(name)
+                continue
+            dst = arena.master_view(name)
+            src = src.detach().to(dst.device, torch.float32)
+            if name in VOCAB_ROWS and src.shape[0] != dst.shape[0]:
+                dst.zero_()
+                dst[: src.shape[0]].copy_(src)
+            else:
+                dst.copy_(src.reshape(dst.shape))
+            loaded.append(name)
+        arena.sync_w16()
+    if strict and missing:
+        raise KeyError(f"reference state_dict lacks {len(missing)} tensors, e.g. {missing[:4]}")
+    return loaded
+
+
+def export_reference_stage(trainer) -> Dict[str, torch.Tensor]:
+    """This rank's part of the model as the reference's per-stage ``state_dict`` (global
+    FQNs, unpadded).  A distributed head (replicated on every rank) is exported by the
+    rank holding the last stage, where the reference keeps ``output``."""
+    arenas = [st.arena for st in trainer.stages]
+    if getattr(trainer, "head", None) is not None and any(st.is_last for st in trainer.stages):
+        arenas.append(trainer.head.arena)
+    return reference_state_dict(arenas, trainer.cfg)
+
+
+def import_reference_stage(trainer, state_dict: Dict[str, torch.Tensor], strict: bool = True) -> List[str]:
+    """Load reference-layout weights (one stage's dict, several merged, or a full model's)
+    into every arena of this rank (including a replicated distributed head)."""
+    arenas = [st.arena for st in trainer.stages]
+    if getattr(trainer, "head", None) is not None:
+        arenas.append(trainer.head.arena)
+    return load_reference_state_dict(arenas, trainer.cfg, state_dict, strict=strict)

@@ -37,3 +37,35 @@ def test_sweep_analysis_tables_and_plots(tmp_path):
     assert os.path.getsize(tmp_path / "eff.png") > 0 and os.path.getsize(tmp_path / "thr.png") > 0
     rep = compat.environment_report()
     assert "torch" in rep and rep["cpu_count"] > 0
+
+
+def test_native_last_stage_step_returns_merged_logits():
+    """schedule.step(target=y, losses=...) on the last rank returns the merged logits
+    [B, S, vocab] (reference helper:128, dependency schedules.py:646-652) on the native
+    engine too, equal to the reference module's output for the same weights."""
+    import torch
+    from mipipe.models.ref_transformer import ModelArgs, Transformer, tokenwise_loss_fn
+    from mipipe.models.stage import build_reference_stage
+    from mipipe.parallel.api import Schedule1F1B
+    from mipipe.utils.checkpoint import load_reference_state_dict
+    torch.manual_seed(0)
+    a = ModelArgs(dim=64, n_layers=2, n_heads=4, vocab_size=100, dim_feedforward=128, dropout=0.0)
+    ref = Transformer(a)
+    st = build_reference_stage(a, 0, 1, torch.device("cpu"), mbs=2, seq_len=16)
+    load_reference_state_dict([st.arena], st.cfg, ref.state_dict())
+    sched = Schedule1F1B(st, n_microbatches=4, loss_fn=tokenwise_loss_fn(a.vocab_size))
+    x = torch.randint(0, 100, (8, 16))
+    y = torch.randint(0, 100, (8, 16))
+    losses = []
+    out = sched.step(x, target=y, losses=losses)
+    assert out.shape == (8, 16, 100) and len(losses) == 4
+    torch.testing.assert_close(out.float(), ref(x).detach(), atol=1e-4, rtol=1e-4)
+    assert sched.step(x, target=y, losses=[], return_outputs=False) is None
+
+
+def test_run_train_iterations_reports_bubble():
+    m = compat.run_one_experiment(4, 4, 2, "GPipe", batch_size=8, seq_length=16, num_iterations=1, device="cpu",
+                                  engine="native", timeout=300)
+    assert "error" not in m, m
+    assert 0.0 <= m["bubble_fraction"] < 1.0
+    assert m["analytic_bubble"] == pytest.approx(1 / 5)

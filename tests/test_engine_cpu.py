@@ -12,7 +12,11 @@ from dist_utils import run_world
 CFG = dict(gpt2=lambda: NativeConfig.gpt2("tiny", vocab_size=100, d_model=64, n_layers=4, n_heads=4, d_ff=128,
                                           max_seq_len=16),
            llama=lambda: NativeConfig.llama3("tiny", vocab_size=100, d_model=64, n_layers=4, n_heads=4, n_kv_heads=2,
-                                             d_ff=128, max_seq_len=16))
+                                             d_ff=128, max_seq_len=16),
+           gpt2_8=lambda: NativeConfig.gpt2("tiny", vocab_size=100, d_model=64, n_layers=8, n_heads=4, d_ff=128,
+                                            max_seq_len=16),
+           llama_8=lambda: NativeConfig.llama3("tiny", vocab_size=100, d_model=64, n_layers=8, n_heads=4,
+                                               n_kv_heads=2, d_ff=128, max_seq_len=16))
 M, MBS, S = 4, 2, 16
 
 
@@ -23,13 +27,13 @@ def _data(cfg, dp_rank=0, step=0):
 
 
 def _train(name, pp, dp, schedule, steps=2, split_head=None, layer_ranges="auto", max_grad_norm=1.0,
-           concat_dp=1, adam_eps=1e-8, lr=1e-3):
+           concat_dp=1, adam_eps=1e-8, lr=1e-3, v=None):
     """concat_dp=k (PP=1, DP=1 only): train on the concatenation of k DP replicas' batches
     (k*M microbatches) -- the single-process oracle of a DP=k run."""
     cfg = CFG[name]()
     if layer_ranges == "auto":
-        layer_ranges = [(0, 2), (2, 4)] if pp == 2 else None
-    tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=schedule, n_microbatches=M * concat_dp, mbs=MBS, seq_len=S,
+        layer_ranges = [(0, 2), (2, 4)] if (pp == 2 and not v) else None
+    tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=schedule, n_microbatches=M * concat_dp, mbs=MBS, seq_len=S, v=v,
                          device=torch.device("cpu"), dtype=torch.float32, lr=lr,
                          layer_ranges=layer_ranges, split_head=split_head, head_align=8,
                          max_grad_norm=max_grad_norm, adam_eps=adam_eps)
@@ -48,9 +52,27 @@ def _train(name, pp, dp, schedule, steps=2, split_head=None, layer_ranges="auto"
 
 
 def _worker(rank, world, name, pp, dp, schedule, split_head=None, layer_ranges="auto", max_grad_norm=1.0,
-            adam_eps=1e-8, lr=1e-3):
+            adam_eps=1e-8, lr=1e-3, v=None):
     return _train(name, pp, dp, schedule, split_head=split_head, layer_ranges=layer_ranges,
-                  max_grad_norm=max_grad_norm, adam_eps=adam_eps, lr=lr)
+                  max_grad_norm=max_grad_norm, adam_eps=adam_eps, lr=lr, v=v)
+
+
+@pytest.mark.parametrize("name", ["gpt2_8", "llama_8"])
+@pytest.mark.parametrize("pp", [2, 4])
+@pytest.mark.parametrize("split_head", [False, True])
+def test_interleaved_v2_matches_pp1(name, pp, split_head):
+    """Interleaved 1F1B with 2 virtual stages per rank (reference helper:182-185,
+    204-211, 219-220; BASELINE config 3) on the native engine: PP=2 (4 stages) and PP=4
+    (8 stages, loop placement: rank r holds stages r and r+P, wrap-around P-1 -> 0)."""
+    ref = _train(name, 1, 1, "1F1B")
+    res = run_world(_worker, pp, name, pp, 1, "Interleaved1F1B", split_head, None, 1.0, 1e-8, 1e-3, 2)
+    holders = range(pp) if split_head else [pp - 1]      # loss lives on the last stage's rank
+    for r in holders:
+        assert res[r]["losses"] == pytest.approx(ref["losses"], rel=1e-5)
+    for r in res.values():
+        for k, w in r["sd"].items():
+            torch.testing.assert_close(torch.from_numpy(w), torch.from_numpy(ref["sd"][k]), atol=1e-4, rtol=1e-4,
+                                       msg=lambda m: f"{k}: {m}")
 
 
 @pytest.mark.parametrize("name,split_head", [("gpt2", True), ("gpt2", False), ("llama", True)])

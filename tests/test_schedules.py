@@ -60,7 +60,9 @@ def test_validate_lower_and_no_deadlock(name, P, m, v):
         pytest.skip("torch-style interleave requires m % rounds == 0")
     o = generate(name, P, m, v)
     validate(o, P, v, m)
-    prog = lower(o, P, v)  # runs check_lowered
+    prog = lower(o, P, v)  # runs check_lowered (one comm stream per rank)
+    # the native engine's per-direction channels (2 comm streams per rank) must be safe too
+    check_lowered(prog, P * v, channels=2)
     # every send has exactly one matching recv with the same key, posted by the peer
     sends, recvs = {}, {}
     for r, es in prog.items():
@@ -98,6 +100,38 @@ def test_checker_detects_deadlock():
     }
     with pytest.raises(RuntimeError):
         check_lowered(prog, 2)
+    # with one comm stream per direction the early gradient receive no longer holds back
+    # the activation send: the same program is safe on the native engine's 2 channels
+    check_lowered(prog, 2, channels=2)
+
+
+def test_pp8_interleaved_v2_m16_gpt2_medium_lowering():
+    """BASELINE config 3 (configs/gpt2_medium_interleaved_pp8.yaml): GPT-2 medium,
+    Interleaved 1F1B, PP=8, v=2, m=16, distributed head -- the exact program the runtime
+    builds must validate, lower and be hang-free on 1 and 2 comm channels, with the
+    simulated bubble of the plain schedule equal to the analytic (P-1)/(v*m+P-1)."""
+    from mipipe.models.config import NativeConfig
+    from mipipe.models.native import balanced_layer_ranges, stage_cost_model
+    from mipipe.parallel.headsplit import head_token_split, plan_head_schedule
+    P, v, m = 8, 2, 16
+    base = generate("Interleaved1F1B", P, m, v)
+    validate(base, P, v, m)
+    assert simulate(base, P, v).bubble == pytest.approx((P - 1) / (v * m + P - 1), abs=1e-9)
+    cfg = NativeConfig.gpt2("medium")
+    lr = balanced_layer_ranges(cfg, P * v, 1024, head_on_last=False)
+    assert len(lr) == 16 and lr[0][0] == 0 and lr[-1][1] == 24
+    lc, head_units, ec = stage_cost_model(cfg, 1024)
+    stage_costs = [(b - a) * lc + (ec if s == 0 else 0.0) for s, (a, b) in enumerate(lr)]
+    rank_load = [sum(stage_costs[s] for s in range(P * v) if s % P == r) for r in range(P)]
+    chunks = head_token_split(8 * 1024, rank_load, head_units, align=256)
+    assert sum(chunks) == 8 * 1024
+    head_costs = {r: 3.0 * head_units * chunks[r] / (8 * 1024) for r in range(P) if chunks[r] > 0}
+    orders, lag, makespan = plan_head_schedule(base, P, v, "loop", head_costs, stage_costs)
+    prog = lower(orders, P, v, "loop", head_costs=head_costs, stage_costs=stage_costs)
+    check_lowered(prog, P * v, channels=1)
+    check_lowered(prog, P * v, channels=2)
+    ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * m / P
+    assert ideal / makespan > 0.75, (ideal, makespan, lag)
 
 
 @pytest.mark.parametrize("P,m", [(2, 4), (4, 4), (4, 8), (8, 16)])
