@@ -44,9 +44,11 @@ int mp_transpose_batched(const void* src, void* dst, const int64_t* desc, const 
 int mp_set_drop_step_attn(uint64_t v, hipStream_t st);
 int mp_set_drop_step_elem(uint64_t v, hipStream_t st);
 int mp_set_drop_step_norm(uint64_t v, hipStream_t st);
+int mp_set_drop_step_gemm(uint64_t v, hipStream_t st);
 int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
              int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
-             int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, float* colsum, hipStream_t st);
+             int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, float* colsum, float p_drop,
+             uint64_t seed, hipStream_t st);
 int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg, int* split_out);
 int mp_gemm(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
@@ -85,7 +87,9 @@ void norm_fwd(bool rms, torch::Tensor a, c10::optional<torch::Tensor> b, torch::
         "norm_fwd");
 }
 
-void norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c10::optional<torch::Tensor> mean,
+// returns 0, or -3 when the requested fused column sums are not available for this shape
+// (the caller then sums separately); other failures raise
+int64_t norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c10::optional<torch::Tensor> mean,
               torch::Tensor rstd, c10::optional<torch::Tensor> dres, torch::Tensor ds,
               c10::optional<torch::Tensor> dbranch, torch::Tensor dw, c10::optional<torch::Tensor> dbias, double p,
               int64_t seed, c10::optional<torch::Tensor> cs_res, c10::optional<torch::Tensor> cs_ds) {
@@ -96,14 +100,16 @@ void norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c10:
   const int D = dy.size(-1);
   const int rows = dy.numel() / D;
   TORCH_CHECK(s.numel() == dy.numel() && ds.numel() == dy.numel() && dw.numel() == D, "bad norm_bwd shapes");
-  check(mp_norm_bwd(rms, dy.data_ptr(), s.data_ptr(), w.data_ptr(),
-                    mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), ptr_or_null(dres),
-                    ds.data_ptr(), mptr_or_null(dbranch), dw.data_ptr<float>(),
-                    dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
-                    cs_res.has_value() ? cs_res->data_ptr<float>() : nullptr,
-                    cs_ds.has_value() ? cs_ds->data_ptr<float>() : nullptr, rows, D, (float)p, (uint64_t)seed,
-                    cur_stream()),
-        "norm_bwd");
+  const int rc = mp_norm_bwd(rms, dy.data_ptr(), s.data_ptr(), w.data_ptr(),
+                             mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(),
+                             ptr_or_null(dres), ds.data_ptr(), mptr_or_null(dbranch), dw.data_ptr<float>(),
+                             dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
+                             cs_res.has_value() ? cs_res->data_ptr<float>() : nullptr,
+                             cs_ds.has_value() ? cs_ds->data_ptr<float>() : nullptr, rows, D, (float)p,
+                             (uint64_t)seed, cur_stream());
+  if (rc == -3) return -3;
+  check(rc, "norm_bwd");
+  return 0;
 }
 
 void xent(torch::Tensor logits, torch::Tensor target, torch::Tensor loss, int64_t V, double grad_scale,
@@ -262,7 +268,8 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch
 // 2 if done WITHOUT the requested fused column sums (caller sums separately)
 int64_t gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> bias,
               c10::optional<torch::Tensor> residual, c10::optional<torch::Tensor> aux, bool transA, bool transB,
-              int64_t epilogue, bool accum, double alpha, int64_t force_cfg, c10::optional<torch::Tensor> colsum) {
+              int64_t epilogue, bool accum, double alpha, int64_t force_cfg, c10::optional<torch::Tensor> colsum,
+              double p_drop, int64_t seed) {
   const int M = C.size(0), N = C.size(1);
   const int K = transA ? A.size(0) : A.size(1);
   TORCH_CHECK((transA ? A.size(1) : A.size(0)) == M, "gemm2: A/M mismatch");
@@ -282,13 +289,15 @@ int64_t gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<t
                           residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
                           transA, transB, epilogue, accum, (float)alpha, (int)force_cfg,
                           ws.defined() ? ws.data_ptr<float>() : nullptr,
-                          colsum.has_value() ? colsum->data_ptr<float>() : nullptr, cur_stream());
+                          colsum.has_value() ? colsum->data_ptr<float>() : nullptr, (float)p_drop, (uint64_t)seed,
+                          cur_stream());
   if (rc == -3) {
     const int rc2 = mp_gemm2(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual),
                              mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),
                              residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
                              transA, transB, epilogue, accum, (float)alpha, (int)force_cfg,
-                             ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, cur_stream());
+                             ws.defined() ? ws.data_ptr<float>() : nullptr, nullptr, (float)p_drop, (uint64_t)seed,
+                             cur_stream());
     if (rc2 == -2 || rc2 == -1) return 0;
     check(rc2, "gemm2");
     return 2;
@@ -342,6 +351,7 @@ void set_dropout_step(int64_t step) {
   check(mp_set_drop_step_attn(v, cur_stream()), "set_drop_step");
   check(mp_set_drop_step_elem(v, cur_stream()), "set_drop_step");
   check(mp_set_drop_step_norm(v, cur_stream()), "set_drop_step");
+  check(mp_set_drop_step_gemm(v, cur_stream()), "set_drop_step");
 }
 
 }  // namespace
@@ -374,7 +384,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
-  m.def("gemm2", &gemm2);
+  m.def("gemm2", &gemm2, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
+        pybind11::arg("residual"), pybind11::arg("aux"), pybind11::arg("transA"), pybind11::arg("transB"),
+        pybind11::arg("epilogue"), pybind11::arg("accum"), pybind11::arg("alpha"), pybind11::arg("force_cfg"),
+        pybind11::arg("colsum"), pybind11::arg("p_drop") = 0.0, pybind11::arg("seed") = 0);
   m.def("transpose", &transpose);
   m.def("set_dropout_step", &set_dropout_step);
   m.def("create_stream", &create_stream, pybind11::arg("device"), pybind11::arg("priority") = 0);

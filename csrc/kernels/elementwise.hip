@@ -10,6 +10,8 @@
 //                   (forward: +theta, backward: -theta), f32 cos/sin table from the host
 #include "mp_common.h"
 
+#include <stdlib.h>
+
 using namespace mp;
 
 enum Act { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_RELU = 2 };
@@ -235,10 +237,19 @@ extern "C" int mp_act_fwd(const void* a, void* g, int64_t n, int act, float p, u
 }
 
 static void colsum_grid(int rows, int cols, dim3& grid, int& rpb) {
+  // every block ends with one f32 atomic per column: at least MIPIPE_COLSUM_RPB (32) rows
+  // per block, so short (1024-row) problems do not turn into atomic contention
+  static const int min_rpb = [] {
+    const char* e = getenv("MIPIPE_COLSUM_RPB");
+    const int v = e ? atoi(e) : 32;
+    return v > 0 ? v : 32;
+  }();
   const int ny = (cols / 8 + 63) / 64;
   int nx = 1024 / ny;
   if (nx < 1) nx = 1;
   if (nx > (rows + 3) / 4) nx = (rows + 3) / 4;
+  if (nx > (rows + min_rpb - 1) / min_rpb) nx = (rows + min_rpb - 1) / min_rpb;
+  if (nx < 1) nx = 1;
   rpb = (rows + nx - 1) / nx;
   grid = dim3((rows + rpb - 1) / rpb, ny);
 }

@@ -131,7 +131,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 template <int EPI>
 __device__ __forceinline__ void epi_store8(float (&v)[8], int gr, int gc, bf16_t* __restrict__ C, int64_t ldc,
                                            const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
-                                           int64_t ldr, bf16_t* __restrict__ AUX, int64_t ldx) {
+                                           int64_t ldr, bf16_t* __restrict__ AUX, int64_t ldx, float p_drop,
+                                           uint64_t seed) {
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU || EPI == EPI_BIAS_RES) {
     u16x8 bv = *reinterpret_cast<const u16x8*>(bias + gc);
 #pragma unroll
@@ -144,6 +145,9 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int gr, int gc, bf16_t
       pre[e] = f2bf(v[e]);
       const float x = bf2f(pre[e]);
       v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
+      // dropout after the activation (the reference FFN's drop(relu(.))), mask index =
+      // element index of the contiguous output, as act_fwd / act_bwd regenerate it
+      if (p_drop > 0.f) v[e] *= dropout_scale(seed, (uint64_t)gr * ldc + gc + e, p_drop);
     }
     *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
   }
@@ -158,6 +162,7 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int gr, int gc, bf16_t
     for (int e = 0; e < 8; ++e) {
       const float x = bf2f(xv[e]);
       v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
+      if (p_drop > 0.f) v[e] *= dropout_scale(seed, (uint64_t)gr * ldc + gc + e, p_drop);
     }
   }
   u16x8 o;
@@ -208,7 +213,8 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
                                          void* __restrict__ Cv,
                                          const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
                                          bf16_t* __restrict__ AUX, float* __restrict__ WS, int M, int N, int64_t ldc,
-                                         int64_t ldr, int64_t ldx, float alpha, int nsplit) {
+                                         int64_t ldr, int64_t ldx, float alpha, int nsplit, float p_drop,
+                                         uint64_t seed) {
   constexpr int RG = BM / WM;      // rows per group
   constexpr int CP = BN + 4;       // f32 pitch
   float* ct = reinterpret_cast<float*>(smem);
@@ -271,7 +277,7 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
         *reinterpret_cast<float4*>(cp) = c0;
         *reinterpret_cast<float4*>(cp + 4) = c1;
       } else {
-        epi_store8<EPI>(v, gr, gc, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, AUX, ldx);
+        epi_store8<EPI>(v, gr, gc, reinterpret_cast<bf16_t*>(Cv), ldc, bias, R, ldr, AUX, ldx, p_drop, seed);
         if (cs) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) csum[e] += v[e];
@@ -303,7 +309,8 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
                                                       const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
                                                       float* __restrict__ WS, int M, int N, int K, int64_t lda,
                                                       int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx,
-                                                      float alpha) {
+                                                      float alpha, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   static_assert(WM * WN == 8, "8 waves");
   constexpr int WTM = BM / WM / 32, WTN = BN / WN / 32;
   static_assert(WTM * 32 * WM == BM && WTN * 32 * WN == BN, "tile/wave mismatch");
@@ -425,7 +432,7 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 
   epilogue<BM, BN, WM, WN, EPI, ACC>(Stage32<WTM, WTN>{acc, wn, hl, l32}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M,
-                                     N, ldc, ldr, ldx, alpha, nsplit);  } else {
+                                     N, ldc, ldr, ldx, alpha, nsplit, p_drop, seed);  } else {
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -504,7 +511,7 @@ __global__ void __launch_bounds__(NT, 2) __attribute__((amdgpu_waves_per_eu(2, 2
   }
 
   epilogue<BM, BN, WM, WN, EPI, ACC>(Stage16<TM, TN>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M, N, ldc,
-                                     ldr, ldx, alpha, nsplit);
+                                     ldr, ldx, alpha, nsplit, p_drop, seed);
   }
 
 }
@@ -531,7 +538,8 @@ __global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2
 gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
              const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
              float* __restrict__ WS, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr,
-             int64_t ldx, float alpha) {
+             int64_t ldx, float alpha, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
   constexpr int HALF = 128 * 128;          // one half-tile image: 128 rows x 128 B
   constexpr int BUF = 4 * HALF;            // A0 A1 B0 B1
@@ -728,7 +736,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
   __syncthreads();
   epilogue<BM, BN, WM, WN, EPI, ACC>(Stage32<4, 2>{acc, wn, hl, l32}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M,
-                                     N, ldc, ldr, ldx, alpha, nsplit);
+                                     N, ldc, ldr, ldx, alpha, nsplit, p_drop, seed);
   } else {
   // 16x16x32 MFMAs: same phases, DMA and barriers; a phase quadrant (64 rows x 32 cols)
   // is 4 x 2 blocks of 16x16, K = 64 in two 32-deep steps (16 MFMAs of 16 cycles)
@@ -837,7 +845,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
   __syncthreads();
   epilogue<BM, BN, WM, WN, EPI, ACC>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M, N, ldc,
-                                     ldr, ldx, alpha, nsplit);
+                                     ldr, ldx, alpha, nsplit, p_drop, seed);
   }
 }
 
@@ -845,7 +853,7 @@ template <int EPI, bool ACC, bool M16, bool TT = false>
 static int launch3(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
                    int N, int K,
                    int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
-                   hipStream_t st) {
+                   float p_drop, uint64_t seed, hipStream_t st) {
   constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
   constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
   constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
@@ -857,16 +865,163 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   }
   const int nwg = ((M + 255) / 256) * ((N + 255) / 256);
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
-                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
+                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
   return (int)hipGetLastError();
 }
 
+
+// ---------------------------------------------------------------------------------------
+// gemms: small-tile NT engine for short-token problems (the reference model's 1024-token
+// microbatches: M = 1024, N = 768..2304).  A 256x256 grid there has 12-36 tiles for 256
+// CUs, and split-K to fill the chip costs an f32 slab round trip plus a reduce/epilogue
+// kernel per GEMM (~40 % of those GEMMs' time, profiles/r2_ref_L8H8_kernel_stats.csv).
+// Here: 256-thread workgroups (2x2 waves), BM x BN in {64x64, 64x32, 32x32}, 16x16x32
+// MFMAs, the same 2-stage global_load_lds pipeline / swizzled K-contiguous images as
+// gemm2, several workgroups per CU (32 KiB LDS at 64x64), and the fused epilogue applied
+// directly -- one launch per GEMM, no split-K.
+// ---------------------------------------------------------------------------------------
+template <int BM, int BN, int EPI, bool ACC>
+__global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                    void* __restrict__ Cv, const bf16_t* __restrict__ bias,
+                                                    const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+                                                    float* __restrict__ WS, int M, int N, int K, int64_t lda,
+                                                    int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  constexpr int NTH = 256, WM = 2, WN = 2;
+  constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
+  static_assert(TM >= 1 && TN >= 1 && TM * 16 * WM == BM && TN * 16 * WN == BN, "tile/wave mismatch");
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int PIECES = STAGE / 1024, PW = PIECES / 4;
+  static_assert(PW * 4 == PIECES, "pieces must split over 4 waves");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int wg = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GROUP = 8;
+  const int group = wg / (GROUP * gn);
+  const int first_m = group * GROUP;
+  const int gsz = min(gm - first_m, GROUP);
+  const int tm = first_m + (wg % (GROUP * gn)) % gsz;
+  const int tn = (wg % (GROUP * gn)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int wm = wr * (BM / WM), wn = wc * (BN / WN);
+
+  const int nsplit = gridDim.y;
+  const int ktiles = K / BK;
+  const int kt0 = (int)blockIdx.y * ktiles / nsplit;
+  const int nk = ((int)blockIdx.y + 1) * ktiles / nsplit - kt0;
+  const int kbase = kt0 * BK;
+
+  const bf16_t* psrc[PW];
+  bool pisA[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int p = wave + 4 * i;
+    const int pos = p * 1024 + lane * 16;
+    pisA[i] = p * 1024 < A_BYTES;
+    if (pisA[i]) psrc[i] = src_of<false, BM, true>(A, lda, pos, m0, M, kbase);
+    else psrc[i] = src_of<false, BN, true>(B, ldb, pos - A_BYTES, n0, N, kbase);
+  }
+  auto issue = [&](int stage, int kt) {
+    char* sb = smem + stage * STAGE;
+    const int64_t dk = (int64_t)kt * BK;
+#pragma unroll
+    for (int i = 0; i < PW; ++i) {
+      const int p = wave + 4 * i;
+      __builtin_amdgcn_global_load_lds((const void*)(psrc[i] + dk),
+                                       (__attribute__((address_space(3))) void*)(sb + p * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{};
+
+  if (nk > 0) {
+    issue(0, 0);
+    if (nk > 1) {
+      issue(1, 1);
+      wait_vmcnt<PW>();
+    } else {
+      wait_vmcnt<0>();
+    }
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nk; ++t) {
+    const char* sa = smem + (t & 1) * STAGE;
+    const char* sbB = sa + A_BYTES;
+    bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[s_][i] = frag16<false, BM>(sa, wm + 16 * i, s_);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[s_][j] = frag16<false, BN>(sbB, wn + 16 * j, s_);
+    }
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_) {
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[s_][i], bfr[s_][j], acc[i][j]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < nk) {
+      issue(t & 1, t + 2);
+      wait_vmcnt<PW>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  epilogue<BM, BN, WM, WN, EPI, ACC, NTH>(Stage16<TM, TN>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M,
+                                          N, ldc, ldr, ldx, alpha, nsplit, p_drop, seed);
+}
+
+template <int BM, int BN, int EPI, bool ACC>
+static int launchs(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
+                   int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
+                   float p_drop, uint64_t seed, hipStream_t st) {
+  constexpr int STAGE = (BM + BN) * BK * 2;
+  constexpr int EPI_BYTES = (BM / 2) * (BN + 4) * 4;
+  constexpr int RED_BYTES = 256 * 8 * 4;   // the column-sum reduction reuses the staging area
+  constexpr int LDS0 = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
+  constexpr int LDS = LDS0 > RED_BYTES ? LDS0 : RED_BYTES;
+  auto kern = gemms_kernel<BM, BN, EPI, ACC>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  kern<<<dim3(nwg, split), 256, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
+                                           (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
+  return (int)hipGetLastError();
+}
 
 template <int BM, int BN, int WM, int WN, bool TA, bool TB, int EPI, bool ACC>
 static int launch(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
                   int N, int K,
                   int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
-                  hipStream_t st) {
+                  float p_drop, uint64_t seed, hipStream_t st) {
   constexpr int STAGE = (BM + BN) * BK * 2;
   constexpr int EPI_BYTES = (BM / WM) * (BN + 4) * 4;
   constexpr int LDS = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
@@ -883,7 +1038,7 @@ static int launch(const void* A, const void* B, void* C, const void* bias, const
   }
   const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
-                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha);
+                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
   return (int)hipGetLastError();
 }
 
@@ -935,19 +1090,22 @@ template <bool TA, bool TB, int EPI, bool ACC>
 static int dispatch(int cfg, const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws,
                     int M,
                     int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
-                    int split, hipStream_t st) {
+                    int split, float p_drop, uint64_t seed, hipStream_t st) {
   if constexpr (TA && TB && ACC && EPI == EPI_NONE) {
-    if (cfg == 6) return launch3<EPI, ACC, true, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    if (cfg == 6) return launch3<EPI, ACC, true, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
   }
   if constexpr (!TA && !TB) {
-    if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
-    if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    if (cfg == 10) return launchs<64, 64, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    if (cfg == 11) return launchs<64, 32, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    if (cfg == 12) return launchs<32, 32, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
   }
   switch (cfg) {
-    case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
-    case 1: return launch<256, 192, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
-    case 2: return launch<256, 128, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
-    default: return launch<128, 128, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, st);
+    case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    case 1: return launch<256, 192, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    case 2: return launch<256, 128, 4, 2, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    default: return launch<128, 128, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
   }
 }
 
@@ -976,7 +1134,9 @@ template <int EPI>
 __global__ void __launch_bounds__(256) splitk_epi_kernel(const float* __restrict__ ws, bf16_t* __restrict__ C, int M,
                                                          int N, int64_t ldc, int split, const bf16_t* __restrict__ bias,
                                                          const bf16_t* __restrict__ R, int64_t ldr,
-                                                         bf16_t* __restrict__ AUX, int64_t ldx) {
+                                                         bf16_t* __restrict__ AUX, int64_t ldx, float p_drop,
+                                                         uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
   const int64_t n8 = (int64_t)M * N / 8;
   const int64_t slab = (int64_t)M * N;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
@@ -990,17 +1150,18 @@ __global__ void __launch_bounds__(256) splitk_epi_kernel(const float* __restrict
       b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
     }
     float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    epi_store8<EPI>(v, m, n, C, ldc, bias, R, ldr, AUX, ldx);
+    epi_store8<EPI>(v, m, n, C, ldc, bias, R, ldr, AUX, ldx, p_drop, seed);
   }
 }
 
 template <int EPI>
 static int launch_splitk_epi(const float* ws, void* C, int M, int N, int64_t ldc, int split, const void* bias,
-                             const void* R, int64_t ldr, void* X, int64_t ldx, hipStream_t st) {
+                             const void* R, int64_t ldr, void* X, int64_t ldx, float p_drop, uint64_t seed,
+                             hipStream_t st) {
   const int64_t n8 = (int64_t)M * N / 8;
   const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 4096);
   splitk_epi_kernel<EPI><<<blocks, 256, 0, st>>>(ws, (bf16_t*)C, M, N, ldc, split, (const bf16_t*)bias,
-                                                 (const bf16_t*)R, ldr, (bf16_t*)X, ldx);
+                                                 (const bf16_t*)R, ldr, (bf16_t*)X, ldx, p_drop, seed);
   return (int)hipGetLastError();
 }
 
@@ -1011,6 +1172,7 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   int split = 1;
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
   if (force_cfg >= 0 && force_cfg < 7) cfg = force_cfg;
+  if (force_cfg >= 10) cfg = 0;   // placeholder; the small-engine branch below sets it
   // the ping-pong 256x256 engine for both-K-contiguous operands (MIPIPE_GEMM3=0 disables;
   // MIPIPE_GEMM_M16=1 selects its 16x16x32-MFMA build)
   static const bool use3 = [] { const char* e = getenv("MIPIPE_GEMM3"); return !(e && e[0] == '0'); }();
@@ -1033,6 +1195,26 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   // bf16-output split-K runs the f32-accumulate instantiation (NT or TT) into slabs
   if (!c_f32_accum && transA != transB) split = 1;
   if (!c_f32_accum && split > 1 && (cfg == 4 || cfg == 5)) cfg = transA ? 0 : cfg;
+  // short-token NT problems (few 256-row tiles): the small-tile engine, one launch, no
+  // split-K (MIPIPE_GEMM_SMALL=0 disables; MIPIPE_GEMMS_MINWG = workgroups to aim for)
+  static const bool use_small = [] { const char* e = getenv("MIPIPE_GEMM_SMALL"); return !(e && e[0] == '0'); }();
+  static const int minwg = [] {
+    const char* e = getenv("MIPIPE_GEMMS_MINWG");
+    const int v = e ? atoi(e) : 256;
+    return v > 0 ? v : 256;
+  }();
+  if (!transA && !transB && use_small && (force_cfg < 0 || force_cfg >= 10)) {
+    const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
+    if (force_cfg >= 10 && force_cfg <= 12) {
+      cfg = force_cfg;
+      split = 1;
+    } else if (t256 < 64 && !c_f32_accum && K <= 4096) {   // long K: the big split-K plan wins
+      const int w64 = ((M + 63) / 64) * ((N + 63) / 64);
+      const int w6432 = ((M + 63) / 64) * ((N + 31) / 32);
+      cfg = w64 >= minwg ? 10 : (w6432 >= minwg ? 11 : 12);
+      split = 1;
+    }
+  }
   *split_out = split;
   return cfg;
 }
@@ -1043,7 +1225,7 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
 extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux,
                         int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux,
                         int transA, int transB, int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws,
-                        float* colsum, hipStream_t st) {
+                        float* colsum, float p_drop, uint64_t seed, hipStream_t st) {
   if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
   int split = 1;
   const int cfg = mp_gemm2_plan(M, N, K, transA, transB, c_f32_accum, force_cfg, &split);
@@ -1060,26 +1242,26 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
     // one pass sums them and applies the fused epilogue
     if (ws == nullptr) return -1;
     if (transA && transB) rc = dispatch<true, true, EPI_NONE, true>(cfg, A, B, nullptr, nullptr, nullptr, nullptr, ws, M, N, K,
-                                                              lda, ldb, N, 0, 0, alpha, split, st);
+                                                              lda, ldb, N, 0, 0, alpha, split, p_drop, seed, st);
     else rc = dispatch<false, false, EPI_NONE, true>(cfg, A, B, nullptr, nullptr, nullptr, nullptr, ws, M, N, K, lda, ldb,
-                                                     N, 0, 0, alpha, split, st);
+                                                     N, 0, 0, alpha, split, p_drop, seed, st);
     if (rc != 0) return rc;
     switch (epilogue) {
-      case EPI_NONE: return launch_splitk_epi<EPI_NONE>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
-      case EPI_BIAS: return launch_splitk_epi<EPI_BIAS>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
-      case EPI_BIAS_GELU: return launch_splitk_epi<EPI_BIAS_GELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
-      case EPI_BIAS_RELU: return launch_splitk_epi<EPI_BIAS_RELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
-      case EPI_BIAS_RES: return launch_splitk_epi<EPI_BIAS_RES>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
-      case EPI_RES: return launch_splitk_epi<EPI_RES>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
-      case EPI_DGELU: return launch_splitk_epi<EPI_DGELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
-      case EPI_DRELU: return launch_splitk_epi<EPI_DRELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, st);
+      case EPI_NONE: return launch_splitk_epi<EPI_NONE>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
+      case EPI_BIAS: return launch_splitk_epi<EPI_BIAS>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
+      case EPI_BIAS_GELU: return launch_splitk_epi<EPI_BIAS_GELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
+      case EPI_BIAS_RELU: return launch_splitk_epi<EPI_BIAS_RELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
+      case EPI_BIAS_RES: return launch_splitk_epi<EPI_BIAS_RES>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
+      case EPI_RES: return launch_splitk_epi<EPI_RES>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
+      case EPI_DGELU: return launch_splitk_epi<EPI_DGELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
+      case EPI_DRELU: return launch_splitk_epi<EPI_DRELU>(ws, C, M, N, ldc, split, bias, residual, ld_res, aux, ld_aux, p_drop, seed, st);
       default: return -2;
     }
   }
 #define MP_G(TA_, TB_, E_, ACC_)                                                                                  \
   if (rc == -2 && (bool)transA == TA_ && (bool)transB == TB_ && epilogue == E_ && (bool)c_f32_accum == ACC_)     \
     rc = dispatch<TA_, TB_, E_, ACC_>(cfg, A, B, C, bias, residual, aux, wsp, M, N, K, lda, ldb, ldc, ld_res,       \
-                                      ld_aux, alpha, split, st);
+                                      ld_aux, alpha, split, p_drop, seed, st);
   MP_G(false, false, EPI_NONE, false)
   MP_G(false, false, EPI_BIAS, false)
   MP_G(false, false, EPI_BIAS_GELU, false)
@@ -1099,3 +1281,5 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   }
   return rc;
 }
+
+MP_DROP_STEP_SETTER(mp_set_drop_step_gemm)

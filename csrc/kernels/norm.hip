@@ -14,6 +14,8 @@
 // SURVEY §2.5 K7 (post-LN: 3 per layer + final) and the pre-norm GPT-2 / Llama blocks.
 #include "mp_common.h"
 
+#include <stdlib.h>
+
 using namespace mp;
 
 template <int MAXJ, bool RMS, bool HAS_B, bool HAS_BIAS>
@@ -94,8 +96,9 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(
 }
 
 // Backward.  grid.x blocks, each handling a contiguous slab of rows (4 waves, wave-strided).
-// COLS: also accumulate column sums of dres and of ds (the bias grads of the two
-// projections that feed / consume this residual point: GPT-2's FFN-out and attn-out biases)
+// COLS: also accumulate column sums of dres and of ds -- or, with a dropped branch, of the
+// branch gradient (the bias grads of the projections that feed / consume this residual
+// point: GPT-2's FFN-out and attn-out biases, the reference block's out_proj / linear2)
 template <int MAXJ, bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BRANCH_GRAD, bool COLS>
 __global__ void __launch_bounds__(256) norm_bwd_kernel(
     const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
@@ -197,11 +200,12 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
           float v = rstd * (g[j][e] - s1 - xh[j][e] * s2);
           if (HAS_DRES) v += bf2f(rv[e]);
           out[e] = f2bf(v);
-          if constexpr (COLS) {
-            acc_r[j][e] += bf2f(rv[e]);
-            acc_s[j][e] += bf2f(out[e]);
-          }
           if (BRANCH_GRAD) bout[e] = f2bf(v * dropout_scale(seed, base + c * 8 + e, p_drop));
+          if constexpr (COLS) {
+            if constexpr (HAS_DRES) acc_r[j][e] += bf2f(rv[e]);
+            // with a dropped branch: the branch gradient's column sums (its projection's bias grad)
+            acc_s[j][e] += BRANCH_GRAD ? bf2f(bout[e]) : bf2f(out[e]);
+          }
         }
         *reinterpret_cast<u16x8*>(ds_out + base + c * 8) = out;
         if (BRANCH_GRAD) *reinterpret_cast<u16x8*>(dbranch + base + c * 8) = bout;
@@ -236,7 +240,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
         const int j = j0 + jj;
         const int c = ln + 64 * j;
         if (j < MAXJ && c < nchunk) {
-          atomicAdd(o0 + c * 8 + e, red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i]);
+          if (o0 != nullptr) atomicAdd(o0 + c * 8 + e, red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i]);
           if (o1 != nullptr) atomicAdd(o1 + c * 8 + e, red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i]);
         }
       }
@@ -293,7 +297,17 @@ template <bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG, bool COLS>
 static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
                        const void* dres, void* ds, void* dbr, float* dw, float* db, float* csr, float* css, int rows,
                        int D, float p, uint64_t seed, hipStream_t st) {
-  const int nblk = rows < 512 ? (rows + 3) / 4 : 512;
+  // rows per workgroup: every workgroup ends with one f32 atomic per column and output
+  // (dw, dbias, column sums), all into the same few KB, so short problems want few, long
+  // workgroups (1024 rows: 512 workgroups of 2 rows measured 20-22 us, contention-bound)
+  static const int min_rpb = [] {
+    const char* e = getenv("MIPIPE_NORM_BWD_RPB");
+    const int v = e ? atoi(e) : 8;
+    return v > 0 ? v : 8;
+  }();
+  int nblk = rows < 512 ? (rows + 3) / 4 : 512;
+  if ((rows + nblk - 1) / nblk < min_rpb) nblk = (rows + min_rpb - 1) / min_rpb;
+  if (nblk < 1) nblk = 1;
   const int rpb = (rows + nblk - 1) / nblk;
   dim3 grid((rows + rpb - 1) / rpb), block(256);
 #define MP_BWD(J)                                                                                                   \
@@ -313,13 +327,18 @@ extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w
   const int J = pick_j(D);
   const bool hd = dres != nullptr, hb = dbias != nullptr, bg = dbranch != nullptr;
   if (cs_res != nullptr || cs_ds != nullptr) {
-    // column sums of dres and ds (bias grads of the adjacent projections): LN, dres, no branch
-    if (rms || !hd || bg || cs_res == nullptr || cs_ds == nullptr || J > 4) return -3;
-    if (hb) launch_bwd<false, true, true, false, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res,
-                                                       cs_ds, rows, D, p, seed, st);
-    else launch_bwd<false, true, false, false, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res,
-                                                     cs_ds, rows, D, p, seed, st);
-    return (int)hipGetLastError();
+    // column sums of dres and of ds / the branch gradient (bias grads of the adjacent
+    // projections), LayerNorm rows of up to 2048
+    if (rms || J > 4 || (cs_res != nullptr && !hd)) return -3;
+#define MP_C(HD, HB, BG_)                                                                                        \
+    if (hd == HD && hb == HB && bg == BG_) {                                                                       \
+      launch_bwd<false, HD, HB, BG_, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res, cs_ds,   \
+                                           rows, D, p, seed, st);                                                  \
+      return (int)hipGetLastError();                                                                               \
+    }
+    MP_C(1, 1, 0) MP_C(1, 0, 0) MP_C(0, 1, 1) MP_C(0, 0, 1) MP_C(1, 1, 1) MP_C(1, 0, 1) MP_C(0, 1, 0) MP_C(0, 0, 0)
+#undef MP_C
+    return -2;
   }
 #define MP_B(R, HD, HB, BG_)                                                                                   \
   if (rms == R && hd == HD && hb == HB && bg == BG_) {                                                          \

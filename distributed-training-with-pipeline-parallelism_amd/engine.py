@@ -114,14 +114,17 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
 
     bytes = parameters x 20 (bf16 weights + bf16 W^T copies + f32 master, grad, Adam m, v)
           + in-flight microbatches x local layers x per-layer stash (config.stash_bytes_per_layer)
-          + logits of the rank's head tokens (bf16, gradient written in place) + 4 GB workspace.
+          + logits of one head token chunk (bf16, gradient written in place; the whole
+            microbatch's with MIPIPE_HEAD_CHUNK=0) + 4 GB workspace.
     Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute."""
     T = mbs * seq_len
     nlayers = sum(layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages)
     emb = cfg.vocab_padded * cfg.d_model
     nparams = cfg.layer_params() * nlayers + (emb if 0 in my_stages else 0) + (emb if head_tokens else 0)
     inflight = max_inflight_microbatches(order, set(my_stages))
-    fixed = 20.0 * nparams + 2.0 * head_tokens * cfg.vocab_padded + 4e9
+    from .models.native import _HEAD_CHUNK
+    logit_rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
+    fixed = 20.0 * nparams + 2.0 * logit_rows * cfg.vocab_padded + 4e9
     full = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=False)
     rec = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=True) + \
         cfg.stash_bytes_per_layer(T, recompute=False)

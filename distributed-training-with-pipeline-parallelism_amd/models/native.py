@@ -496,8 +496,9 @@ class Block:
         ca = self._mha("multihead_attn", x1, h, B, S, _seed(sd, 3), st, "ca_", False)
         x2, s2, mu2, rs2 = ops.norm_fwd(x1, self.w("norm2.weight"), self.w("norm2.bias"), branch=ca,
                                         eps=cfg.norm_eps, p_drop=p, seed=_seed(sd, 4))
-        a, _ = ops.linear(x2, self.w("linear1.weight"), self.w("linear1.bias"))
-        gact = ops.act_fwd(a, "relu", p_drop=p, seed=_seed(sd, 5))
+        # linear1 + bias + ReLU + dropout in one GEMM epilogue (pre-activation kept in a)
+        gact, a = ops.linear(x2, self.w("linear1.weight"), self.w("linear1.bias"), act="relu", p_drop=p,
+                             seed=_seed(sd, 5))
         f, _ = ops.linear(gact, self.w("linear2.weight"), self.w("linear2.bias"))
         y, s3, mu3, rs3 = ops.norm_fwd(x2, self.w("norm3.weight"), self.w("norm3.bias"), branch=f, eps=cfg.norm_eps,
                                        p_drop=p, seed=_seed(sd, 6))
@@ -506,14 +507,14 @@ class Block:
         return y
 
     def _mha_bwd(self, prefix, dout, xq, xkv, B, S, seed, st, key, self_attn, wjobs, dres_q, dres_kv):
-        """Returns (dxq, dxkv) with the residual grads folded in."""
+        """Returns (dxq, dxkv) with the residual grads folded in.  The out_proj bias grad
+        (column sums of ``dout``) was accumulated by the norm backward that produced it."""
         cfg = self.cfg
         H, Dh, d = cfg.n_heads, cfg.head_dim, cfg.d_model
         W = self.w(prefix + ".in_proj_weight")
         gW, gb = self.g(prefix + ".in_proj_weight"), self.g(prefix + ".in_proj_bias")
         o = st[key + "o"]
         wjobs.append(lambda dout=dout, o=o: ops.linear_dw(dout, o, self.g(prefix + ".out_proj.weight")))
-        wjobs.append(lambda dout=dout: ops.colsum(dout, self.g(prefix + ".out_proj.bias")))
         do = ops.linear_dx(dout, self.w(prefix + ".out_proj.weight"), wt=self.wt(prefix + ".out_proj.weight"))
         if self_attn:
             qkv = st[key + "qkv"]
@@ -545,26 +546,30 @@ class Block:
     def _ref_backward(self, dy, B, S, st, sd, wjobs):
         cfg = self.cfg
         p = cfg.dropout
-        # norm3(x2 + drop(f))
+        # norm3(x2 + drop(f)); the linear2 bias grad (column sums of the branch gradient)
+        # accumulates in the same pass
         ds3, df = ops.norm_bwd(dy, st["s3"], self.w("norm3.weight"), st["mu3"], st["rs3"], dw=self.g("norm3.weight"),
-                               dbias=self.g("norm3.bias"), p_drop=p, seed=_seed(sd, 6), want_branch=True)
+                               dbias=self.g("norm3.bias"), p_drop=p, seed=_seed(sd, 6), want_branch=True,
+                               colsum_branch=self.g("linear2.bias"))
         gact, a, x2 = st["g"], st["a"], st["x2"]
         wjobs.append(lambda df=df, gact=gact: ops.linear_dw(df, gact, self.g("linear2.weight")))
-        wjobs.append(lambda df=df: ops.colsum(df, self.g("linear2.bias")))
-        dg = ops.linear_dx(df, self.w("linear2.weight"), wt=self.wt("linear2.weight"))
-        da = ops.act_bwd(dg, a, "relu", dbias=None, p_drop=p, seed=_seed(sd, 5))
-        wjobs.append(lambda da=da: ops.colsum(da, self.g("linear1.bias")))
+        # linear2 dX GEMM with dReLU x dropout mask in its epilogue and the linear1 bias
+        # grad (column sums of the result) accumulated there too
+        da = ops.linear_dx(df, self.w("linear2.weight"), act_input=a, act="relu", wt=self.wt("linear2.weight"),
+                           colsum=self.g("linear1.bias"), p_drop=p, seed=_seed(sd, 5))
         wjobs.append(lambda da=da, x2=x2: ops.linear_dw(da, x2, self.g("linear1.weight")))
         dx2 = ops.linear_dx(da, self.w("linear1.weight"), residual=ds3, wt=self.wt("linear1.weight"))
         # norm2(x1 + drop(ca))
         ds2, dca = ops.norm_bwd(dx2, st["s2"], self.w("norm2.weight"), st["mu2"], st["rs2"], dw=self.g("norm2.weight"),
-                                dbias=self.g("norm2.bias"), p_drop=p, seed=_seed(sd, 4), want_branch=True)
+                                dbias=self.g("norm2.bias"), p_drop=p, seed=_seed(sd, 4), want_branch=True,
+                                colsum_branch=self.g("multihead_attn.out_proj.bias"))
         h, x1 = st["x"], st["x1"]
         dx1, dh_mem = self._mha_bwd("multihead_attn", dca, x1, h, B, S, _seed(sd, 3), st, "ca_", False, wjobs,
                                     dres_q=ds2, dres_kv=None)
         # norm1(h + drop(sa))
         ds1, dsa = ops.norm_bwd(dx1, st["s1"], self.w("norm1.weight"), st["mu1"], st["rs1"], dw=self.g("norm1.weight"),
-                                dbias=self.g("norm1.bias"), p_drop=p, seed=_seed(sd, 2), want_branch=True)
+                                dbias=self.g("norm1.bias"), p_drop=p, seed=_seed(sd, 2), want_branch=True,
+                                colsum_branch=self.g("self_attn.out_proj.bias"))
         dres = ds1 + dh_mem
         dh, _ = self._mha_bwd("self_attn", dsa, h, h, B, S, _seed(sd, 1), st, "sa_", True, wjobs, dres_q=dres,
                               dres_kv=None)
@@ -650,6 +655,45 @@ def head_param_specs(cfg: NativeConfig) -> List[ParamSpec]:
     return out
 
 
+# MIPIPE_HEAD_CHUNK: how the last stage runs its LM head + CE.
+#   -1 (default): logits GEMM + fused CE in the forward, the dX / dW GEMMs in the backward
+#       (the [T, Vp] dlogits live from F to B);
+#    0: head forward AND backward inside the forward action, one chunk: only dL/dh
+#       ([T, D]) is stashed, the logits are transient;
+#    N: the same in token chunks of N (a chunk's logits fit the 256 MB Infinity Cache).
+# Measured, GPT-2 small bench, 1 GPU (profiles/r2_head_chunk_ab.txt): -1 834K tok/s,
+# 8192 810K, 4096 793K, 2048 788K -- the smaller dX / dW GEMMs cost more than the
+# logits traffic saves, and 288 GB of HBM holds the stash; chunking is for memory-bound
+# configurations (long sequences, large vocabularies, deep 1F1B stashes).
+_HEAD_CHUNK = int(os.environ.get("MIPIPE_HEAD_CHUNK", "-1"))
+
+
+def head_fwd_bwd(h: torch.Tensor, target: torch.Tensor, W: torch.Tensor, Wt: Optional[torch.Tensor],
+                 hb: Optional[torch.Tensor], gW: torch.Tensor, gb: Optional[torch.Tensor], dh_out: torch.Tensor,
+                 vocab: int, grad_scale: float, loss_out: torch.Tensor, chunk: int = 0,
+                 ov: Optional["WGradOverlap"] = None) -> None:
+    """LM head + softmax-CE forward AND backward for the rows of ``h`` [T, D]: per token
+    chunk, logits = h W^T (+ hb) -> fused CE (row losses into ``loss_out``, dlogits in
+    place) -> dh = dlogits W into ``dh_out`` and gW (+= dlogits^T h), gb (+= colsum).
+    With ``ov`` the weight-gradient GEMMs run on its side stream (the caller joins)."""
+    T = h.shape[0]
+    step = T if chunk <= 0 else min(chunk, T)
+    for c0 in range(0, T, step):
+        r = slice(c0, min(T, c0 + step))
+        hc = h[r]
+        logits, _ = ops.linear(hc, W, hb)
+        ops.xent_fwd_bwd(logits, target[r], vocab, grad_scale=grad_scale, loss=loss_out[r])
+        jobs = [lambda lg=logits, hc=hc: ops.linear_dw(lg, hc, gW)]
+        if gb is not None:
+            jobs.append(lambda lg=logits: ops.colsum(lg, gb))
+        if ov is not None:
+            ov.run(jobs)
+        ops.linear_dx(logits, W, out=dh_out[r], wt=Wt)
+        if ov is None:
+            for j in jobs:
+                j()
+
+
 class HeadShard:
     """LM head + loss replicated on every pipeline rank (distributed head,
     parallel/headsplit.py).  Runs one token chunk of a microbatch: logits, fused
@@ -670,14 +714,11 @@ class HeadShard:
         """h [Tc, D] final-norm output rows, target [Tc] ids; writes dL/dh into
         ``dh_out`` and returns the chunk's summed token loss (f32 scalar tensor)."""
         A = self.arena
-        W = self.weight()
         hb = A.w("output.bias") if A.has("output.bias") else None
-        logits, _ = ops.linear(h, W, hb)
-        row_loss = ops.xent_fwd_bwd(logits, target.reshape(-1), self.cfg.vocab_size, grad_scale=grad_scale)
-        ops.linear_dx(logits, W, out=dh_out, wt=A.wt(self.wname))
-        ops.linear_dw(logits, h, A.g(self.wname))
-        if hb is not None:
-            ops.colsum(logits, A.g("output.bias"))
+        row_loss = torch.empty(h.shape[0], device=h.device, dtype=torch.float32)
+        head_fwd_bwd(h, target.reshape(-1), self.weight(), A.wt(self.wname), hb, A.g(self.wname),
+                     A.g("output.bias") if hb is not None else None, dh_out, self.cfg.vocab_size, grad_scale,
+                     row_loss, chunk=_HEAD_CHUNK)
         return row_loss.sum()
 
 
@@ -779,8 +820,21 @@ class NativeModel:
         if self.split_head:  # the head runs as distributed chunks (HeadShard.run)
             return hn
         hb = self.arena.w("output.bias") if self.arena.has("output.bias") else None
-        logits, _ = ops.linear(hn, self.head_weight(), hb)
         T = hn.shape[0]
+        if target is not None and not keep_logits and _HEAD_CHUNK >= 0:
+            # fused head: forward + backward of the LM head and CE now, chunk by chunk; the
+            # backward starts from dhn (no [T, V] logits kept)
+            dhn = torch.empty_like(hn)
+            row_loss = torch.empty(T, device=hn.device, dtype=torch.float32)
+            ov = WGradOverlap.make(self.device, True)
+            head_fwd_bwd(hn, target.reshape(-1), self.head_weight(), self.head_weight_t(), hb, self.head_grad(),
+                         self.arena.g("output.bias") if hb is not None else None, dhn, cfg.vocab_size,
+                         loss_scale / T, row_loss, chunk=_HEAD_CHUNK, ov=ov)
+            if ov is not None:
+                ov.join()
+            ctx.misc.update(dhn=dhn)
+            return row_loss.mean()
+        logits, _ = ops.linear(hn, self.head_weight(), hb)
         if target is None:
             ctx.misc.update(hn=hn, logits=logits)
             return logits
@@ -801,6 +855,15 @@ class NativeModel:
                 dy, _ = ops.norm_bwd(dy, ctx.misc.pop("hpre"), self.arena.w("norm.weight"), ctx.misc.pop("mu"),
                                      ctx.misc.pop("rs"), kind=cfg.norm, dw=self.arena.g("norm.weight"),
                                      dbias=self.arena.g("norm.bias") if self.arena.has("norm.bias") else None)
+        elif self.last and "dhn" in ctx.misc:
+            # the fused head already produced dL/d(final-norm output) in the forward
+            dhn = ctx.misc.pop("dhn")
+            if cfg.final_norm:
+                dy, _ = ops.norm_bwd(dhn, ctx.misc.pop("hpre"), self.arena.w("norm.weight"), ctx.misc.pop("mu"),
+                                     ctx.misc.pop("rs"), kind=cfg.norm, dw=self.arena.g("norm.weight"),
+                                     dbias=self.arena.g("norm.bias") if self.arena.has("norm.bias") else None)
+            else:
+                dy = dhn
         elif self.last:
             dl = ctx.misc.pop("dlogits")
             hn = ctx.misc.pop("hn")

@@ -111,10 +111,12 @@ def norm_bwd(dy: torch.Tensor, s: torch.Tensor, w: torch.Tensor, mean, rstd, kin
              dres: Optional[torch.Tensor] = None, dw: Optional[torch.Tensor] = None,
              dbias: Optional[torch.Tensor] = None, p_drop: float = 0.0, seed: int = 0, ds=None, dbranch=None,
              want_branch: bool = False, colsum_dres: Optional[torch.Tensor] = None,
-             colsum_ds: Optional[torch.Tensor] = None):
+             colsum_ds: Optional[torch.Tensor] = None, colsum_branch: Optional[torch.Tensor] = None):
     """ds = d(norm input) (+ dres); dw/dbias (f32) accumulate.  Optionally also accumulates
     the column sums of ``dres`` and of ``ds`` (f32) -- the bias grads of the projections
-    around this residual point -- in the same pass.  Returns (ds, dbranch)."""
+    around this residual point -- in the same pass; ``colsum_branch`` (needs
+    ``want_branch``): the column sums of the returned branch gradient (= ds without
+    dropout, ds * mask with it).  Returns (ds, dbranch)."""
     rms = kind == "rmsnorm"
     D = dy.shape[-1]
     rows = dy.numel() // D
@@ -123,10 +125,20 @@ def norm_bwd(dy: torch.Tensor, s: torch.Tensor, w: torch.Tensor, mean, rstd, kin
     need_branch = want_branch and p_drop > 0
     if need_branch and dbranch is None:
         dbranch = torch.empty_like(dy)
+    if colsum_branch is not None:
+        if not want_branch or colsum_ds is not None:
+            raise ValueError("colsum_branch needs want_branch and excludes colsum_ds")
     if _gpu(dy):
-        _ext().norm_bwd(rms, dy, s, w, mean, rstd, dres, ds, dbranch if need_branch else None, dw, dbias,
-                        float(p_drop), int(seed), colsum_dres, colsum_ds)
-        return ds, (dbranch if need_branch else (ds if want_branch else None))
+        cs_ds = colsum_branch if colsum_branch is not None else colsum_ds
+        rc = _ext().norm_bwd(rms, dy, s, w, mean, rstd, dres, ds, dbranch if need_branch else None, dw, dbias,
+                             float(p_drop), int(seed), colsum_dres, cs_ds)
+        out_branch = dbranch if need_branch else (ds if want_branch else None)
+        if rc == -3:     # no fused column sums for this shape: separate passes
+            if colsum_dres is not None:
+                _ext().colsum(dres, colsum_dres)
+            if cs_ds is not None:
+                _ext().colsum(out_branch if colsum_branch is not None else ds, cs_ds)
+        return ds, out_branch
     d = dy.float().reshape(rows, D)
     x = s.float().reshape(rows, D)
     mu = torch.zeros(rows) if rms else mean.float()
@@ -149,7 +161,11 @@ def norm_bwd(dy: torch.Tensor, s: torch.Tensor, w: torch.Tensor, mean, rstd, kin
     if need_branch:
         m = _cpu_dropout_mask(dy.shape, p_drop, seed, dy.device)
         dbranch.copy_((v.reshape(dy.shape) * m).to(dbranch.dtype))
+        if colsum_branch is not None:
+            colsum_branch += dbranch.float().reshape(rows, D).sum(0)
         return ds, dbranch
+    if colsum_branch is not None:
+        colsum_branch += ds.float().reshape(rows, D).sum(0)
     return ds, (ds if want_branch else None)
 
 
@@ -221,17 +237,22 @@ def embed_bwd(idx: torch.Tensor, dout: torch.Tensor, dwte: torch.Tensor, dwpe: O
 # GEMMs (linear layers)
 # ======================================================================================
 def _gemm(A, B, C, bias=None, residual=None, aux=None, transA=False, transB=False, epi=EPI_NONE, accum=False,
-          alpha=1.0, cfg: int = -1, colsum=None):
+          alpha=1.0, cfg: int = -1, colsum=None, p_drop: float = 0.0, seed: int = 0):
     """``colsum`` (f32 [N]): also accumulate the column sums of the bf16 output (fused in
-    the GEMM epilogue where the engine supports it, else one extra pass)."""
+    the GEMM epilogue where the engine supports it, else one extra pass).  ``p_drop``
+    (EPI_BIAS_RELU / EPI_DRELU, contiguous output): dropout after the activation / the
+    dropout mask times the activation derivative, regenerated from (seed, element index)
+    exactly as act_fwd / act_bwd do."""
     e = _ext()
     if GEMM_V >= 2:
         rc = e.gemm2(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum), float(alpha),
-                     int(cfg), colsum)
+                     int(cfg), colsum, float(p_drop), int(seed))
         if rc:
             if rc == 2 and colsum is not None:
                 e.colsum(C, colsum)
             return C
+    if p_drop > 0:
+        raise RuntimeError("GEMM dropout epilogue needs the v2 engine for this shape")
     e.gemm(A, B, C, bias, residual, aux, bool(transA), bool(transB), int(epi), bool(accum), float(alpha))
     if colsum is not None:
         e.colsum(C, colsum)
@@ -251,9 +272,12 @@ def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
 
 def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None, act: str = "none",
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
-           aux: Optional[torch.Tensor] = None):
-    """y = act(x @ w^T + bias) (+ residual).  x [T,K], w [N,K].  With an activation the
-    pre-activation is written to ``aux`` (needed by the backward).  Returns (y, aux)."""
+           aux: Optional[torch.Tensor] = None, p_drop: float = 0.0, seed: int = 0):
+    """y = drop(act(x @ w^T + bias)) (+ residual).  x [T,K], w [N,K].  With an activation
+    the pre-activation is written to ``aux`` (needed by the backward); ``p_drop`` (ReLU
+    only) applies the fused dropout of the reference FFN.  Returns (y, aux)."""
+    if p_drop > 0 and act != "relu":
+        raise ValueError("the fused GEMM dropout follows a ReLU epilogue")
     T, K = x.shape
     N = w.shape[0]
     if out is None:
@@ -264,7 +288,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         if act != "none":
             if bias is None or residual is not None:
                 raise ValueError("activation epilogue needs a bias and no residual")
-            _gemm(x, w, out, bias=bias, aux=aux, epi=EPI_BIAS_GELU if ACT[act] == 1 else EPI_BIAS_RELU)
+            _gemm(x, w, out, bias=bias, aux=aux, epi=EPI_BIAS_GELU if ACT[act] == 1 else EPI_BIAS_RELU,
+                  p_drop=p_drop, seed=seed)
         elif residual is not None:
             _gemm(x, w, out, bias=bias, residual=residual, epi=EPI_BIAS_RES if bias is not None else EPI_RES)
         elif bias is not None:
@@ -281,6 +306,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         pre = y.to(x.dtype)
         aux.copy_(pre)
         y = _act_cpu(pre.float(), act)
+        if p_drop > 0:
+            y = y * _cpu_dropout_mask(y.shape, p_drop, seed, y.device)
     if residual is not None:
         y = y + residual.float()
     out.copy_(y.to(out.dtype))
@@ -308,7 +335,8 @@ def _act_grad_cpu(x, act):
 
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tensor] = None, act: str = "none",
               out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
-              wt: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None):
+              wt: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None, p_drop: float = 0.0,
+              seed: int = 0):
     """dx = dy @ w  (w [N,K]), optionally times act'(act_input) (the previous layer's
     pre-activation) and plus ``residual``.  With ``wt`` (= w^T, [K,N], kept by the param
     arena) the GEMM runs in the both-K-contiguous form on the v2 engine."""
@@ -325,7 +353,8 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
             out.copy_(acc)
             return out
         if act != "none":
-            _gemm(dy, wt, out, aux=act_input, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU, colsum=colsum)
+            _gemm(dy, wt, out, aux=act_input, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU, colsum=colsum,
+                  p_drop=p_drop, seed=seed)
         elif residual is not None:
             _gemm(dy, wt, out, residual=residual, epi=EPI_RES, colsum=colsum)
         else:
@@ -333,7 +362,8 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
         return out
     if _gpu(dy):
         if act != "none":
-            _gemm(dy, w, out, aux=act_input, transB=True, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU)
+            _gemm(dy, w, out, aux=act_input, transB=True, epi=EPI_DGELU if ACT[act] == 1 else EPI_DRELU,
+                  p_drop=p_drop, seed=seed)
         elif residual is not None:
             _gemm(dy, w, out, residual=residual, transB=True, epi=EPI_RES)
         elif GEMM_BACKEND == "blas":
@@ -346,6 +376,8 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
     g = dy.float() @ w.float()
     if act != "none":
         g = g * _act_grad_cpu(act_input.float(), act)
+        if p_drop > 0:
+            g = g * _cpu_dropout_mask(g.shape, p_drop, seed, g.device)
     if residual is not None:
         g = g + residual.float()
     out.copy_(g.to(out.dtype))

@@ -236,7 +236,7 @@ def test_adamw():
     assert abs(ss.item() - (g.double() ** 2).sum().item()) / ss.item() < 1e-4
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, "bias_gelu"), (1000, 2304, 256, "bias"), (256, 384, 128, "res"),
                                        (520, 136, 64, "none"), (512, 768, 3072, "dgelu"), (1000, 1000, 640, "none"),
                                        (768, 512, 128, "bias")])
@@ -278,7 +278,7 @@ def test_gemm2_dw_splitk(cfg, M, N, K):
     close(g, base + dy.float().t() @ x.float(), atol=3e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 4, 5])
+@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 10])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 50304), (2048, 768, 8192), (300, 200, 4096)])
 def test_gemm2_nt_splitk_accumulate(cfg, M, N, K):
     """Both-K-contiguous operands into an f32 accumulator with split-K (distributed-head dX)."""
@@ -291,6 +291,28 @@ def test_gemm2_nt_splitk_accumulate(cfg, M, N, K):
     close(g, base + a.float() @ b.float().t(), atol=5e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("cfg", [10, 11, 12, -1])
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (1024, 2304, 768), (1000, 2048, 768), (1024, 768, 2048)])
+def test_gemm_small_engine_bias_relu_and_colsum(cfg, M, N, K):
+    """Small-tile NT engine (reference-model 1024-token shapes): fused bias + ReLU with the
+    pre-activation in aux, and the fused output column sums (-1: the planner's pick)."""
+    from mipipe.ops import kernels as _k
+    torch.manual_seed(0)
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    _k._gemm(x.to(DEV), w.to(DEV), y, bias=b.to(DEV), aux=aux, epi=3, cfg=cfg)
+    pre = x.float() @ w.float().t() + b.float()
+    close(aux, pre.to(torch.bfloat16))
+    close(y, torch.relu(pre.to(torch.bfloat16).float()))
+    cs = torch.zeros(N, device=DEV)
+    y2 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    _k._gemm(x.to(DEV), w.to(DEV), y2, cfg=cfg, colsum=cs)
+    ref = x.float() @ w.float().t()
+    close(y2, ref)
+    close(cs, y2.float().sum(0), atol=5e-1, rtol=2e-2)
+
+
 def test_linear_dx_with_transposed_weight():
     torch.manual_seed(0)
     dy, w, a = rnd(1024, 2304), rnd(2304, 768, scale=0.02), rnd(1024, 768)
@@ -299,6 +321,28 @@ def test_linear_dx_with_transposed_weight():
     ref = ops.linear_dx(dy, w, act_input=a, act="gelu_tanh")
     got = ops.linear_dx(dy.to(DEV), w.to(DEV), act_input=a.to(DEV), act="gelu_tanh", wt=wt)
     close(got, ref)
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+@pytest.mark.parametrize("D", [768, 2048])
+def test_norm_bwd_branch_colsum(p_drop, D):
+    """colsum_branch: the column sums of the (dropout-masked) branch gradient accumulate
+    in the norm backward pass itself (the reference block's out_proj / linear2 bias grads)."""
+    torch.manual_seed(0)
+    T = 1024
+    x, w, b = rnd(T, D), rnd(D, scale=0.5) + 1, rnd(D, scale=0.1)
+    dy = rnd(T, D)
+    xg, wg, bg, dyg = (t.to(DEV) for t in (x, w, b, dy))
+    y, s_, mean, rstd = ops.norm_fwd(xg, wg, bg, kind="layernorm", eps=1e-5)
+    cs = torch.zeros(D, device=DEV)
+    dw, db = torch.zeros(D, device=DEV), torch.zeros(D, device=DEV)
+    ds, dbr = ops.norm_bwd(dyg, xg, wg, mean, rstd, dw=dw, dbias=db, p_drop=p_drop, seed=7, want_branch=True,
+                           colsum_branch=cs)
+    close(cs, dbr.float().sum(0), atol=5e-1, rtol=2e-2)
+    ref_ds, ref_br = ops.norm_bwd(dyg, xg, wg, mean, rstd, dw=torch.zeros(D, device=DEV),
+                                  dbias=torch.zeros(D, device=DEV), p_drop=p_drop, seed=7, want_branch=True)
+    close(ds, ref_ds, atol=0, rtol=0)
+    close(dbr, ref_br, atol=0, rtol=0)
 
 
 def test_norm_bwd_fused_colsums():
@@ -362,3 +406,34 @@ def test_gemm_fused_colsum(cfg, epi):
              aux=aux.to(DEV) if epi == "dgelu" else None, epi=epi_id, cfg=cfg, colsum=cs)
     ref = y.float().cpu().sum(0) + 0.5
     close(cs, ref, atol=0.05 * (M ** 0.5), rtol=2e-2)
+
+
+@pytest.mark.parametrize("cfg", [-1, 10, 11, 5])
+def test_gemm_dropout_epilogues_match_act_kernels(cfg):
+    """Reference FFN fusions: linear1 + bias + ReLU + dropout in the GEMM epilogue equals
+    linear1 -> act_fwd(relu, p); the linear2 dX GEMM with dReLU x mask (+ the linear1 bias
+    grad column sums) equals dX -> act_bwd(relu, p, dbias) -- same masks (seed, element
+    index, device step counter)."""
+    from mipipe.ops import kernels as _k
+    torch.manual_seed(0)
+    T, D, F, p = 1024, 768, 2048, 0.1
+    ops.set_dropout_step(3, torch.device(DEV))
+    x, w1, b1 = rnd(T, D).to(DEV), rnd(F, D, scale=D ** -0.5).to(DEV), rnd(F, scale=0.1).to(DEV)
+    out = torch.empty(T, F, dtype=torch.bfloat16, device=DEV)
+    aux = torch.empty(T, F, dtype=torch.bfloat16, device=DEV)
+    _k._gemm(x, w1, out, bias=b1, aux=aux, epi=3, cfg=cfg, p_drop=p, seed=1234)
+    a, _ = ops.linear(x, w1, b1)
+    ref = ops.act_fwd(a, "relu", p_drop=p, seed=1234)
+    close(aux, a, atol=2e-2, rtol=2e-2)     # another engine may have computed `a`
+    close(out, ref, atol=2e-2, rtol=2e-2)
+    keep = (out != 0) | (ref == 0)
+    assert keep.float().mean() > 0.999
+    df, w2 = rnd(T, D).to(DEV), rnd(D, F, scale=F ** -0.5).to(DEV)
+    w2t = ops.transpose(w2)
+    cs = torch.zeros(F, device=DEV)
+    da = ops.linear_dx(df, w2, act_input=aux, act="relu", wt=w2t, colsum=cs, p_drop=p, seed=99)
+    dg = ops.linear_dx(df, w2, wt=w2t)
+    cs_ref = torch.zeros(F, device=DEV)
+    da_ref = ops.act_bwd(dg, aux, "relu", dbias=cs_ref, p_drop=p, seed=99)
+    close(da, da_ref, atol=2e-2, rtol=2e-2)
+    close(cs, cs_ref, atol=0.5, rtol=2e-2)
