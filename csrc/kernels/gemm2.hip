@@ -46,8 +46,13 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
 // K-contiguous image [rows][64 k]: 128-byte rows, 8 chunks
 __device__ __forceinline__ int offK(int row, int chunk) { return row * 128 + 16 * (chunk ^ swz8(row)); }
 // outer-contiguous image [64 k][COLS]: 2*COLS-byte rows; swizzle the low 4 chunk bits
+// (COLS = 64, the small engine's TT tiles: 8 chunks per row, chunk pairs XORed by row bits
+// 1 and 3 -- the 8 rows a 32-lane ds_read_b64_tr_b16 group touches land in 8 distinct
+// 8-bank groups, conflict-free)
+__device__ __forceinline__ int swz8o(int row) { return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1)); }
 template <int COLS>
 __device__ __forceinline__ int offO(int row, int chunk) {
+  if constexpr (COLS == 64) return row * 128 + 16 * (chunk ^ swz8o(row));
   return row * (COLS * 2) + 16 * ((chunk & ~15) | ((chunk & 15) ^ swz16(row)));
 }
 
@@ -107,7 +112,7 @@ __device__ __forceinline__ const bf16_t* src_of(const bf16_t* base, int64_t ld, 
   } else {  // [64k][ROWS cols]
     constexpr int PITCH = ROWS * 2;
     const int row = pos / PITCH, phys = (pos % PITCH) >> 4;
-    const int chunk = (phys & ~15) | ((phys & 15) ^ swz16(row));
+    const int chunk = ROWS == 64 ? (phys ^ swz8o(row)) : ((phys & ~15) | ((phys & 15) ^ swz16(row)));
     int o = outer0 + chunk * 8;
     o = o < outer_lim ? o : outer_lim - 8;
     return base + (int64_t)(k0 + row) * ld + o;
@@ -880,7 +885,7 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
 // gemm2, several workgroups per CU (32 KiB LDS at 64x64), and the fused epilogue applied
 // directly -- one launch per GEMM, no split-K.
 // ---------------------------------------------------------------------------------------
-template <int BM, int BN, int EPI, bool ACC>
+template <int BM, int BN, int EPI, bool ACC, bool TA = false, bool TB = false>
 __global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                     void* __restrict__ Cv, const bf16_t* __restrict__ bias,
                                                     const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
@@ -924,16 +929,17 @@ __global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A
     const int p = wave + 4 * i;
     const int pos = p * 1024 + lane * 16;
     pisA[i] = p * 1024 < A_BYTES;
-    if (pisA[i]) psrc[i] = src_of<false, BM, true>(A, lda, pos, m0, M, kbase);
-    else psrc[i] = src_of<false, BN, true>(B, ldb, pos - A_BYTES, n0, N, kbase);
+    if (pisA[i]) psrc[i] = src_of<TA, BM, true>(A, lda, pos, m0, M, kbase);
+    else psrc[i] = src_of<TB, BN, true>(B, ldb, pos - A_BYTES, n0, N, kbase);
   }
   auto issue = [&](int stage, int kt) {
     char* sb = smem + stage * STAGE;
-    const int64_t dk = (int64_t)kt * BK;
+    const int64_t dA = TA ? (int64_t)kt * BK * lda : (int64_t)kt * BK;
+    const int64_t dB = TB ? (int64_t)kt * BK * ldb : (int64_t)kt * BK;
 #pragma unroll
     for (int i = 0; i < PW; ++i) {
       const int p = wave + 4 * i;
-      __builtin_amdgcn_global_load_lds((const void*)(psrc[i] + dk),
+      __builtin_amdgcn_global_load_lds((const void*)(psrc[i] + (pisA[i] ? dA : dB)),
                                        (__attribute__((address_space(3))) void*)(sb + p * 1024), 16, 0, 0);
     }
   };
@@ -964,9 +970,9 @@ __global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A
 #pragma unroll
     for (int s_ = 0; s_ < 2; ++s_) {
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[s_][i] = frag16<false, BM>(sa, wm + 16 * i, s_);
+      for (int i = 0; i < TM; ++i) af[s_][i] = frag16<TA, BM>(sa, wm + 16 * i, s_);
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bfr[s_][j] = frag16<false, BN>(sbB, wn + 16 * j, s_);
+      for (int j = 0; j < TN; ++j) bfr[s_][j] = frag16<TB, BN>(sbB, wn + 16 * j, s_);
     }
 #pragma unroll
     for (int s_ = 0; s_ < 2; ++s_) {
@@ -996,7 +1002,7 @@ __global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A
                                           N, ldc, ldr, ldx, alpha, nsplit, p_drop, seed);
 }
 
-template <int BM, int BN, int EPI, bool ACC>
+template <int BM, int BN, int EPI, bool ACC, bool TA = false, bool TB = false>
 static int launchs(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
                    int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
                    float p_drop, uint64_t seed, hipStream_t st) {
@@ -1005,7 +1011,7 @@ static int launchs(const void* A, const void* B, void* C, const void* bias, cons
   constexpr int RED_BYTES = 256 * 8 * 4;   // the column-sum reduction reuses the staging area
   constexpr int LDS0 = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
   constexpr int LDS = LDS0 > RED_BYTES ? LDS0 : RED_BYTES;
-  auto kern = gemms_kernel<BM, BN, EPI, ACC>;
+  auto kern = gemms_kernel<BM, BN, EPI, ACC, TA, TB>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
@@ -1092,6 +1098,7 @@ static int dispatch(int cfg, const void* A, const void* B, void* C, const void* 
                     int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
                     int split, float p_drop, uint64_t seed, hipStream_t st) {
   if constexpr (TA && TB && ACC && EPI == EPI_NONE) {
+    if (cfg == 13) return launchs<64, 64, EPI, ACC, true, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 6) return launch3<EPI, ACC, true, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
   }
   if constexpr (!TA && !TB) {
@@ -1172,7 +1179,7 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   int split = 1;
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
   if (force_cfg >= 0 && force_cfg < 7) cfg = force_cfg;
-  if (force_cfg >= 10) cfg = 0;   // placeholder; the small-engine branch below sets it
+  if (force_cfg >= 10) cfg = 0;   // placeholder; the small-engine branches below set it
   // the ping-pong 256x256 engine for both-K-contiguous operands (MIPIPE_GEMM3=0 disables;
   // MIPIPE_GEMM_M16=1 selects its 16x16x32-MFMA build)
   static const bool use3 = [] { const char* e = getenv("MIPIPE_GEMM3"); return !(e && e[0] == '0'); }();
@@ -1212,6 +1219,16 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
       const int w64 = ((M + 63) / 64) * ((N + 63) / 64);
       const int w6432 = ((M + 63) / 64) * ((N + 31) / 32);
       cfg = w64 >= minwg ? 10 : (w6432 >= minwg ? 11 : 12);
+      split = 1;
+    }
+  }
+  // short-token dW GEMMs (both operands k-major, f32 accumulate): the small engine's TT
+  // build, 64x64 tiles, no split-K (the slabs + reduce pass cost as much as the GEMM here)
+  if (transA && transB && c_f32_accum && use_small && (force_cfg < 0 || force_cfg == 13) && M % 8 == 0 &&
+      N % 8 == 0) {
+    const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
+    if (force_cfg == 13 || (t256 < 64 && K <= 4096)) {
+      cfg = 13;
       split = 1;
     }
   }

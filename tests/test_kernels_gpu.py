@@ -266,8 +266,9 @@ def test_gemm2_configs(cfg, M, N, K, epi):
     close(y, ref)
 
 
-@pytest.mark.parametrize("cfg", [0, 2, 3, 6, -1])
-@pytest.mark.parametrize("M,N,K", [(768, 768, 8192), (2304, 768, 1024), (136, 200, 512), (3072, 768, 2048), (1000, 776, 1024)])
+@pytest.mark.parametrize("cfg", [0, 2, 3, 6, 13, -1])
+@pytest.mark.parametrize("M,N,K", [(768, 768, 8192), (2304, 768, 1024), (136, 200, 512), (3072, 768, 2048), (1000, 776, 1024),
+                                   (768, 2048, 1024)])
 def test_gemm2_dw_splitk(cfg, M, N, K):
     from mipipe.ops import kernels as _k
     torch.manual_seed(0)

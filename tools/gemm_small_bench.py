@@ -45,3 +45,16 @@ for name, M, N, K in SHAPES:
     row["best_ours_tf"] = round(fl / min(row[f"cfg{c_}_us"] for c_ in (10, 11, 12, -1)) / 1e6, 1)
     row["blas_tf"] = round(fl / row["blas_us"] / 1e6, 1)
     print(json.dumps(row), flush=True)
+# dW (TT): dw[N, K] += dy^T x with K = 1024 tokens (f32 accumulate)
+for name, N_, K_ in [("dw_qkv", 3 * d, d), ("dw_q", d, d), ("dw_kv", 2 * d, d), ("dw_ff1", f, d), ("dw_ff2", d, f)]:
+    dy = (torch.randn(T, N_, device="cuda") * 0.1).to(torch.bfloat16)
+    x = (torch.randn(T, K_, device="cuda") * 0.1).to(torch.bfloat16)
+    g = torch.zeros(N_, K_, device="cuda")
+    row = {"shape": name, "M": N_, "N": K_, "K": T}
+    for cfg in (13, -1, 2, 6):
+        row[f"cfg{cfg}_us"] = round(timeit(lambda: _k._gemm(dy, x, g, transA=True, transB=True, accum=True, cfg=cfg)), 2)
+    dyt = dy.t()
+    row["blas_us"] = round(timeit(lambda: g.add_(torch.mm(dyt, x, out_dtype=torch.float32))), 2)
+    fl = 2.0 * N_ * K_ * T
+    row["best_ours_tf"] = round(fl / min(row[f"cfg{c_}_us"] for c_ in (13, -1, 2, 6)) / 1e6, 1)
+    print(json.dumps(row), flush=True)
