@@ -45,7 +45,13 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
+                    help="bf16: the native HIP path (PipelineTrainer, AdamW included); fp32: the reference's own "
+                         "nn.Module model in f32 on the GPU through the reference-compatible schedule API "
+                         "(fwd+bwd only, exactly the reference's timed loop)")
     a = ap.parse_args()
+    if a.precision == "fp32":
+        return main_fp32(a)
     import torch
     import mipipe  # noqa: F401
     from mipipe.engine import PipelineTrainer
@@ -87,6 +93,52 @@ def main():
     summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
                          "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, bf16, AdamW step included, "
                          + ("eager" if a.no_graphs else "HIP graphs"),
+               "rows": out}
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(summary, f, indent=1)
+
+
+def main_fp32(a):
+    """The reference's workload at the reference's precision: Transformer(ModelArgs(L, H))
+    (nn.TransformerDecoderLayer, f32, dropout 0.1) split by manual_model_split into one
+    stage, Schedule1F1B(m=4) from mipipe.parallel.api, run_train_iterations' 2 warmup + 5
+    timed fwd+bwd steps (no optimizer, as helper:98-143) -- on one MI355X (ATen f32 compute
+    through hipBLASLt / MIOpen; the HIP kernels of this framework are bf16-only)."""
+    import torch
+    import mipipe  # noqa: F401
+    from mipipe.bench.compat import run_train_iterations
+    from mipipe.models.ref_transformer import ModelArgs, Transformer, manual_model_split, tokenwise_loss_fn
+    from mipipe.parallel.api import Schedule1F1B
+
+    torch.backends.cuda.matmul.allow_tf32 = False
+    ref = reference_rows()
+    dev = torch.device("cuda", 0)
+    B, S, m = 32, 128, 4
+    out = []
+    for L in (4, 8, 12):
+        for H in (4, 8, 12):
+            torch.manual_seed(L * 100 + H)
+            args = ModelArgs(n_layers=L, n_heads=H)
+            stage = manual_model_split(Transformer(args), 0, 1, dev)
+            sched = Schedule1F1B(stage, n_microbatches=m, loss_fn=tokenwise_loss_fn(args.vocab_size))
+            x = torch.randint(0, args.vocab_size, (B, S), device=dev)
+            y = torch.randint(0, args.vocab_size, (B, S), device=dev)
+            met = run_train_iterations(sched, x, y, 0, 1, num_iterations=a.iters, warmup=a.warmup, device=dev,
+                                       measure_bubble=False)
+            mine = {k: v for k, v in ref.items() if k[0] == L and k[1] == H}
+            best_k = max(mine, key=mine.get)
+            row = {"L": L, "H": H, "tokens_per_s": round(met["throughput"], 1),
+                   "ms_per_iter": round(met["elapsed_time"] / a.iters * 1e3, 3), "ref_best_tok_s": mine[best_k],
+                   "ref_best_run": f"P={best_k[2]} {best_k[3]}", "ref_gpipe_p2_tok_s": mine.get((L, H, 2, "GPipe")),
+                   "x_vs_ref_best": round(met["throughput"] / mine[best_k], 1)}
+            out.append(row)
+            print(json.dumps(row), flush=True)
+            del sched, stage
+            torch.cuda.empty_cache()
+    summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
+                         "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, **f32** (the reference's precision; ATen "
+                         "compute, TF32 off), fwd+bwd only (no optimizer), reference-compatible API",
                "rows": out}
     if a.json:
         with open(a.json, "w") as f:
