@@ -10,7 +10,9 @@ int mp_norm_fwd(int rms, const void* a, const void* b, const void* w, const void
                 float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed, hipStream_t st);
 int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
                 const void* dres, void* ds, void* dbranch, float* dw, float* dbias, float* cs_res, float* cs_ds,
-                int rows, int D, float p, uint64_t seed, hipStream_t st);
+                int rows, int D, float p, uint64_t seed, float* part, hipStream_t st);
+int64_t mp_norm_bwd_part_elems(int rows, int D);
+int64_t mp_colsum_part_elems(int rows, int cols);
 int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss, int T, int V, int Vp, float grad_scale,
                     int64_t ignore_index, int write_grad, hipStream_t st);
 int mp_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int T, int S, int D, int pos_offset,
@@ -24,8 +26,8 @@ int mp_adamw(float* p, float* g, float* m, float* v, void* w16, int64_t n, int64
 int mp_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t st);
 int mp_act_fwd(const void* a, void* g, int64_t n, int act, float p, uint64_t seed, hipStream_t st);
 int mp_act_bwd(const void* dg, const void* a, void* da, float* dbias, int rows, int cols, int act, float p,
-               uint64_t seed, hipStream_t st);
-int mp_colsum(const void* x, float* dbias, int rows, int cols, hipStream_t st);
+               uint64_t seed, float* part, hipStream_t st);
+int mp_colsum(const void* x, float* dbias, int rows, int cols, float* part, hipStream_t st);
 int mp_swiglu_fwd(const void* gu, void* y, int T, int F, hipStream_t st);
 int mp_swiglu_bwd(const void* gu, const void* dy, void* dgu, int T, int F, hipStream_t st);
 int mp_rope(void* qkv, const float* cs, const float* sn, int T, int S, int H, int Hkv, int Dh, int pos_offset,
@@ -100,13 +102,17 @@ int64_t norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c
   const int D = dy.size(-1);
   const int rows = dy.numel() / D;
   TORCH_CHECK(s.numel() == dy.numel() && ds.numel() == dy.numel() && dw.numel() == D, "bad norm_bwd shapes");
+  // per-block partial column sums (two-stage reduction instead of contended atomics)
+  const int64_t pe = mp_norm_bwd_part_elems(rows, D);
+  torch::Tensor part;
+  if (pe > 0) part = torch::empty({pe}, dy.options().dtype(torch::kFloat32));
   const int rc = mp_norm_bwd(rms, dy.data_ptr(), s.data_ptr(), w.data_ptr(),
                              mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(),
                              ptr_or_null(dres), ds.data_ptr(), mptr_or_null(dbranch), dw.data_ptr<float>(),
                              dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
                              cs_res.has_value() ? cs_res->data_ptr<float>() : nullptr,
                              cs_ds.has_value() ? cs_ds->data_ptr<float>() : nullptr, rows, D, (float)p,
-                             (uint64_t)seed, cur_stream());
+                             (uint64_t)seed, part.defined() ? part.data_ptr<float>() : nullptr, cur_stream());
   if (rc == -3) return -3;
   check(rc, "norm_bwd");
   return 0;
@@ -181,8 +187,12 @@ void act_bwd(torch::Tensor dg, torch::Tensor a, torch::Tensor da, c10::optional<
   req(dg, torch::kBFloat16, "dg");
   const int cols = dg.size(-1);
   const int rows = dg.numel() / cols;
+  const int64_t pe = dbias.has_value() ? mp_colsum_part_elems(rows, cols) : 0;
+  torch::Tensor part;
+  if (pe > 0) part = torch::empty({pe}, dg.options().dtype(torch::kFloat32));
   check(mp_act_bwd(dg.data_ptr(), a.data_ptr(), da.data_ptr(), dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
-                   rows, cols, act, (float)p, (uint64_t)seed, cur_stream()),
+                   rows, cols, act, (float)p, (uint64_t)seed, part.defined() ? part.data_ptr<float>() : nullptr,
+                   cur_stream()),
         "act_bwd");
 }
 
@@ -190,7 +200,13 @@ void colsum(torch::Tensor x, torch::Tensor dbias) {
   req(x, torch::kBFloat16, "x");
   req(dbias, torch::kFloat32, "dbias");
   const int cols = x.size(-1);
-  check(mp_colsum(x.data_ptr(), dbias.data_ptr<float>(), x.numel() / cols, cols, cur_stream()), "colsum");
+  const int rows = x.numel() / cols;
+  const int64_t pe = mp_colsum_part_elems(rows, cols);
+  torch::Tensor part;
+  if (pe > 0) part = torch::empty({pe}, x.options().dtype(torch::kFloat32));
+  check(mp_colsum(x.data_ptr(), dbias.data_ptr<float>(), rows, cols, part.defined() ? part.data_ptr<float>() : nullptr,
+                  cur_stream()),
+        "colsum");
 }
 
 void swiglu_fwd(torch::Tensor gu, torch::Tensor y) {

@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
     bf16_t* __restrict__ ds_out, bf16_t* __restrict__ dbranch, float* __restrict__ dw, float* __restrict__ dbias,
     float* __restrict__ cs_res, float* __restrict__ cs_ds, int rows, int D, int rows_per_block, float p_drop,
-    uint64_t seed) {
+    uint64_t seed, float* __restrict__ part) {
   if (p_drop > 0.f) seed = step_seed(seed);
   __shared__ float red[4][2][MAXJ * 64 * 8 > 1024 ? 1024 : MAXJ * 64 * 8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -240,8 +240,19 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
         const int j = j0 + jj;
         const int c = ln + 64 * j;
         if (j < MAXJ && c < nchunk) {
-          if (o0 != nullptr) atomicAdd(o0 + c * 8 + e, red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i]);
-          if (o1 != nullptr) atomicAdd(o1 + c * 8 + e, red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i]);
+          const float v0 = red[0][0][i] + red[1][0][i] + red[2][0][i] + red[3][0][i];
+          const float v1 = red[0][1][i] + red[1][1][i] + red[2][1][i] + red[3][1][i];
+          if (part != nullptr) {
+            // per-block partials [block][slot][D] (slots dw, dbias, cs_res, cs_ds), summed by
+            // colpart_reduce_kernel: every block atomically adding into the same few KB
+            // serialises at the memory side (the COLS build ran 3x the plain one)
+            float* pb = part + (int64_t)blockIdx.x * 4 * D;
+            if (o0 != nullptr) pb[(2 * q) * D + c * 8 + e] = v0;
+            if (o1 != nullptr) pb[(2 * q + 1) * D + c * 8 + e] = v1;
+          } else {
+            if (o0 != nullptr) atomicAdd(o0 + c * 8 + e, v0);
+            if (o1 != nullptr) atomicAdd(o1 + c * 8 + e, v1);
+          }
         }
       }
     }
@@ -293,13 +304,13 @@ extern "C" int mp_norm_fwd(int rms, const void* a, const void* b, const void* w,
   return (int)hipGetLastError();
 }
 
-template <bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG, bool COLS>
-static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
-                       const void* dres, void* ds, void* dbr, float* dw, float* db, float* csr, float* css, int rows,
-                       int D, float p, uint64_t seed, hipStream_t st) {
-  // rows per workgroup: every workgroup ends with one f32 atomic per column and output
-  // (dw, dbias, column sums), all into the same few KB, so short problems want few, long
-  // workgroups (1024 rows: 512 workgroups of 2 rows measured 20-22 us, contention-bound)
+extern "C" int mp_colpart_reduce(const float* part, int nblk, int nslot, int D, float* o0, float* o1, float* o2,
+                                 float* o3, hipStream_t st);
+
+static int norm_bwd_blocks(int rows) {
+  // rows per workgroup: every workgroup ends with one f32 sum per column and output
+  // (dw, dbias, column sums), so short problems want few, long workgroups (1024 rows: 512
+  // workgroups of 2 rows measured 20-22 us)
   static const int min_rpb = [] {
     const char* e = getenv("MIPIPE_NORM_BWD_RPB");
     const int v = e ? atoi(e) : 8;
@@ -307,22 +318,43 @@ static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, c
   }();
   int nblk = rows < 512 ? (rows + 3) / 4 : 512;
   if ((rows + nblk - 1) / nblk < min_rpb) nblk = (rows + min_rpb - 1) / min_rpb;
-  if (nblk < 1) nblk = 1;
+  return nblk < 1 ? 1 : nblk;
+}
+
+// f32 elements of the partial-sum buffer the backward of [rows, D] uses (0: atomics only)
+extern "C" int mp_colpart_enabled();
+
+extern "C" int64_t mp_norm_bwd_part_elems(int rows, int D) {
+  if (!mp_colpart_enabled()) return 0;
+  const int nblk = norm_bwd_blocks(rows);
+  const int rpb = (rows + nblk - 1) / nblk;
+  const int g = (rows + rpb - 1) / rpb;
+  return g >= 256 ? (int64_t)g * 4 * D : 0;  // as kColpartMinBlocks (elementwise.hip)
+}
+
+template <bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG, bool COLS>
+static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
+                       const void* dres, void* ds, void* dbr, float* dw, float* db, float* csr, float* css, int rows,
+                       int D, float p, uint64_t seed, float* part, hipStream_t st) {
+  const int nblk = norm_bwd_blocks(rows);
   const int rpb = (rows + nblk - 1) / nblk;
   dim3 grid((rows + rpb - 1) / rpb), block(256);
+  if (grid.x < 256) part = nullptr;
 #define MP_BWD(J)                                                                                                   \
   case J:                                                                                                           \
     norm_bwd_kernel<J, RMS, HAS_DRES, HAS_BIAS, BG, COLS><<<grid, block, 0, st>>>(                                  \
         (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)ds,        \
-        (bf16_t*)dbr, dw, db, csr, css, rows, D, rpb, p, seed);                                                     \
+        (bf16_t*)dbr, dw, db, csr, css, rows, D, rpb, p, seed, part);                                               \
     break;
   switch (maxj) { MP_BWD(1) MP_BWD(2) MP_BWD(4) MP_BWD(8) MP_BWD(10) MP_BWD(16) }
 #undef MP_BWD
+  if (part != nullptr) mp_colpart_reduce(part, grid.x, 4, D, dw, db, csr, css, st);
 }
 
 extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean,
                            const float* rstd, const void* dres, void* ds, void* dbranch, float* dw, float* dbias,
-                           float* cs_res, float* cs_ds, int rows, int D, float p, uint64_t seed, hipStream_t st) {
+                           float* cs_res, float* cs_ds, int rows, int D, float p, uint64_t seed, float* part,
+                           hipStream_t st) {
   if (D % 8 != 0 || D > 16 * 512) return -1;
   const int J = pick_j(D);
   const bool hd = dres != nullptr, hb = dbias != nullptr, bg = dbranch != nullptr;
@@ -333,7 +365,7 @@ extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w
 #define MP_C(HD, HB, BG_)                                                                                        \
     if (hd == HD && hb == HB && bg == BG_) {                                                                       \
       launch_bwd<false, HD, HB, BG_, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res, cs_ds,   \
-                                           rows, D, p, seed, st);                                                  \
+                                           rows, D, p, seed, part, st);                                            \
       return (int)hipGetLastError();                                                                               \
     }
     MP_C(1, 1, 0) MP_C(1, 0, 0) MP_C(0, 1, 1) MP_C(0, 0, 1) MP_C(1, 1, 1) MP_C(1, 0, 1) MP_C(0, 1, 0) MP_C(0, 0, 0)
@@ -343,7 +375,7 @@ extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w
 #define MP_B(R, HD, HB, BG_)                                                                                   \
   if (rms == R && hd == HD && hb == HB && bg == BG_) {                                                          \
     launch_bwd<R, HD, HB, BG_, false>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, nullptr, nullptr, \
-                                      rows, D, p, seed, st);                                                   \
+                                      rows, D, p, seed, part, st);                                             \
     return (int)hipGetLastError();                                                                            \
   }
   MP_B(0, 0, 0, 0) MP_B(0, 0, 0, 1) MP_B(0, 0, 1, 0) MP_B(0, 0, 1, 1)

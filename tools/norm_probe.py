@@ -38,3 +38,9 @@ for kind, T, D, cols in [("layernorm", 16384, 768, True), ("layernorm", 16384, 7
                                 colsum_ds=c2))
     nbytes = 4 * T * D * 2
     print(f"norm_bwd {kind} {T}x{D} cols={cols}: {us:.1f} us, {nbytes / us / 1e6:.2f} TB/s", flush=True)
+
+for T, D in [(16384, 768), (1024, 768), (8192, 3072), (1024, 2048)]:
+    x = torch.randn(T, D, device="cuda").to(torch.bfloat16)
+    db = torch.zeros(D, device="cuda")
+    us = t(lambda: ops.colsum(x, db))
+    print(f"colsum {T}x{D}: {us:.1f} us, {T * D * 2 / us / 1e6:.2f} TB/s", flush=True)
