@@ -104,7 +104,8 @@ def main():
                         lib_us=round(min(tl) * 1e6, 1))
         print(tag, res[tag], flush=True)
     # attention: GPT-2 small / Llama-3 8B shapes
-    for (B, S, H, KV, D, causal) in [(8, 1024, 12, 12, 64, True), (1, 8192, 32, 8, 128, True),
+    for (B, S, H, KV, D, causal) in [(8, 1024, 12, 12, 64, True), (16, 1024, 12, 12, 64, True),
+                                     (1, 8192, 32, 8, 128, True),
                                      (8, 128, 8, 8, 96, False)]:
         tag = f"attn_B{B}S{S}H{H}KV{KV}D{D}c{int(causal)}"
         if a.only and a.only not in tag:
