@@ -27,6 +27,8 @@
 //         accumulates dQ^T += K^T dS^T.
 #include "mp_common.h"
 
+#include <type_traits>
+
 using namespace mp;
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
@@ -471,23 +473,32 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
         // masks only where needed: the causal diagonal and query rows past Sq (their
         // stats were clamped); keys past Sk only feed their own unwritten outputs
         const bool edge = (q0 + 64 > Sq) || (CAUSAL && (k0 + 32 * w + 31 > q0 + 32 * u + shift));
+        // the element math twice, masked and unmasked, behind one wave-uniform branch: as a
+        // per-element select the mask's index compares and cndmasks were issued on every
+        // tile (~half of the loop's VALU, profiles/r2_attention_pmc_counters.json)
+        auto elems = [&](auto masked) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int qr = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl;
-          const int q = q0 + qr;
-          const float lv = (&lsv[r >> 2].x)[r & 3], dv_ = (&dlv[r >> 2].x)[r & 3];
-          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -lv));
-          if (edge && (q >= Sq || (CAUSAL && key > q + shift))) p = 0.f;
-          float dpv = pacc[r];
-          float pd = p;
-          if (DROP) {
-            const float msk = dropout_scale(seed, drop_idx(bhq, q, key, Sk), p_drop);
-            pd = p * msk;
-            dpv = dpv * msk;
+          for (int r = 0; r < 16; ++r) {
+            const int qr = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            const int q = q0 + qr;
+            const float lv = (&lsv[r >> 2].x)[r & 3], dv_ = (&dlv[r >> 2].x)[r & 3];
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -lv));
+            if constexpr (decltype(masked)::value) {
+              if (q >= Sq || (CAUSAL && key > q + shift)) p = 0.f;
+            }
+            float dpv = pacc[r];
+            float pd = p;
+            if (DROP) {
+              const float msk = dropout_scale(seed, drop_idx(bhq, q, key, Sk), p_drop);
+              pd = p * msk;
+              dpv = dpv * msk;
+            }
+            pm[r] = pd;                      // dropped P for dV
+            ds[r] = p * (dpv - dv_);         // dS
           }
-          pm[r] = pd;                      // dropped P for dV
-          ds[r] = p * (dpv - dv_);         // dS
-        }
+        };
+        if (edge) elems(std::true_type{});
+        else elems(std::false_type{});
         // dV^T += dO^T P ;  dK^T += Q^T dS     (A via transposed LDS reads of the row images)
         const bf16x8 pb0 = pack8(pm, 0), pb1 = pack8(pm, 1);
         const bf16x8 db0 = pack8(ds, 0), db1 = pack8(ds, 1);
@@ -645,21 +656,28 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
       }
       // causal / key-end mask only on edge tiles; invalid query rows have lse = +inf
       const bool edge = (n0 + 64 > Sk) || (CAUSAL && n0 + 63 > m0 + 32 * w + shift);
+      // masked / unmasked element math behind one wave-uniform branch (see the dK/dV kernel)
+      auto elems = [&](auto masked) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+        for (int r = 0; r < 16; ++r) {
+          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
 #pragma unroll
-        for (int half = 0; half < 2; ++half) {
-          const int kk = n0 + 32 * half + kr;
-          float sv = half ? s1[r] : s0[r];
-          float dpv = half ? p1[r] : p0[r];
-          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse));
-          if (edge && (kk >= Sk || (CAUSAL && kk > qrow + shift))) p = 0.f;
-          if (DROP) dpv *= dropout_scale(seed, drop_idx(bh, qrow, kk, Sk), p_drop);
-          const float dsv = p * (dpv - dlt);
-          if (half) s1[r] = dsv; else s0[r] = dsv;
+          for (int half = 0; half < 2; ++half) {
+            const int kk = n0 + 32 * half + kr;
+            float sv = half ? s1[r] : s0[r];
+            float dpv = half ? p1[r] : p0[r];
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse));
+            if constexpr (decltype(masked)::value) {
+              if (kk >= Sk || (CAUSAL && kk > qrow + shift)) p = 0.f;
+            }
+            if (DROP) dpv *= dropout_scale(seed, drop_idx(bh, qrow, kk, Sk), p_drop);
+            const float dsv = p * (dpv - dlt);
+            if (half) s1[r] = dsv; else s0[r] = dsv;
+          }
         }
-      }
+      };
+      if (edge) elems(std::true_type{});
+      else elems(std::false_type{});
       const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 1), d10 = pack8(s1, 0), d11 = pack8(s1, 1);
 #pragma unroll
       for (int d = 0; d < DP / 32; ++d) {

@@ -116,7 +116,8 @@ def main():
                 torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         if (step + 1) % t.log_every == 0 or step == t.steps - 1:
-            gn = float(trainer.optimizer.sumsq.sqrt().item()) if t.max_grad_norm else None
+            gn = (float(trainer.optimizer.sumsq.sqrt().item()) * trainer.optimizer.grad_scale  # un-scaled sums (1/dp folded)
+                  if t.max_grad_norm else None)
             rec = log.log(step + 1, tokens_per_step, dt, loss=None if loss is None else float(loss), lr=lr,
                           grad_norm=gn)
             if rank == 0:
