@@ -44,3 +44,12 @@ for T, D in [(16384, 768), (1024, 768), (8192, 3072), (1024, 2048)]:
     db = torch.zeros(D, device="cuda")
     us = t(lambda: ops.colsum(x, db))
     print(f"colsum {T}x{D}: {us:.1f} us, {T * D * 2 / us / 1e6:.2f} TB/s", flush=True)
+
+for T, D, branch in [(16384, 768, True), (16384, 768, False), (8192, 4096, True), (1024, 768, True)]:
+    x = torch.randn(T, D, device="cuda").to(torch.bfloat16)
+    br = torch.randn(T, D, device="cuda").to(torch.bfloat16) if branch else None
+    w = torch.randn(D, device="cuda").to(torch.bfloat16)
+    b = torch.randn(D, device="cuda").to(torch.bfloat16)
+    us = t(lambda: ops.norm_fwd(x, w, b, branch=br))
+    nbytes = (4 if branch else 2) * T * D * 2
+    print(f"norm_fwd {T}x{D} branch={branch}: {us:.1f} us, {nbytes / us / 1e6:.2f} TB/s", flush=True)
