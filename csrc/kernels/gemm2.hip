@@ -173,7 +173,14 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int gr, int gc, bf16_t
   u16x8 o;
 #pragma unroll
   for (int e = 0; e < 8; ++e) o[e] = f2bf(v[e]);
+#ifndef MP_GEMM_PLAIN_STORE
+  // non-temporal: the bf16 C tiles stream out without displacing the A/B panels other
+  // workgroups still read from L2 (GPT-2 bench +0.9 %, 3 interleaved pairs on one box;
+  // MP_GEMM_PLAIN_STORE builds the plain store for A/B)
+  __builtin_nontemporal_store(o, reinterpret_cast<u16x8*>(C + (int64_t)gr * ldc + gc));
+#else
   *reinterpret_cast<u16x8*>(C + (int64_t)gr * ldc + gc) = o;
+#endif
 }
 
 // accumulator layout of the 32x32x16 engines: acc[i][j] element r -> wave-local

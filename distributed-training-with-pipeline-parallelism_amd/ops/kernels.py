@@ -28,7 +28,10 @@ def load_ext():
     global _EXT, _EXT_ERR
     if _EXT is not None or _EXT_ERR is not None:
         return _EXT
-    path = os.path.join(_PKG_DIR, "_C.so")
+    # MIPIPE_EXT_VARIANT=name loads _C_<name>.so: a build of the same sources with extra
+    # compile-time defines (tools/build_ext.py --variant), for in-process A/B of kernel variants
+    variant = os.environ.get("MIPIPE_EXT_VARIANT", "")
+    path = os.path.join(_PKG_DIR, f"_C_{variant}.so" if variant else "_C.so")
     if not os.path.exists(path):
         _EXT_ERR = f"{path} not found (build it with: python tools/build_ext.py)"
         return None

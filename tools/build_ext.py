@@ -50,12 +50,16 @@ def _run(cmd):
     return r.stderr
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int = 8, verbose: bool = False, variant: str = "", defines=()) -> str:
+    """``variant`` + ``defines``: an A/B build (``_C_<variant>.so``, its own object dir) of the
+    same sources with extra ``-D`` flags, loaded with MIPIPE_EXT_VARIANT=<variant>."""
+    OBJ = os.path.join(ROOT, "build", "obj" + (f"_{variant}" if variant else ""))
+    OUT = os.path.join(PKG, f"_C_{variant}.so" if variant else "_C.so")
     os.makedirs(OBJ, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "include", "*.h"))
     kernels = sorted(glob.glob(os.path.join(CSRC, "kernels", "*.hip")))
     base = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-I", os.path.join(CSRC, "include"),
-            "-Wno-unused-result", "-Wno-unused-variable"]
+            "-Wno-unused-result", "-Wno-unused-variable"] + [f"-D{d}" for d in defines]
     jobs_list = []
     objs = []
     for k in kernels:
@@ -95,5 +99,9 @@ if __name__ == "__main__":
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", type=int, default=8)
     ap.add_argument("-v", action="store_true")
+    ap.add_argument("--variant", default="", help="A/B build name: writes _C_<variant>.so")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for a --variant build")
     a = ap.parse_args()
-    print(build(a.force, a.j, a.v))
+    if a.defines and not a.variant:
+        ap.error("-D needs --variant (the default _C.so is always the plain build)")
+    print(build(a.force, a.j, a.v, a.variant, a.defines))
