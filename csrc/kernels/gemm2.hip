@@ -24,6 +24,17 @@ using namespace mp;
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(8))) short s16x8;
 
+// tile rows per raster group of the ping-pong engine: GPT-2 bench (3 interleaved runs
+// each, one box) 841K tok/s at 8, 851K at 4, 856K at 2, 863-864K vs 870K at 1 vs 2 on a
+// second box, 829K at 16 -- the isolated GEMM is flat (+-1 %); inside the step (dW GEMMs on
+// the side stream sharing L2) short groups win
+#ifndef MP_G3_GROUP
+#define MP_G3_GROUP 2
+#endif
+#ifndef MP_G2_GROUP
+#define MP_G2_GROUP 8
+#endif
+
 namespace g2 {
 
 enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RELU = 3, EPI_BIAS_RES = 4, EPI_RES = 5,
@@ -560,7 +571,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
   const int nwg = gm * gn;
   const int wg = xcd_remap((int)blockIdx.x, nwg);
-  constexpr int GROUP = 8;
+  constexpr int GROUP = MP_G3_GROUP;   // tile rows per raster group (L2 reuse of the A panels)
   const int group = wg / (GROUP * gn);
   const int first_m = group * GROUP;
   const int gsz = min(gm - first_m, GROUP);
