@@ -71,15 +71,41 @@ __device__ __forceinline__ float block_max(float v, float* red) {
   return t;
 }
 
-// Counter-based RNG (Philox-lite: 2 rounds of a 64-bit multiply-xorshift hash).
-// Deterministic in (seed, offset, index) so dropout masks are regenerated in the
-// backward pass instead of stored.
+// Counter-based RNG, deterministic in (seed, index) so dropout masks are regenerated in
+// the backward pass instead of stored.  32-bit arithmetic only: two keys from the seed and
+// the index's high word (the attention kernels put (b, h) there and compute the keys once,
+// `drop_key`), the low word through the "lowbias32" integer finaliser (two v_mul_lo_u32 +
+// three xorshifts) with the second key xored in mid-way, so streams whose inputs overlap
+// after the additive offset still differ.  The round-1 64-bit splitmix chain (emulated
+// 64-bit multiplies per element) made the dropout attention kernels run 1.8-2.7x their
+// dropout-free form and pushed them into register spills.
+// Per-stream keys (scalar work: seed and the index's high word are wave-uniform).
+struct DropKey {
+  uint32_t k0, k1;
+};
+__device__ __forceinline__ DropKey drop_key(uint64_t seed, uint32_t hi) {
+  DropKey k;
+  k.k0 = ((uint32_t)seed ^ 0x9E3779B9u) + hi * 0x85EBCA6Bu;
+  k.k1 = ((uint32_t)(seed >> 32) ^ hi) * 0xC2B2AE35u + 0x27D4EB2Fu;
+  return k;
+}
+__device__ __forceinline__ uint32_t hash_lo(DropKey k, uint32_t lo) {
+  uint32_t x = lo + k.k0;
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= k.k1;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t hash_u32(uint64_t seed, uint64_t idx) {
-  uint64_t x = idx * 0x9E3779B97F4A7C15ull ^ (seed + 0xD1B54A32D192ED03ull);
-  x ^= x >> 31; x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 27; x *= 0x94D049BB133111EBull;
-  x ^= x >> 33;
-  return (uint32_t)x;
+  return hash_lo(drop_key(seed, (uint32_t)(idx >> 32)), (uint32_t)idx);
+}
+// keep threshold / scale of a drop probability, hoisted out of element loops
+__device__ __forceinline__ uint32_t drop_thr(float p) { return (uint32_t)(p * 4294967296.0f); }
+__device__ __forceinline__ float drop_scale_lo(DropKey k, uint32_t lo, uint32_t thr, float inv) {
+  return hash_lo(k, lo) >= thr ? inv : 0.0f;
 }
 
 // Graph-safe dropout: every kernel that drops mixes a per-process training-step counter

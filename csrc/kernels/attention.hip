@@ -115,6 +115,8 @@ struct Stage64 {
   }
 };
 
+// dropout element index of score (bh, q, k): bh in the high word, q * Sk + k in the low
+// word (the kernels use drop_key(seed, bh) + the low word directly; this is the reference)
 __device__ __forceinline__ uint64_t drop_idx(int bh, int q, int k, int Sk) {
   return ((uint64_t)bh * 0x100000000ull) + (uint64_t)q * (uint64_t)Sk + (uint64_t)k;
 }
@@ -159,6 +161,10 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
     qf[s] = __builtin_bit_cast(bf16x8, t);
   }
   const float c = scale * LOG2E;
+  // dropout stream of this (b, h): keys once, 32-bit index q * Sk + key (drop_idx's low word)
+  const DropKey dkey = drop_key(seed, (uint32_t)bh);
+  const uint32_t dthr = drop_thr(p_drop), qoff = (uint32_t)qrow * (uint32_t)Sk;
+  const float dinv = 1.0f / (1.0f - p_drop);
   f32x16 o[DP / 32];
 #pragma unroll
   for (int d = 0; d < DP / 32; ++d) o[d] = {};
@@ -217,6 +223,18 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
       const float m_new = fmaxf(m_run, mx * c);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
       const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+      // dropout: the 32 keep bits of this lane's scores first (only the bit mask stays live
+      // across the hashes: computed beside the probabilities the DP = 128 build spilled)
+      uint32_t keep = 0xffffffffu;
+      if (DROP) {
+        keep = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t kr = (uint32_t)(n0 + (r & 3) + 8 * (r >> 2) + 4 * hl);
+          keep |= (hash_lo(dkey, qoff + kr) >= dthr ? 1u : 0u) << r;
+          keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
+        }
+      }
       float rs = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
@@ -224,9 +242,8 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
         float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c, -m_use));
         rs += p0 + p1;
         if (DROP) {
-          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
-          p0 *= dropout_scale(seed, drop_idx(bh, qrow, n0 + kr, Sk), p_drop);
-          p1 *= dropout_scale(seed, drop_idx(bh, qrow, n0 + 32 + kr, Sk), p_drop);
+          p0 = (keep >> r) & 1u ? p0 * dinv : 0.f;
+          p1 = (keep >> (16 + r)) & 1u ? p1 * dinv : 0.f;
         }
         s0[r] = p0;
         s1[r] = p1;
@@ -400,6 +417,8 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     dv[d] = {};
   }
   const float c = scale * LOG2E;
+  const uint32_t dthr = drop_thr(p_drop);
+  const float dinv = 1.0f / (1.0f - p_drop);
   // first query that can see key k0: q >= k0 - shift
   const int q_begin = CAUSAL ? max(0, ((k0 - shift) / 64) * 64) : 0;
   const int ntq = (Sq - q_begin + 63) / 64;
@@ -431,6 +450,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
     const int hq = hk * grp + it / ntq;
     const int q0 = q_begin + (it % ntq) * 64;
     const int bhq = b * H + hq;
+    const DropKey dkey = drop_key(seed, (uint32_t)bhq);
     // tile `it` landed (up to LOOK-1 younger tiles may stay in flight), then publish to all
     // waves; wave 0 issues 2 extra DMAs per tile (the row stats)
     if (LOOK >= 3 && it + 2 < total) {
@@ -476,6 +496,16 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
         // the element math twice, masked and unmasked, behind one wave-uniform branch: as a
         // per-element select the mask's index compares and cndmasks were issued on every
         // tile (~half of the loop's VALU, profiles/r2_attention_pmc_counters.json)
+        // dropout keep bits first (only the mask stays live across the hashes)
+        uint32_t keep = 0xffffu;
+        if (DROP) {
+          keep = 0;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t q = (uint32_t)(q0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl);
+            keep |= (hash_lo(dkey, q * (uint32_t)Sk + (uint32_t)key) >= dthr ? 1u : 0u) << r;
+          }
+        }
         auto elems = [&](auto masked) {
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -489,7 +519,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dkdv_kernel(
             float dpv = pacc[r];
             float pd = p;
             if (DROP) {
-              const float msk = dropout_scale(seed, drop_idx(bhq, q, key, Sk), p_drop);
+              const float msk = (keep >> r) & 1u ? dinv : 0.f;
               pd = p * msk;
               dpv = dpv * msk;
             }
@@ -604,6 +634,9 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
     if (qvalid && hl == 0) DELTA[sidx] = dlt;
   }
   const float c = scale * LOG2E;
+  const DropKey dkey = drop_key(seed, (uint32_t)bh);
+  const uint32_t dthr = drop_thr(p_drop), qoff = (uint32_t)qrow * (uint32_t)Sk;
+  const float dinv = 1.0f / (1.0f - p_drop);
   f32x16 dq[DP / 32];
 #pragma unroll
   for (int d = 0; d < DP / 32; ++d) dq[d] = {};
@@ -657,6 +690,17 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
       // causal / key-end mask only on edge tiles; invalid query rows have lse = +inf
       const bool edge = (n0 + 64 > Sk) || (CAUSAL && n0 + 63 > m0 + 32 * w + shift);
       // masked / unmasked element math behind one wave-uniform branch (see the dK/dV kernel)
+      // dropout keep bits first (only the mask stays live across the hashes)
+      uint32_t keep = 0xffffffffu;
+      if (DROP) {
+        keep = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t kr = (uint32_t)(n0 + (r & 3) + 8 * (r >> 2) + 4 * hl);
+          keep |= (hash_lo(dkey, qoff + kr) >= dthr ? 1u : 0u) << r;
+          keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
+        }
+      }
       auto elems = [&](auto masked) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
@@ -670,7 +714,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
             if constexpr (decltype(masked)::value) {
               if (kk >= Sk || (CAUSAL && kk > qrow + shift)) p = 0.f;
             }
-            if (DROP) dpv *= dropout_scale(seed, drop_idx(bh, qrow, kk, Sk), p_drop);
+            if (DROP) dpv = (keep >> (16 * half + r)) & 1u ? dpv * dinv : 0.f;
             const float dsv = p * (dpv - dlt);
             if (half) s1[r] = dsv; else s0[r] = dsv;
           }
