@@ -31,6 +31,13 @@ def reference():
     return _run(1, port=29771)["losses"]
 
 
+@pytest.fixture(scope="module")
+def reference8():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return _run(1, "--layers", "8", port=29761)["losses"]
+
+
 @pytest.mark.parametrize("n,schedule,graphs,split,dp", [(2, "1F1B", 0, 1, 1), (2, "ZBH1", 1, 1, 1),
                                                         (4, "1F1B", 1, 1, 1), (4, "GPipe", 0, 0, 1),
                                                         (2, "ZBV", 0, 1, 1), (4, "1F1B", 1, 1, 2)])
@@ -43,4 +50,15 @@ def test_multirank_gpu_matches_single(reference, n, schedule, graphs, split, dp)
     assert res["losses"] == pytest.approx(reference, rel=2e-3)
     # with graphs, steps after the first replay run from the native stage runner's tape
     # (gloo transfers recorded as CALLs)
+    assert res["native_runner"] == bool(graphs), res["native_reason"]
+
+
+@pytest.mark.parametrize("n,graphs,split", [(2, 1, 1), (4, 1, 1), (4, 0, 0)])
+def test_multirank_gpu_interleaved_matches_single(reference8, n, graphs, split):
+    """Interleaved 1F1B with 2 virtual stages per rank (BASELINE config 3's schedule;
+    reference helper:182-185, 204-211): 8 layers over 2*PP stages, HIP graphs + native
+    tape, with and without the distributed head, vs one process."""
+    res = _run(n, "--schedule", "Interleaved1F1B", "--vstages", "2", "--layers", "8", "--graphs", str(graphs),
+               "--split-head", str(split), port=29860 + n + 10 * graphs + 20 * split)
+    assert res["losses"] == pytest.approx(reference8, rel=2e-3)
     assert res["native_runner"] == bool(graphs), res["native_reason"]

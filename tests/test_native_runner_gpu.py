@@ -50,9 +50,10 @@ def test_native_runner_matches_python_path(name):
     kinds = tr_n.runtime.native_runner.kinds()
     assert 0 in kinds   # graph launches on the tape
     # f32-atomic reductions (embedding / norm / bias grads) make two runs of either path
-    # differ at ~1e-5 after a few updates; a missing instruction on the tape shows up as
-    # errors orders of magnitude larger
-    assert l_native[:2] == pytest.approx(l_python[:2], rel=1e-6, abs=1e-6)
+    # differ at ~1e-5 after one update (6.8e-6 relative measured); a missing instruction on
+    # the tape shows up as errors orders of magnitude larger
+    assert l_native[0] == pytest.approx(l_python[0], rel=1e-6, abs=1e-6)
+    assert l_native[1] == pytest.approx(l_python[1], rel=3e-5)
     assert l_native == pytest.approx(l_python, rel=5e-4)
     assert l_native[-1] < l_native[0]
 

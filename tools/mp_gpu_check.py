@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--split-head", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--dp", type=int, default=1, help="data-parallel replicas (pp = world / dp)")
+    ap.add_argument("--vstages", type=int, default=None, help="virtual stages per rank (Interleaved1F1B)")
+    ap.add_argument("--layers", type=int, default=4)
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -25,14 +27,14 @@ def main():
     from mipipe.models.config import NativeConfig
     from mipipe.parallel.mesh import init_distributed
     rank, world, _, device = init_distributed()
-    cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=4, n_heads=4, d_ff=1024, max_seq_len=256)
+    cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=a.layers, n_heads=4, d_ff=1024, max_seq_len=256)
     m, mbs, S = 8, 2, 256   # same data for every world size
     dp = a.dp
     pp = world // dp
     tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m // dp,
                          mbs=mbs,
                          seq_len=S, device=device, seed=3, graphs=bool(a.graphs),
-                         split_head=bool(a.split_head), lr=1e-3)
+                         split_head=bool(a.split_head), lr=1e-3, v=a.vstages if pp > 1 else None)
     g = torch.Generator(device=device).manual_seed(11)
     x = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
     y = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
