@@ -52,6 +52,9 @@ int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void
              int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, float* colsum, float p_drop,
              uint64_t seed, hipStream_t st);
 int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg, int* split_out);
+int mp_gemm_tt_grouped(int n, const void* const* A, const void* const* B, float* const* C, const int* M, const int* N,
+                       const int* K, const int64_t* lda, const int64_t* ldb, const int64_t* ldc, float alpha,
+                       hipStream_t st);
 int mp_gemm(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
             int epilogue, int c_f32_accum, float alpha, hipStream_t st);
@@ -323,6 +326,39 @@ int64_t gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<t
   return 1;
 }
 
+// grouped weight-gradient GEMMs: C[i] (f32 [N_i, K_i]) += alpha * dy[i]^T x[i]
+// (dy [T_i, N_i], x [T_i, K_i] bf16, unit inner stride) in one launch of 64x64 tiles
+void gemm_tt_grouped(std::vector<torch::Tensor> dy, std::vector<torch::Tensor> x, std::vector<torch::Tensor> C,
+                     double alpha) {
+  const int n = (int)dy.size();
+  TORCH_CHECK(n == (int)x.size() && n == (int)C.size() && n >= 1 && n <= 8, "gemm_tt_grouped: 1..8 problems");
+  const void* A[8];
+  const void* B[8];
+  float* Cp[8];
+  int M[8], N[8], K[8];
+  int64_t lda[8], ldb[8], ldc[8];
+  for (int i = 0; i < n; ++i) {
+    TORCH_CHECK(dy[i].is_cuda() && dy[i].scalar_type() == torch::kBFloat16 && x[i].scalar_type() == torch::kBFloat16 &&
+                    C[i].scalar_type() == torch::kFloat32,
+                "gemm_tt_grouped: bf16 dy/x, f32 C");
+    TORCH_CHECK(dy[i].dim() == 2 && x[i].dim() == 2 && C[i].dim() == 2 && dy[i].stride(1) == 1 &&
+                    x[i].stride(1) == 1 && C[i].stride(1) == 1,
+                "gemm_tt_grouped: 2-D, unit inner stride");
+    TORCH_CHECK(dy[i].size(0) == x[i].size(0) && C[i].size(0) == dy[i].size(1) && C[i].size(1) == x[i].size(1),
+                "gemm_tt_grouped: shape mismatch");
+    A[i] = dy[i].data_ptr();
+    B[i] = x[i].data_ptr();
+    Cp[i] = C[i].data_ptr<float>();
+    M[i] = (int)dy[i].size(1);
+    N[i] = (int)x[i].size(1);
+    K[i] = (int)dy[i].size(0);
+    lda[i] = dy[i].stride(0);
+    ldb[i] = x[i].stride(0);
+    ldc[i] = C[i].stride(0);
+  }
+  check(mp_gemm_tt_grouped(n, A, B, Cp, M, N, K, lda, ldb, ldc, (float)alpha, cur_stream()), "gemm_tt_grouped");
+}
+
 void transpose(torch::Tensor in, torch::Tensor out) {
   TORCH_CHECK(in.dim() == 2 && out.dim() == 2 && in.stride(1) == 1 && out.stride(1) == 1, "transpose: 2-D rows");
   TORCH_CHECK(out.size(0) == in.size(1) && out.size(1) == in.size(0), "transpose: shape");
@@ -400,6 +436,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
+  m.def("gemm_tt_grouped", &gemm_tt_grouped, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("C"),
+        pybind11::arg("alpha") = 1.0);
   m.def("gemm2", &gemm2, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
         pybind11::arg("residual"), pybind11::arg("aux"), pybind11::arg("transA"), pybind11::arg("transB"),
         pybind11::arg("epilogue"), pybind11::arg("accum"), pybind11::arg("alpha"), pybind11::arg("force_cfg"),

@@ -35,6 +35,10 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 #define MP_G2_GROUP 8
 #endif
 
+#ifndef MP_GROUP_MAX
+#define MP_GROUP_MAX 8
+#endif
+
 namespace g2 {
 
 enum Epi { EPI_NONE = 0, EPI_BIAS = 1, EPI_BIAS_GELU = 2, EPI_BIAS_RELU = 3, EPI_BIAS_RES = 4, EPI_RES = 5,
@@ -903,24 +907,24 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
 // gemm2, several workgroups per CU (32 KiB LDS at 64x64), and the fused epilogue applied
 // directly -- one launch per GEMM, no split-K.
 // ---------------------------------------------------------------------------------------
-template <int BM, int BN, int EPI, bool ACC, bool TA = false, bool TB = false>
-__global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
-                                                    void* __restrict__ Cv, const bf16_t* __restrict__ bias,
-                                                    const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
-                                                    float* __restrict__ WS, int M, int N, int K, int64_t lda,
-                                                    int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop, uint64_t seed) {
-  if (p_drop > 0.f) seed = step_seed(seed);
+// one BM x BN output tile (workgroup-linear index wg of the problem's tile grid, split
+// ``split`` of ``nsplit``) of the small engine; shared by gemms_kernel and the grouped
+// weight-gradient kernel below
+template <int BM, int BN, int EPI, bool ACC, bool TA, bool TB>
+__device__ __forceinline__ void gemms_tile(char* smem, const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                           void* __restrict__ Cv, const bf16_t* __restrict__ bias,
+                                           const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+                                           float* __restrict__ WS, int M, int N, int K, int64_t lda, int64_t ldb,
+                                           int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop,
+                                           uint64_t seed, int wg, int nsplit, int split) {
   constexpr int NTH = 256, WM = 2, WN = 2;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;
   static_assert(TM >= 1 && TN >= 1 && TM * 16 * WM == BM && TN * 16 * WN == BN, "tile/wave mismatch");
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
   constexpr int PIECES = STAGE / 1024, PW = PIECES / 4;
   static_assert(PW * 4 == PIECES, "pieces must split over 4 waves");
-  extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
-  const int nwg = gm * gn;
-  const int wg = xcd_remap((int)blockIdx.x, nwg);
   constexpr int GROUP = 8;
   const int group = wg / (GROUP * gn);
   const int first_m = group * GROUP;
@@ -934,10 +938,9 @@ __global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A
   const int wr = wave / WN, wc = wave % WN;
   const int wm = wr * (BM / WM), wn = wc * (BN / WN);
 
-  const int nsplit = gridDim.y;
   const int ktiles = K / BK;
-  const int kt0 = (int)blockIdx.y * ktiles / nsplit;
-  const int nk = ((int)blockIdx.y + 1) * ktiles / nsplit - kt0;
+  const int kt0 = split * ktiles / nsplit;
+  const int nk = (split + 1) * ktiles / nsplit - kt0;
   const int kbase = kt0 * BK;
 
   const bf16_t* psrc[PW];
@@ -1018,6 +1021,53 @@ __global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A
   }
   epilogue<BM, BN, WM, WN, EPI, ACC, NTH>(Stage16<TM, TN>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M,
                                           N, ldc, ldr, ldx, alpha, nsplit, p_drop, seed);
+}
+
+template <int BM, int BN, int EPI, bool ACC, bool TA = false, bool TB = false>
+__global__ void __launch_bounds__(256) gemms_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                    void* __restrict__ Cv, const bf16_t* __restrict__ bias,
+                                                    const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+                                                    float* __restrict__ WS, int M, int N, int K, int64_t lda,
+                                                    int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nwg = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  gemms_tile<BM, BN, EPI, ACC, TA, TB>(smem, A, B, Cv, bias, R, AUX, WS, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop,
+                                       seed, xcd_remap((int)blockIdx.x, nwg), (int)gridDim.y, (int)blockIdx.y);
+}
+
+// ---------------------------------------------------------------------------------------
+// Grouped weight-gradient GEMMs: up to MP_GROUP_MAX independent TT problems
+// C_g[M_g, N_g] += alpha * A_g^T B_g (A_g [K_g][M_g], B_g [K_g][N_g] k-major, f32 C) in ONE
+// launch of 64x64 tiles.  A layer's dW GEMMs at 1024-token microbatches are 144-432 tiles
+// each: one launch per GEMM leaves most of the 256 CUs idle and pays the short k-loop's
+// latency per GEMM (97-230 TF, tools/wbatch_probe.py); grouped, ~1900 tiles of a layer
+// share the chip, several workgroups per CU hide each other's load latency.  Workgroup
+// b -> problem g with tile_start[g] <= b' < tile_start[g + 1] (b' = XCD-remapped b;
+// wave-uniform scan of <= 8 entries), then the problem-local tile of gemms_tile.
+// ---------------------------------------------------------------------------------------
+struct GroupTT {
+  const bf16_t* A[MP_GROUP_MAX];
+  const bf16_t* B[MP_GROUP_MAX];
+  float* C[MP_GROUP_MAX];
+  int64_t lda[MP_GROUP_MAX], ldb[MP_GROUP_MAX], ldc[MP_GROUP_MAX];
+  int M[MP_GROUP_MAX], N[MP_GROUP_MAX], K[MP_GROUP_MAX];
+  int tile_start[MP_GROUP_MAX + 1];
+  int n;
+  float alpha;
+};
+
+__global__ void __launch_bounds__(256) gemms_tt_grouped_kernel(const GroupTT g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int total = g.tile_start[g.n];
+  const int b = xcd_remap((int)blockIdx.x, total);
+  int p = 0;
+#pragma unroll
+  for (int i = 1; i < MP_GROUP_MAX; ++i)
+    if (i < g.n && b >= g.tile_start[i]) p = i;
+  gemms_tile<64, 64, EPI_NONE, true, true, true>(smem, g.A[p], g.B[p], g.C[p], nullptr, nullptr, nullptr, nullptr,
+                                                 g.M[p], g.N[p], g.K[p], g.lda[p], g.ldb[p], g.ldc[p], 0, 0, g.alpha,
+                                                 0.f, 0, b - g.tile_start[p], 1, 0);
 }
 
 template <int BM, int BN, int EPI, bool ACC, bool TA = false, bool TB = false>
@@ -1318,3 +1368,42 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
 }
 
 MP_DROP_STEP_SETTER(mp_set_drop_step_gemm)
+
+// C_g += alpha * A_g^T B_g for n <= MP_GROUP_MAX problems (A_g [K_g][M_g], B_g [K_g][N_g]
+// bf16 k-major, C_g f32 [M_g][N_g] row stride ldc_g) in one launch; -1 if a shape does not
+// fit the 64x64 TT tile contract (M, N multiples of 8, K of 64)
+extern "C" int mp_gemm_tt_grouped(int n, const void* const* A, const void* const* B, float* const* C, const int* M,
+                                  const int* N, const int* K, const int64_t* lda, const int64_t* ldb,
+                                  const int64_t* ldc, float alpha, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > MP_GROUP_MAX) return -1;
+  GroupTT g{};
+  g.n = n;
+  g.alpha = alpha;
+  int t = 0;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] % 8 || N[i] % 8 || K[i] % BK || M[i] <= 0 || N[i] <= 0) return -1;
+    g.A[i] = (const bf16_t*)A[i];
+    g.B[i] = (const bf16_t*)B[i];
+    g.C[i] = C[i];
+    g.M[i] = M[i];
+    g.N[i] = N[i];
+    g.K[i] = K[i];
+    g.lda[i] = lda[i];
+    g.ldb[i] = ldb[i];
+    g.ldc[i] = ldc[i];
+    g.tile_start[i] = t;
+    t += ((M[i] + 63) / 64) * ((N[i] + 63) / 64);
+  }
+  for (int i = n; i <= MP_GROUP_MAX; ++i) g.tile_start[i] = t;
+  constexpr int STAGE = (64 + 64) * BK * 2;
+  constexpr int EPI_BYTES = 32 * (64 + 4) * 4;
+  constexpr int LDS = 2 * STAGE > EPI_BYTES ? 2 * STAGE : EPI_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)gemms_tt_grouped_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  gemms_tt_grouped_kernel<<<t, 256, LDS, st>>>(g);
+  return (int)hipGetLastError();
+}

@@ -246,8 +246,7 @@ class WGradOverlap:
             return
         self.side.wait_stream(self.main)
         with torch.cuda.stream(self.side):
-            for j in jobs:
-                j()
+            ops.run_wjobs(jobs)
         ev = torch.cuda.Event()
         ev.record(self.side)
         self.inflight.append((ev, jobs))
@@ -408,9 +407,9 @@ class Block:
             if cfg.activation == "swiglu":
                 dgact = ops.linear_dx(dy, self.w("ffn.w2.weight"), wt=self.wt("ffn.w2.weight"))
                 gact, h2, gu = st["g"], st["h2"], st["gu"]
-                wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
+                wjobs.append(ops.DW(dy, gact, self.g("ffn.w2.weight")))
                 dgu = ops.swiglu_bwd(gu, dgact)
-                wjobs.append(lambda dgu=dgu, h2=h2: ops.linear_dw(dgu, h2, self.g("ffn.w13.weight")))
+                wjobs.append(ops.DW(dgu, h2, self.g("ffn.w13.weight")))
                 dh2 = ops.linear_dx(dgu, self.w("ffn.w13.weight"), wt=self.wt("ffn.w13.weight"))
             else:
                 gact, a, h2 = st["g"], st["a"], st["h2"]
@@ -419,10 +418,10 @@ class Block:
                 fuse_b1 = cfg.bias and _FUSE_FC1_BIAS
                 da = ops.linear_dx(dy, self.w("ffn.w2.weight"), act_input=a, act=cfg.activation,
                                    wt=self.wt("ffn.w2.weight"), colsum=self.g("ffn.w1.bias") if fuse_b1 else None)
-                wjobs.append(lambda dy=dy, gact=gact: ops.linear_dw(dy, gact, self.g("ffn.w2.weight")))
+                wjobs.append(ops.DW(dy, gact, self.g("ffn.w2.weight")))
                 if cfg.bias and not fuse_b1:
                     wjobs.append(lambda da=da: ops.colsum(da, self.g("ffn.w1.bias")))
-                wjobs.append(lambda da=da, h2=h2: ops.linear_dw(da, h2, self.g("ffn.w1.weight")))
+                wjobs.append(ops.DW(da, h2, self.g("ffn.w1.weight")))
                 dh2 = ops.linear_dx(da, self.w("ffn.w1.weight"), wt=self.wt("ffn.w1.weight"))
             fuse_cs = cfg.bias and kind == "layernorm"
             dx2, _ = ops.norm_bwd(dh2, st["x2"], self.w("ffn_norm.weight"), st["mu2"], st["rs2"], kind=kind,
@@ -434,7 +433,7 @@ class Block:
             # ---------------- attention
             o = st["o"]
             do = ops.linear_dx(dx2, self.w("attn.wo.weight"), wt=self.wt("attn.wo.weight"))
-            wjobs.append(lambda dx2=dx2, o=o: ops.linear_dw(dx2, o, self.g("attn.wo.weight")))
+            wjobs.append(ops.DW(dx2, o, self.g("attn.wo.weight")))
             if cfg.bias and not fuse_cs:
                 wjobs.append(lambda dx2=dx2: ops.colsum(dx2, self.g("attn.wo.bias")))
             qkv = st["qkv"]
@@ -450,7 +449,7 @@ class Block:
             if cfg.pos == "rope":
                 ops.rope_(dqkv, self.rope[0], self.rope[1], S, H, KV, Dh, inverse=True)
             h1 = st["h1"]
-            wjobs.append(lambda dqkv=dqkv, h1=h1: ops.linear_dw(dqkv, h1, self.g("attn.wqkv.weight")))
+            wjobs.append(ops.DW(dqkv, h1, self.g("attn.wqkv.weight")))
             if cfg.bias and not fuse_qkv_bias:
                 wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, self.g("attn.wqkv.bias")))
             dh1 = ops.linear_dx(dqkv, self.w("attn.wqkv.weight"), wt=self.wt("attn.wqkv.weight"))
@@ -459,8 +458,7 @@ class Block:
         if ov is not None:
             ov.run(wjobs)
         elif weight_grads:
-            for j in wjobs:
-                j()
+            ops.run_wjobs(wjobs)
         else:
             defer.extend(wjobs)
         del ctx.layers[self.i]
@@ -514,7 +512,7 @@ class Block:
         W = self.w(prefix + ".in_proj_weight")
         gW, gb = self.g(prefix + ".in_proj_weight"), self.g(prefix + ".in_proj_bias")
         o = st[key + "o"]
-        wjobs.append(lambda dout=dout, o=o: ops.linear_dw(dout, o, self.g(prefix + ".out_proj.weight")))
+        wjobs.append(ops.DW(dout, o, self.g(prefix + ".out_proj.weight")))
         do = ops.linear_dx(dout, self.w(prefix + ".out_proj.weight"), wt=self.wt(prefix + ".out_proj.weight"))
         if self_attn:
             qkv = st[key + "qkv"]
@@ -530,13 +528,13 @@ class Block:
         ops.attn_bwd(q, k, v, o, do, st[key + "lse"], dq, dk, dv, B, S, S, H, H, Dh, False, p_drop=cfg.dropout,
                      seed=seed)
         if self_attn:
-            wjobs.append(lambda dqkv=dqkv, xq=xq: ops.linear_dw(dqkv, xq, gW))
+            wjobs.append(ops.DW(dqkv, xq, gW))
             wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, gb))
             dx = ops.linear_dx(dqkv, W, residual=dres_q, wt=self.wt(prefix + ".in_proj_weight"))
             return dx, None
-        wjobs.append(lambda dq=dq, xq=xq: ops.linear_dw(dq, xq, gW[:d]))
+        wjobs.append(ops.DW(dq, xq, gW[:d]))
         wjobs.append(lambda dq=dq: ops.colsum(dq, gb[:d]))
-        wjobs.append(lambda dkv=dkv, xkv=xkv: ops.linear_dw(dkv, xkv, gW[d:]))
+        wjobs.append(ops.DW(dkv, xkv, gW[d:]))
         wjobs.append(lambda dkv=dkv: ops.colsum(dkv, gb[d:]))
         WT = self.wt(prefix + ".in_proj_weight")
         dxq = ops.linear_dx(dq, W[:d], residual=dres_q, wt=None if WT is None else WT[:, :d])
@@ -552,12 +550,12 @@ class Block:
                                dbias=self.g("norm3.bias"), p_drop=p, seed=_seed(sd, 6), want_branch=True,
                                colsum_branch=self.g("linear2.bias"))
         gact, a, x2 = st["g"], st["a"], st["x2"]
-        wjobs.append(lambda df=df, gact=gact: ops.linear_dw(df, gact, self.g("linear2.weight")))
+        wjobs.append(ops.DW(df, gact, self.g("linear2.weight")))
         # linear2 dX GEMM with dReLU x dropout mask in its epilogue and the linear1 bias
         # grad (column sums of the result) accumulated there too
         da = ops.linear_dx(df, self.w("linear2.weight"), act_input=a, act="relu", wt=self.wt("linear2.weight"),
                            colsum=self.g("linear1.bias"), p_drop=p, seed=_seed(sd, 5))
-        wjobs.append(lambda da=da, x2=x2: ops.linear_dw(da, x2, self.g("linear1.weight")))
+        wjobs.append(ops.DW(da, x2, self.g("linear1.weight")))
         dx2 = ops.linear_dx(da, self.w("linear1.weight"), residual=ds3, wt=self.wt("linear1.weight"))
         # norm2(x1 + drop(ca))
         ds2, dca = ops.norm_bwd(dx2, st["s2"], self.w("norm2.weight"), st["mu2"], st["rs2"], dw=self.g("norm2.weight"),
@@ -683,7 +681,7 @@ def head_fwd_bwd(h: torch.Tensor, target: torch.Tensor, W: torch.Tensor, Wt: Opt
         hc = h[r]
         logits, _ = ops.linear(hc, W, hb)
         ops.xent_fwd_bwd(logits, target[r], vocab, grad_scale=grad_scale, loss=loss_out[r])
-        jobs = [lambda lg=logits, hc=hc: ops.linear_dw(lg, hc, gW)]
+        jobs = [ops.DW(logits, hc, gW)]
         if gb is not None:
             jobs.append(lambda lg=logits: ops.colsum(lg, gb))
         if ov is not None:
@@ -868,7 +866,7 @@ class NativeModel:
             dl = ctx.misc.pop("dlogits")
             hn = ctx.misc.pop("hn")
             W = self.head_weight()
-            jobs = [lambda dl=dl, hn=hn: ops.linear_dw(dl, hn, self.head_grad())]
+            jobs = [ops.DW(dl, hn, self.head_grad())]
             if self.arena.has("output.bias"):
                 jobs.append(lambda dl=dl: ops.colsum(dl, self.arena.g("output.bias")))
             if ov is not None:
@@ -909,5 +907,4 @@ class NativeModel:
         return dy
 
     def backward_weight(self, mb: int):
-        for j in self.defer_w.pop(mb, []):
-            j()
+        ops.run_wjobs(self.defer_w.pop(mb, []))

@@ -401,6 +401,65 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, alpha: float 
     return dw
 
 
+# MIPIPE_WGRAD_GROUP=0: every weight-gradient GEMM of a job list in its own launch
+_WGRAD_GROUP = os.environ.get("MIPIPE_WGRAD_GROUP", "1") != "0"
+_GROUP_MAX = 8
+
+
+class DW:
+    """A weight-gradient job ``dw (f32) += alpha * dy^T x`` kept as data, so that
+    :func:`run_wjobs` can issue the short-token ones of a job list as ONE grouped launch
+    (csrc/kernels/gemm2.hip ``gemms_tt_grouped_kernel``).  Calling it runs it alone."""
+    __slots__ = ("dy", "x", "dw", "alpha")
+
+    def __init__(self, dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, alpha: float = 1.0):
+        self.dy, self.x, self.dw, self.alpha = dy, x, dw, alpha
+
+    def __call__(self):
+        linear_dw(self.dy, self.x, self.dw, self.alpha)
+
+    def groupable(self) -> bool:
+        """Short reductions (<= 4096 tokens) over few 256x256 output tiles: the shapes the
+        planner sends to the small 64x64 TT engine (gemm2.hip mp_gemm2_plan, cfg 13)."""
+        dy, x, dw = self.dy, self.x, self.dw
+        if not (_gpu(dy) and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and dw.dtype == torch.float32):
+            return False
+        if dy.stride(1) != 1 or x.stride(1) != 1 or dw.stride(1) != 1:
+            return False
+        T, N = dy.shape
+        K = x.shape[1]
+        if T % 64 or N % 8 or K % 8 or T > 4096:
+            return False
+        return ((N + 255) // 256) * ((K + 255) // 256) < 64
+
+
+def run_wjobs(jobs) -> None:
+    """Run a list of weight-gradient jobs (:class:`DW` objects and plain callables such as
+    bias column sums).  The groupable DW jobs with the same alpha go out as grouped
+    launches of up to 8 GEMMs; everything else runs in list order.  Jobs of one list
+    write distinct gradient buffers, so the reordering is exact."""
+    if not jobs:
+        return
+    rest, groups = [], {}
+    if _WGRAD_GROUP and GEMM_BACKEND != "blas":
+        for j in jobs:
+            if isinstance(j, DW) and j.groupable():
+                groups.setdefault(j.alpha, []).append(j)
+            else:
+                rest.append(j)
+    else:
+        rest = list(jobs)
+    for alpha, g in groups.items():
+        if len(g) == 1:
+            g[0]()
+            continue
+        for i in range(0, len(g), _GROUP_MAX):
+            part = g[i:i + _GROUP_MAX]
+            _ext().gemm_tt_grouped([j.dy for j in part], [j.x for j in part], [j.dw for j in part], float(alpha))
+    for j in rest:
+        j()
+
+
 # ======================================================================================
 # elementwise
 # ======================================================================================

@@ -127,6 +127,43 @@ def test_linear_dw(T, N, K):
     close(got, ref, atol=2e-2, rtol=1e-2)
 
 
+def test_grouped_wgrad_jobs_vs_f32():
+    """run_wjobs issues the short-token DW jobs of a list as ONE grouped launch
+    (gemms_tt_grouped_kernel): every problem (different N/K, strided row views, two
+    halves of one gradient, alpha) must match the f32 reference; non-groupable jobs and
+    plain callables still run."""
+    torch.manual_seed(0)
+    T = 1024
+    shapes = [(2304, 768), (768, 768), (2048, 768), (768, 2048), (1536, 768), (768, 768), (8, 64), (136, 200)]
+    jobs_cpu, jobs_gpu, outs = [], [], []
+    big = rnd(T, 3 * 768, scale=0.1)            # row-strided column views (dq / dkv of one buffer)
+    for i, (N, K) in enumerate(shapes):
+        dy = big[:, :N] if i == 1 else rnd(T, N, scale=0.1)
+        x = rnd(T, K)
+        base = torch.randn(N, K)
+        g_cpu, g_gpu = base.clone(), base.clone().to(DEV)
+        jobs_cpu.append(ops.DW(dy, x, g_cpu, 0.5))
+        jobs_gpu.append(ops.DW(dy.to(DEV) if i != 1 else big.to(DEV)[:, :N], x.to(DEV), g_gpu, 0.5))
+        outs.append((g_cpu, g_gpu))
+    gw = torch.zeros(1536, 768)
+    dy2, x2 = rnd(T, 1536, scale=0.1), rnd(T, 768)
+    gw_gpu = gw.clone().to(DEV)
+    jobs_cpu += [ops.DW(dy2[:, :768], x2, gw[:768]), ops.DW(dy2[:, 768:], x2, gw[768:])]
+    jobs_gpu += [ops.DW(dy2.to(DEV)[:, :768], x2.to(DEV), gw_gpu[:768]),
+                 ops.DW(dy2.to(DEV)[:, 768:], x2.to(DEV), gw_gpu[768:])]
+    assert sum(j.groupable() for j in jobs_gpu) == len(jobs_gpu)
+    big_job = ops.DW(rnd(8192, 768, scale=0.1).to(DEV), rnd(8192, 768).to(DEV), torch.zeros(768, 768, device=DEV))
+    assert not big_job.groupable()
+    hit = []
+    jobs_gpu.append(lambda: hit.append(1))
+    ops.run_wjobs(jobs_gpu + [big_job])
+    ops.run_wjobs(jobs_cpu)
+    torch.cuda.synchronize()
+    assert hit == [1]
+    for g_cpu, g_gpu in outs + [(gw, gw_gpu)]:
+        close(g_gpu, g_cpu, atol=2e-2, rtol=1e-2)
+
+
 def test_gemm_asymmetric_layout_check():
     """A = I with an asymmetric B catches transposed C writes (cdna guide §3)."""
     n = 128
