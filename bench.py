@@ -313,6 +313,7 @@ def run(a) -> None:
                    "parallelism": f"pp{pp}" + (f"_dp{dp}" if dp > 1 else ""),
                    "layer_split": trainer.layer_ranges, "optimizer": "AdamW(fused, clip 1.0)",
                    "hip_graphs": bool(a.graphs) and gpu,
+                   "microbatch_lanes": getattr(trainer, "lanes", 1),
                    "native_runner": rt.native_runner is not None,
                    "native_reason": rt.native_reason,
                    "p2p": rt.p2p.kind,

@@ -15,6 +15,11 @@
 //   WAIT   slot      the compute stream waits for that group's completion event
 //   CALL   fn        a Python callable (anything not expressible above: gloo transfers,
 //                    DP all-reduce through torch.distributed) -- the GIL is taken only here
+//   SYNC   w, s      stream w waits for everything issued so far on stream s (an event)
+//
+// GRAPH and COPY carry the stream they were issued on (0 = the compute stream): with
+// microbatch lanes (parallel/runtime.py, PP = 1) the odd microbatches' graphs replay on a
+// second stream, forked from and joined back into the compute stream by SYNCs.
 //
 // parallel/native_runner.py records the tape from one instrumented Python step and
 // `run()` replays it with the GIL released: no per-action Python, no allocator calls, no
@@ -51,25 +56,38 @@ using mipipe_comm::RcclP2P;
 
 class StageRunner {
  public:
-  enum Kind { GRAPH = 0, COPY = 1, POST = 2, WAIT = 3, CALL = 4 };
+  enum Kind { GRAPH = 0, COPY = 1, POST = 2, WAIT = 3, CALL = 4, SYNC = 5 };
 
   explicit StageRunner(int device) : device_(device) {}
 
-  void add_graph(int64_t graph_exec, const std::string& label) {
+  void add_graph(int64_t graph_exec, const std::string& label, int64_t stream) {
     TORCH_CHECK(graph_exec != 0, "stage runner: null graph exec");
     Instr i;
     i.kind = GRAPH;
     i.a = graph_exec;
     i.label = label;
+    i.stream = stream;
     tape_.push_back(std::move(i));
   }
 
-  void add_copy(int64_t dst, int64_t src, int64_t nbytes) {
+  void add_copy(int64_t dst, int64_t src, int64_t nbytes, int64_t stream) {
     Instr i;
     i.kind = COPY;
     i.a = dst;
     i.b = src;
     i.c = nbytes;
+    i.stream = stream;
+    tape_.push_back(std::move(i));
+  }
+
+  // waiter / signal: HIP stream handles, 0 = the compute stream
+  void add_sync(int64_t waiter, int64_t signal) {
+    TORCH_CHECK(waiter != signal, "stage runner: SYNC of a stream with itself");
+    Instr i;
+    i.kind = SYNC;
+    i.a = waiter;
+    i.b = signal;
+    i.slot = nsync_++;
     tape_.push_back(std::move(i));
   }
 
@@ -113,20 +131,32 @@ class StageRunner {
     std::vector<RcclP2P*> engines(nslots_, nullptr);
     const bool prof = profile_;
     if (prof) prepare_events();
+    while ((int64_t)sync_ev_.size() < nsync_) {
+      hipEvent_t e;
+      MP_HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      sync_ev_.push_back(e);
+    }
+    auto on = [st](int64_t s) { return s ? reinterpret_cast<hipStream_t>(s) : st; };
     py::gil_scoped_release nogil;
     int ng = 0;
     if (prof) MP_HIPCHK(hipEventRecord(ev_[0], st));
     for (const Instr& i : tape_) {
       switch (i.kind) {
-        case GRAPH:
-          if (prof) MP_HIPCHK(hipEventRecord(ev_[2 + 2 * ng], st));
-          MP_HIPCHK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(i.a), st));
-          if (prof) MP_HIPCHK(hipEventRecord(ev_[3 + 2 * ng], st));
+        case GRAPH: {
+          hipStream_t gs = on(i.stream);
+          if (prof) MP_HIPCHK(hipEventRecord(ev_[2 + 2 * ng], gs));
+          MP_HIPCHK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(i.a), gs));
+          if (prof) MP_HIPCHK(hipEventRecord(ev_[3 + 2 * ng], gs));
           ++ng;
           break;
+        }
         case COPY:
           MP_HIPCHK(hipMemcpyAsync(reinterpret_cast<void*>(i.a), reinterpret_cast<const void*>(i.b), (size_t)i.c,
-                                   hipMemcpyDeviceToDevice, st));
+                                   hipMemcpyDeviceToDevice, on(i.stream)));
+          break;
+        case SYNC:
+          MP_HIPCHK(hipEventRecord(sync_ev_[i.slot], on(i.b)));
+          MP_HIPCHK(hipStreamWaitEvent(on(i.a), sync_ev_[i.slot], 0));
           break;
         case POST:
           handles[i.slot] = i.engine->post_raw(i.channel, i.sends, i.recvs, st);
@@ -204,6 +234,7 @@ class StageRunner {
     int kind = GRAPH;
     int64_t a = 0, b = 0, c = 0;
     int64_t slot = -1;
+    int64_t stream = 0;  // GRAPH / COPY: issuing stream (0 = compute stream)
     int channel = 0;
     std::string label;
     RcclP2P* engine = nullptr;
@@ -229,6 +260,8 @@ class StageRunner {
   int device_;
   std::vector<Instr> tape_;
   int64_t nslots_ = 0;
+  int64_t nsync_ = 0;
+  std::vector<hipEvent_t> sync_ev_;
   int64_t runs_ = 0;
   bool profile_ = false;
   bool profiled_ = false;
@@ -238,8 +271,11 @@ class StageRunner {
 void register_runner(py::module& m) {
   py::class_<StageRunner>(m, "StageRunner")
       .def(py::init<int>(), py::arg("device"))
-      .def("add_graph", &StageRunner::add_graph, py::arg("graph_exec"), py::arg("label") = "")
-      .def("add_copy", &StageRunner::add_copy)
+      .def("add_graph", &StageRunner::add_graph, py::arg("graph_exec"), py::arg("label") = "",
+           py::arg("stream") = 0)
+      .def("add_copy", &StageRunner::add_copy, py::arg("dst"), py::arg("src"), py::arg("nbytes"),
+           py::arg("stream") = 0)
+      .def("add_sync", &StageRunner::add_sync, py::arg("waiter"), py::arg("signal"))
       .def("add_post", &StageRunner::add_post)
       .def("add_wait", &StageRunner::add_wait)
       .def("add_call", &StageRunner::add_call)

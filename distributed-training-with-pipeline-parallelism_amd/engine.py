@@ -12,6 +12,7 @@ global grad-norm clip + one fused AdamW launch per stage arena.
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -215,6 +216,15 @@ class PipelineTrainer:
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
                                        scale_grads=True, style=style, profile=profile, orders=orders,
                                        head=head_plan, head_costs=head_costs, stage_costs=stage_costs)
+        # microbatch lanes (PipelineRuntime.set_lanes): MIPIPE_LANES=auto (default: 2 lanes
+        # at PP = 1 with HIP graphs when a microbatch is <= 4096 tokens), 1 (off) or n
+        lanes_env = os.environ.get("MIPIPE_LANES", "auto")
+        if lanes_env == "auto":
+            lanes = 2 if (pp == 1 and v == 1 and graphs and self.device.type == "cuda" and n_microbatches >= 2
+                          and mbs * seq_len <= 4096) else 1
+        else:
+            lanes = max(1, int(lanes_env))
+        self.lanes = self.runtime.set_lanes(lanes)
         arenas = [st.arena for st in self.stages]
         norm_skip = []
         norm_exclude = {}

@@ -16,6 +16,7 @@ so checkpoints are per-stage shards that re-split to any PP degree (SURVEY §2.7
 """
 from __future__ import annotations
 
+import contextlib
 import hashlib
 import os
 import math
@@ -75,6 +76,9 @@ class ParamArena:
         self.dtype = dtype
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        # per-lane gradient buffers (microbatch lanes, parallel/runtime.py): lane 0 is
+        # ``grad`` itself; the others are summed into it at the end of the step
+        self.grad_lanes: List[torch.Tensor] = [self.grad]
         self.w16 = torch.zeros(self.numel, dtype=dtype, device=self.device)
         # transposed bf16 copies of the matrices used as B in dX = dY W (GPU only)
         self.t_offsets: Dict[str, int] = {}
@@ -167,7 +171,36 @@ class ParamArena:
         self.sync_w16()
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        for g in self.grad_lanes:
+            g.zero_()
+
+    def set_lanes(self, n: int) -> None:
+        """Keep ``n`` gradient buffers: two microbatches of different lanes run their
+        backwards concurrently, and the dW GEMMs' f32 read-modify-write accumulation (and
+        the norm-weight reductions) must not race on one buffer."""
+        while len(self.grad_lanes) < n:
+            self.grad_lanes.append(torch.zeros_like(self.grad_lanes[0]))
+        del self.grad_lanes[max(n, 1):]
+
+    @contextlib.contextmanager
+    def lane(self, idx: int):
+        """Route every gradient view taken inside (``g(name)``, ``grad``) to lane ``idx``."""
+        if idx == 0 or len(self.grad_lanes) <= 1:
+            yield
+            return
+        prev = self.grad
+        self.grad = self.grad_lanes[idx]
+        try:
+            yield
+        finally:
+            self.grad = prev
+
+    def merge_lanes(self) -> None:
+        """grad += every other lane's gradient; those are zeroed for the next step."""
+        g0 = self.grad_lanes[0]
+        for g in self.grad_lanes[1:]:
+            g0.add_(g)
+            g.zero_()
 
 
 # ======================================================================================
@@ -736,6 +769,10 @@ class NativeModel:
         # matrix lives in the shared HeadShard arena
         self.head = head
         self.split_head = head is not None
+        # dW GEMMs of a backward on the side stream (WGradOverlap); off with microbatch
+        # lanes, where a second microbatch fills the CUs instead and a graph that forks onto
+        # a side stream measured no concurrency with the other lane's graphs
+        self.wgrad_side = True
         self.device = torch.device(device)
         self.recompute = recompute
         if layer_range is None:
@@ -824,7 +861,7 @@ class NativeModel:
             # backward starts from dhn (no [T, V] logits kept)
             dhn = torch.empty_like(hn)
             row_loss = torch.empty(T, device=hn.device, dtype=torch.float32)
-            ov = WGradOverlap.make(self.device, True)
+            ov = WGradOverlap.make(self.device, self.wgrad_side)
             head_fwd_bwd(hn, target.reshape(-1), self.head_weight(), self.head_weight_t(), hb, self.head_grad(),
                          self.arena.g("output.bias") if hb is not None else None, dhn, cfg.vocab_size,
                          loss_scale / T, row_loss, chunk=_HEAD_CHUNK, ov=ov)
@@ -846,7 +883,7 @@ class NativeModel:
     def backward(self, dy: Optional[torch.Tensor], ctx: MBContext, B: int, S: int, weight_grads: bool = True):
         cfg = self.cfg
         defer: List = []
-        ov = WGradOverlap.make(self.device, weight_grads)   # dW GEMMs on a side stream
+        ov = WGradOverlap.make(self.device, weight_grads and self.wgrad_side)   # dW GEMMs on a side stream
         if self.last and self.split_head:
             # dy = dL/d(final-norm output), gathered from the head chunks
             if cfg.final_norm:

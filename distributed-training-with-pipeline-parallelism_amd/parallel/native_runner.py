@@ -43,6 +43,9 @@ class TapeRecorder:
             raise RuntimeError("the native stage runner needs the built extension (_C.so)")
         idx = device.index if device.index is not None else (torch.cuda.current_device() if device.type == "cuda" else 0)
         self.runner = ext.StageRunner(idx)
+        # instructions issued on another stream than this one (microbatch lanes) carry it
+        self.cuda = device.type == "cuda"
+        self.main_stream = torch.cuda.current_stream(idx).cuda_stream if self.cuda else 0
         self.valid = True
         self.reason = ""
         self._holders: Dict[int, list] = {}
@@ -66,15 +69,30 @@ class TapeRecorder:
             self.valid, self.reason = False, why
 
     # ------------------------------------------------------------------ instructions
+    def _stream(self) -> int:
+        if not self.cuda:
+            return 0
+        s = torch.cuda.current_stream().cuda_stream
+        return 0 if s == self.main_stream else int(s)
+
     def graph(self, g: torch.cuda.CUDAGraph, label: str = "") -> None:
-        self.runner.add_graph(int(g.raw_cuda_graph_exec()), str(label))
+        st = self._stream()
+        if st:
+            self.runner.add_graph(int(g.raw_cuda_graph_exec()), str(label), st)
+        else:
+            self.runner.add_graph(int(g.raw_cuda_graph_exec()), str(label))
+
+    def sync(self, waiter: "torch.cuda.Stream", signal: "torch.cuda.Stream") -> None:
+        """``waiter.wait_stream(signal)`` on the tape."""
+        w, s = int(waiter.cuda_stream), int(signal.cuda_stream)
+        self.runner.add_sync(0 if w == self.main_stream else w, 0 if s == self.main_stream else s)
 
     def copy(self, dst: torch.Tensor, src: torch.Tensor) -> None:
         if not (dst.is_contiguous() and src.is_contiguous() and dst.dtype == src.dtype
                 and dst.numel() == src.numel()):
             self.invalidate("non-contiguous or mismatched copy")
             return
-        self.runner.add_copy(dst.data_ptr(), src.data_ptr(), dst.numel() * dst.element_size())
+        self.runner.add_copy(dst.data_ptr(), src.data_ptr(), dst.numel() * dst.element_size(), self._stream())
 
     def native_post(self, engine, channel: int, sends, recvs) -> int:
         def ops(lst):

@@ -73,11 +73,12 @@ def test_native_runner_virtual_stages_on_one_rank():
     assert l_native == pytest.approx(l_python, rel=5e-4)
 
 
-def test_profiled_step_is_measured_on_the_tape():
+def test_profiled_step_is_measured_on_the_tape(monkeypatch):
     """The bubble measurement replays the same native tape with timing events around
-    every graph: at PP=1 (no pipeline) the compute stream is busy the whole step."""
+    every graph: at PP=1 (no pipeline, one lane) the compute stream is busy the whole step."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    monkeypatch.setenv("MIPIPE_LANES", "1")
     tr, _ = _train(CFGS["gpt2"], True, steps=4)
     runs = tr.runtime.native_runner.runs
     tr.runtime.profile = True
@@ -101,6 +102,7 @@ def test_wgrad_side_stream_matches_inline(graphs, monkeypatch):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import mipipe.models.native as N
+    monkeypatch.setenv("MIPIPE_LANES", "1")   # lanes turn the side stream off
 
     def grads(side):
         monkeypatch.setattr(N, "_WGRAD_STREAM", side)
@@ -128,3 +130,40 @@ def test_wgrad_side_stream_matches_inline(graphs, monkeypatch):
         assert torch.isfinite(a).all()
         err = (a - b).norm() / b.norm().clamp_min(1e-12)
         assert err < 1e-5, float(err)
+
+
+@pytest.mark.parametrize("name", ["gpt2", "reference"])
+def test_microbatch_lanes_match_single_lane(name, monkeypatch):
+    """PP = 1 microbatch lanes (odd microbatches' graphs on a second HIP stream, per-lane
+    gradient buffers summed at the join, SYNC instructions on the native tape) train like
+    the single-stream path."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = CFGS["gpt2"] if name == "gpt2" else NativeConfig.reference(n_layers=2, n_heads=4, dim=256,
+                                                                      vocab_size=1000, dropout=0.0,
+                                                                      dim_feedforward=512)
+
+    def run(lanes):
+        monkeypatch.setenv("MIPIPE_LANES", str(lanes))
+        dev = torch.device("cuda", 0)
+        tr = PipelineTrainer(cfg, pp=1, n_microbatches=4, mbs=2, seq_len=128, device=dev, seed=3, graphs=True)
+        assert tr.lanes == lanes
+        g = torch.Generator(device="cuda").manual_seed(7)
+        x = torch.randint(0, cfg.vocab_size, (8, 128), device=dev, generator=g)
+        y = torch.randint(0, cfg.vocab_size, (8, 128), device=dev, generator=g)
+        tr.capture_graphs(x, y)
+        losses = [float(tr.train_step(x, y)) for _ in range(5)]
+        torch.cuda.synchronize()
+        return tr, losses
+
+    tr2, l2 = run(2)
+    tr1, l1 = run(1)
+    assert tr2.runtime.native_runner is not None, tr2.runtime.native_reason
+    assert 5 in tr2.runtime.native_runner.kinds()       # SYNC: fork / join of the lane stream
+    assert 5 not in tr1.runtime.native_runner.kinds()
+    assert l2[0] == pytest.approx(l1[0], rel=1e-6)
+    assert l2 == pytest.approx(l1, rel=2e-3)
+    assert l2[-1] < l2[0]
+    for a in tr2.optimizer.arenas:
+        for extra in a.grad_lanes[1:]:
+            assert float(extra.abs().max()) == 0.0     # merged and cleared at the join
