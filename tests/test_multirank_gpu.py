@@ -40,10 +40,12 @@ def reference8():
 
 @pytest.mark.parametrize("n,schedule,graphs,split,dp", [(2, "1F1B", 0, 1, 1), (2, "ZBH1", 1, 1, 1),
                                                         (4, "1F1B", 1, 1, 1), (4, "GPipe", 0, 0, 1),
-                                                        (2, "ZBV", 0, 1, 1), (4, "1F1B", 1, 1, 2)])
+                                                        (2, "ZBV", 0, 1, 1), (4, "1F1B", 1, 1, 2),
+                                                        (2, "1F1B", 1, 1, 2)])
 def test_multirank_gpu_matches_single(reference, n, schedule, graphs, split, dp):
     """dp=2: DP x PP (2 x 2) with HIP graphs -- the stages' DP all-reduce replays as a
-    recorded CALL on the native runner's tape."""
+    recorded CALL on the native runner's tape.  (2, dp=2) is DP2 x PP1: microbatch lanes
+    on each replica, joined (lane gradients summed) before the DP all-reduce."""
     res = _run(n, "--schedule", schedule, "--graphs", str(graphs), "--split-head", str(split), "--dp", str(dp),
                port=29772 + n + 10 * graphs + 20 * split + 40 * dp)
     # bf16 kernels + split-K atomics: equal up to reduction-order rounding

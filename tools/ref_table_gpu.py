@@ -83,7 +83,7 @@ def main():
             mine = {k: v for k, v in ref.items() if k[0] == L and k[1] == H}
             best_k = max(mine, key=mine.get)
             row = {"L": L, "H": H, "tokens_per_s": round(tok_s, 1), "ms_per_iter": round(dt / a.iters * 1e3, 3),
-                   "loss": round(float(loss), 4), "ref_best_tok_s": mine[best_k],
+                   "loss": round(float(loss), 4), "lanes": tr.lanes, "ref_best_tok_s": mine[best_k],
                    "ref_best_run": f"P={best_k[2]} {best_k[3]}", "ref_gpipe_p2_tok_s": mine.get((L, H, 2, "GPipe")),
                    "x_vs_ref_best": round(tok_s / mine[best_k], 1)}
             out.append(row)
@@ -92,7 +92,7 @@ def main():
             torch.cuda.empty_cache()
     summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
                          "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, bf16, AdamW step included, "
-                         + ("eager" if a.no_graphs else "HIP graphs"),
+                         + ("eager" if a.no_graphs else "HIP graphs") + ", microbatch lanes (MIPIPE_LANES)",
                "rows": out}
     if a.json:
         with open(a.json, "w") as f:
