@@ -216,15 +216,10 @@ class PipelineTrainer:
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
                                        scale_grads=True, style=style, profile=profile, orders=orders,
                                        head=head_plan, head_costs=head_costs, stage_costs=stage_costs)
-        # microbatch lanes (PipelineRuntime.set_lanes): MIPIPE_LANES=auto (default: 2 lanes
-        # at PP = 1 with HIP graphs when a microbatch is <= 4096 tokens), 1 (off) or n
-        lanes_env = os.environ.get("MIPIPE_LANES", "auto")
-        if lanes_env == "auto":
-            lanes = 2 if (pp == 1 and v == 1 and graphs and self.device.type == "cuda" and n_microbatches >= 2
-                          and mbs * seq_len <= 4096) else 1
-        else:
-            lanes = max(1, int(lanes_env))
-        self.lanes = self.runtime.set_lanes(lanes)
+        # microbatch lanes (PipelineRuntime.set_lanes): MIPIPE_LANES=auto|1 (off)|n
+        self.lanes = self.runtime.set_lanes(self._auto_lanes(pp, v, graphs, n_microbatches, mbs, seq_len)
+                                            if os.environ.get("MIPIPE_LANES", "auto") == "auto"
+                                            else max(1, int(os.environ["MIPIPE_LANES"])))
         arenas = [st.arena for st in self.stages]
         norm_skip = []
         norm_exclude = {}
@@ -249,6 +244,25 @@ class PipelineTrainer:
                                    pp_group=self.mesh.pp_group if pp > 1 else None, norm_skip=norm_skip,
                                    norm_exclude=norm_exclude, grad_scale=1.0 / self.mesh.dp)
         self.last_losses: List[torch.Tensor] = []
+
+    def _auto_lanes(self, pp: int, v: int, graphs: bool, m: int, mbs: int, seq_len: int) -> int:
+        """Lanes at PP = 1 with HIP graphs: up to 4 for <= 4096-token microbatches, 2 above,
+        if the extra per lane (an f32 gradient buffer + one more microbatch's activation
+        stash in flight) stays within 20 % of HBM.  Measured on one MI355X (profiles/
+        r2_lanes_ab.txt): reference model L8H8 (1024-token microbatches, m = 4) 311K tok/s
+        with 1 lane, 495K with 2, 456K with 3, 594K with 4; GPT-2 small (16K-token
+        microbatches, m = 2) 850K -> 888K with 2."""
+        if not (pp == 1 and v == 1 and graphs and self.device.type == "cuda" and m >= 2):
+            return 1
+        T = mbs * seq_len
+        lanes = min(m, 4 if T <= 4096 else 2)
+        params = sum(st.arena.numel for st in self.stages)
+        layers = sum(r1 - r0 for r0, r1 in self.layer_ranges)
+        per_lane = 4.0 * params + layers * self.cfg.stash_bytes_per_layer(T, recompute=self.recompute)
+        hbm = torch.cuda.get_device_properties(self.device).total_memory
+        while lanes > 1 and (lanes - 1) * per_lane > 0.2 * hbm:
+            lanes -= 1
+        return lanes
 
     @property
     def is_first(self) -> bool:

@@ -132,8 +132,8 @@ def test_wgrad_side_stream_matches_inline(graphs, monkeypatch):
         assert err < 1e-5, float(err)
 
 
-@pytest.mark.parametrize("name", ["gpt2", "reference"])
-def test_microbatch_lanes_match_single_lane(name, monkeypatch):
+@pytest.mark.parametrize("name,lanes", [("gpt2", 2), ("reference", 2), ("reference", 4), ("gpt2", 3)])
+def test_microbatch_lanes_match_single_lane(name, lanes, monkeypatch):
     """PP = 1 microbatch lanes (odd microbatches' graphs on a second HIP stream, per-lane
     gradient buffers summed at the join, SYNC instructions on the native tape) train like
     the single-stream path."""
@@ -156,7 +156,7 @@ def test_microbatch_lanes_match_single_lane(name, monkeypatch):
         torch.cuda.synchronize()
         return tr, losses
 
-    tr2, l2 = run(2)
+    tr2, l2 = run(lanes)
     tr1, l1 = run(1)
     assert tr2.runtime.native_runner is not None, tr2.runtime.native_reason
     assert 5 in tr2.runtime.native_runner.kinds()       # SYNC: fork / join of the lane stream
