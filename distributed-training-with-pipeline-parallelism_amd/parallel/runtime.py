@@ -104,6 +104,9 @@ class _Range:
         return self.rf.__exit__(*exc)
 
 
+_LANE_STREAMS: Dict[int, List[torch.cuda.Stream]] = {}
+
+
 class PipelineRuntime:
     def __init__(self, stages: Sequence[StageBase], schedule: str, n_microbatches: int, pp_rank: int,
                  pp_size: int, p2p: P2P, loss_fn: Optional[Callable] = None, scale_grads: bool = True,
@@ -204,11 +207,19 @@ class PipelineRuntime:
         self.lanes = n
         self.lane_streams = [None]
         idx = (self.device.index if self.device.index is not None else torch.cuda.current_device()) if n > 1 else 0
-        for _ in range(1, n):
+        # one set of lane streams per device and process: HIP maps each stream onto one of
+        # GPU_MAX_HW_QUEUES (4) hardware queues when it is created, and two lanes (or a lane
+        # and the compute stream) sharing a queue serialise.  torch's pool hands streams out
+        # round-robin, so trainers built later in a process would get other queue mappings
+        # (the reference 9-config table measured 444K tok/s for L8H8 vs 594K in a fresh
+        # process); the first ones taken are reused instead
+        cache = _LANE_STREAMS.setdefault(idx, [])
+        main_s = torch.cuda.current_stream(idx).cuda_stream if n > 1 else None
+        while len(cache) < n - 1:
             ls = torch.cuda.Stream(device=idx)
-            if ls.cuda_stream == torch.cuda.current_stream(idx).cuda_stream:
-                ls = torch.cuda.Stream(device=idx)
-            self.lane_streams.append(ls)
+            if ls.cuda_stream != main_s and all(ls.cuda_stream != c.cuda_stream for c in cache):
+                cache.append(ls)
+        self.lane_streams += cache[: n - 1]
         for st in self.stages.values():
             st.arena.set_lanes(n)
             if hasattr(st, "model"):

@@ -42,8 +42,8 @@ def reference_rows():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
-    ap.add_argument("--iters", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="bf16: the native HIP path (PipelineTrainer, AdamW included); fp32: the reference's own "
