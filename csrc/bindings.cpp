@@ -20,6 +20,7 @@ int mp_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out
 int mp_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int T, int S, int D, int pos_offset,
                  hipStream_t st);
 int mp_sumsq(const float* g, int64_t n, float* out, hipStream_t st);
+int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, hipStream_t st);
 int mp_adamw(float* p, float* g, float* m, float* v, void* w16, int64_t n, int64_t n_decay, float lr, float b1,
              float b2, float eps, float wd, int step, const float* sumsq, float max_norm, float grad_scale,
              int zero_grad, hipStream_t st);
@@ -155,6 +156,19 @@ void embed_bwd(torch::Tensor idx, torch::Tensor dout, torch::Tensor dwte, c10::o
   check(mp_embed_bwd(idx.data_ptr<int64_t>(), dout.data_ptr(), dwte.data_ptr<float>(),
                      dwpe.has_value() ? dwpe->data_ptr<float>() : nullptr, T, S, D, pos_offset, cur_stream()),
         "embed_bwd");
+}
+
+// g0 += sum(lanes); lanes zeroed (1..3 extra f32 lane buffers of g0's size)
+void lane_merge(torch::Tensor g0, std::vector<torch::Tensor> lanes) {
+  TORCH_CHECK(lanes.size() >= 1 && lanes.size() <= 3, "lane_merge: 1..3 lane buffers");
+  req(g0, torch::kFloat32, "g0");
+  float* p[3] = {nullptr, nullptr, nullptr};
+  for (size_t i = 0; i < lanes.size(); ++i) {
+    req(lanes[i], torch::kFloat32, "lane");
+    TORCH_CHECK(lanes[i].numel() == g0.numel(), "lane_merge: size mismatch");
+    p[i] = lanes[i].data_ptr<float>();
+  }
+  check(mp_lane_merge(g0.data_ptr<float>(), p[0], p[1], p[2], g0.numel(), cur_stream()), "lane_merge");
 }
 
 void sumsq(torch::Tensor g, torch::Tensor out) {
@@ -436,6 +450,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
+  m.def("lane_merge", &lane_merge);
   m.def("gemm_tt_grouped", &gemm_tt_grouped, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("C"),
         pybind11::arg("alpha") = 1.0);
   m.def("gemm2", &gemm2, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),

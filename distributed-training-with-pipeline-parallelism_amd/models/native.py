@@ -196,9 +196,15 @@ class ParamArena:
             self.grad = prev
 
     def merge_lanes(self) -> None:
-        """grad += every other lane's gradient; those are zeroed for the next step."""
+        """grad += every other lane's gradient; those are zeroed for the next step (one
+        fused pass on GPU: optim.hip lane_merge_kernel)."""
         g0 = self.grad_lanes[0]
-        for g in self.grad_lanes[1:]:
+        rest = self.grad_lanes[1:]
+        if g0.is_cuda:
+            for i in range(0, len(rest), 3):
+                ops.load_ext().lane_merge(g0, rest[i:i + 3])
+            return
+        for g in rest:
             g0.add_(g)
             g.zero_()
 
