@@ -320,6 +320,7 @@ def run(a) -> None:
                    "p2p_channels": rt.p2p.channels if rt.p2p.kind == "native" else None,
                    "p2p_fallback": rt.p2p.fallback_reason or None,
                    "recompute": trainer.recompute,
+                   "recv_arena_mb": round(rt.recv_arena_bytes / 2 ** 20, 1),
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
                    else "last stage",
                    "head_lag": getattr(trainer, "head_lag", None),

@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import contextlib
 import logging
+import math
 import os
 import time
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
@@ -162,6 +163,7 @@ class PipelineRuntime:
         self.last_timeline_source = ""
         self._initialized = False
         self._recv_bufs: Dict[tuple, List[torch.Tensor]] = {}
+        self.recv_arena_bytes = 0
         self._dh_full: Dict[int, torch.Tensor] = {}
         self._steps = 0
         self.head_losses: Dict[int, torch.Tensor] = {}
@@ -311,7 +313,70 @@ class PipelineRuntime:
                 prev_out = out_specs
                 if s < self.num_stages - 1 and self.s2r[s + 1] != self.rank:
                     self.p2p.send_specs(out_specs, self.s2r[s + 1])
+        self._plan_recv_arena()
         self._initialized = True
+
+    def _recv_shapes(self, key: tuple):
+        """(shape, dtype) list of the tensors received under message ``key``."""
+        kind = key[0]
+        if kind == "H":
+            h = self.head
+            return [((h.chunks[key[1]], h.d_model), h.dtype)]
+        _, stage, _ = key
+        st = self.stages[stage]
+        specs = st.input_specs if kind == "F" else st.output_specs
+        return [(tuple(sh), dt) for sh, dt in specs]
+
+    def _plan_recv_arena(self) -> None:
+        """Every receive slot of the lowered program (one per (kind, stage, microbatch)
+        message, plus the last stage's per-microbatch head input-gradient buffers) is
+        carved out of ONE allocation made here, before the first step: the receive side
+        of the 1F1B stash is sized up front from the program instead of growing lazily
+        inside the step.  Slots are 256-byte aligned; ``recv_arena_bytes``
+        is what it holds.  Slots stay persistent (a stage may keep its received input as
+        the backward's saved activation), so graph captures and the native tape see fixed
+        addresses."""
+        want: List[Tuple[tuple, List]] = []
+        seen = set()
+        for e in self.program:
+            if not isinstance(e, CommGroup):
+                continue
+            for op in e.ops:
+                if op.action.op.is_send or op.key in seen or op.key[0] == "D":
+                    continue
+                seen.add(op.key)
+                want.append((op.key, self._recv_shapes(op.key)))
+        dh_mbs = []
+        if self.head is not None and self.s2r[self.num_stages - 1] == self.rank:
+            dh_mbs = list(range(self.m))
+        align = 256
+        off = 0
+        slots = []
+        for key, shapes in want:
+            views = []
+            for sh, dt in shapes:
+                n = math.prod(sh) * torch.empty((), dtype=dt).element_size()
+                views.append((off, n, sh, dt))
+                off += (n + align - 1) // align * align
+            slots.append((key, views))
+        h = self.head
+        dh_views = []
+        for mb in dh_mbs:
+            n = h.tokens * h.d_model * torch.empty((), dtype=h.dtype).element_size()
+            dh_views.append((mb, off, n))
+            off += (n + align - 1) // align * align
+        self.recv_arena_bytes = off
+        if off == 0:
+            return
+        arena = torch.empty(off, dtype=torch.uint8, device=self.device)
+        self._recv_arena = arena
+
+        def view(o, n, sh, dt):
+            return arena[o:o + n].view(dt).view(sh)
+        for key, views in slots:
+            self._recv_bufs[key] = [view(o, n, sh, dt) for o, n, sh, dt in views]
+        for mb, o, n in dh_views:
+            self._dh_full[mb] = view(o, n, (h.tokens, h.d_model), h.dtype)
 
     def _dh_buf(self, mb: int) -> torch.Tensor:
         """[T, D] input-gradient buffer of the last stage for microbatch mb; the head

@@ -193,3 +193,37 @@ def test_recompute_auto_plan():
     o4 = generate("1F1B", 4, 8, 1, "loop")
     assert max_inflight_microbatches(o4[0], {0}) == 4 and max_inflight_microbatches(o4[3], {3}) == 1
     assert max_inflight_microbatches(generate("GPipe", 4, 8, 1, "loop")[0], {0}) == 8
+
+
+def _arena_worker(rank, world, split_head):
+    cfg = CFG["gpt2"]()
+    tr = PipelineTrainer(cfg, pp=world, schedule="1F1B", n_microbatches=M, mbs=MBS, seq_len=S,
+                         device=torch.device("cpu"), dtype=torch.float32, layer_ranges=[(0, 2), (2, 4)],
+                         split_head=split_head, head_align=8)
+    rt = tr.runtime
+    x, y = _data(cfg)
+    tr.train_step(x, y)
+    keys0 = set(rt._recv_bufs)
+    ptrs0 = {k: [t.data_ptr() for t in v] for k, v in rt._recv_bufs.items()}
+    lo = rt._recv_arena.data_ptr() if rt.recv_arena_bytes else 0
+    hi = lo + rt.recv_arena_bytes
+    inside = all(lo <= p < hi for ps in ptrs0.values() for p in ps)
+    dh_inside = all(lo <= t.data_ptr() < hi for t in rt._dh_full.values())
+    tr.train_step(x, y)
+    same = set(rt._recv_bufs) == keys0 and ptrs0 == {k: [t.data_ptr() for t in v] for k, v in rt._recv_bufs.items()}
+    return dict(bytes=rt.recv_arena_bytes, n=len(keys0), inside=inside, dh_inside=dh_inside, same=same,
+                n_dh=len(rt._dh_full))
+
+
+@pytest.mark.parametrize("split_head", [False, True])
+def test_recv_arena_planned_up_front(split_head):
+    """Every receive slot of the lowered program comes from the one arena planned at init
+    (no lazy allocation inside the step, fixed addresses across steps)."""
+    res = run_world(_arena_worker, 2, split_head)
+    for r, o in res.items():
+        assert o["bytes"] > 0 and o["n"] > 0, o
+        assert o["inside"] and o["dh_inside"] and o["same"], o
+    # stage 1 receives M activations; stage 0 receives M gradients (+ head chunks)
+    assert res[0]["n"] >= M and res[1]["n"] >= M
+    if split_head:
+        assert res[1]["n_dh"] == M
