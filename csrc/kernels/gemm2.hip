@@ -35,6 +35,11 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 #define MP_G2_GROUP 8
 #endif
 
+// gemm4: accumulator row blocks (of 8) whose store is deferred into the next tile
+#ifndef MP_G4_SR
+#define MP_G4_SR 2
+#endif
+
 #ifndef MP_GROUP_MAX
 #define MP_GROUP_MAX 8
 #endif
@@ -896,6 +901,311 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// gemm4: persistent 256x256 NT GEMM (gemm3's 16x16x32 phase schedule) whose C write is
+// deferred into the NEXT tile's main loop.
+//
+// At K = 768 about a third of a gemm3 launch is the C write of each tile wave: all 256
+// CUs store their 128 KiB at the same moment while the matrix cores idle
+// (profiles/r2_probes.md "fixed vs per-K-tile cost"; hipBLASLt pays the same).  Here one
+// workgroup per CU walks tiles vb = blockIdx.x + k * gridDim.x (same XCD for every k); a
+// finished tile is packed to bf16 in registers (64 VGPRs, epilogue applied) and its 32
+// 8-byte stores per lane go out one per phase during the first 8 K-tiles of the next
+// tile, so HBM drains C while the MFMAs run.  The last tile is written after the loop.
+//
+// Operand roles are swapped by the host: the kernel computes D = A B^T with A = the
+// weight [N][K] and B = the activations [M][K], and writes D transposed into the
+// row-major C[M][N].  A lane's 16x16x32 accumulator holds 4 consecutive D rows = 4
+// consecutive C columns: one 8-byte store, one 8-byte bias load.
+//
+// vmcnt: stores retire through the same in-order counter as the half-tile DMA, so every
+// counted wait of gemm3 grows by the stores issued after its target half-tile (derivation
+// at the waits; the drain phases keep vmcnt(0)).
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+__device__ __forceinline__ void wait_vm_rt(int n) {
+  switch (n) {   // wave-uniform n: scalar branch to the immediate form
+    case 8: wait_vmcnt<8>(); break;
+    case 9: wait_vmcnt<9>(); break;
+    case 10: wait_vmcnt<10>(); break;
+    case 11: wait_vmcnt<11>(); break;
+    case 12: wait_vmcnt<12>(); break;
+    default: wait_vmcnt<0>(); break;
+  }
+}
+
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm4_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, bf16_t* __restrict__ C,
+             const bf16_t* __restrict__ bias, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+             float alpha) {
+  static_assert(EPI == EPI_NONE || EPI == EPI_BIAS, "gemm4 epilogues: none, bias");
+  constexpr int BM = 256, BN = 256, WN = 4;
+  constexpr int HALF = 128 * 128;
+  constexpr int BUF = 4 * HALF;
+  constexpr int SK = MP_G4_SR;   // K-tiles that carry the previous tile's deferred rows (one store per phase)
+  constexpr int SR = MP_G4_SR;   // accumulator row blocks deferred (the other 8 - SR are stored at the tile end)
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ swzq(8 * (wave & 1) + lr);
+  const int q = lane >> 4;
+  const int nk = K / BK;
+  const int rA = wr * 64 + (lane & 15);
+  const int rB = wc * 32 + (lane & 15);
+
+  // previous tile: stash[i][j] = D rows pm0 + 128 wr + 16 (i + shifts) + 4 q .. +3 at
+  // column pn0 + 64 wc + 16 j + (lane & 15); rows leave through stash[0] (shift())
+  u32x2 stash[SR][4];
+  int pm0 = 0, pn0 = 0;
+  bool has_prev = false;
+  auto put = [&](int j, int srow) {
+    const int r = pm0 + wr * 128 + 16 * srow + 4 * q;
+    const int c = pn0 + 64 * wc + 16 * j + (lane & 15);
+    if (r < M && c < N) __builtin_nontemporal_store(stash[0][j], reinterpret_cast<u32x2*>(C + (int64_t)c * ldc + r));
+  };
+  auto shift = [&]() {
+#pragma unroll
+    for (int i = 0; i < SR - 1; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) stash[i][j] = stash[i + 1][j];
+  };
+
+#define G4_MFMA(R0, BF, C0)                                                              \
+  __builtin_amdgcn_sched_barrier(0);                                                     \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                       \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                       \
+  _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                       \
+    acc[R0 + i_][C0 + j_] = mfma16(af[i_][s_], BF[j_][s_], acc[R0 + i_][C0 + j_]);       \
+  __builtin_amdgcn_s_setprio(0);                                                         \
+  __builtin_amdgcn_sched_barrier(0);
+#define G4_BAR()                          \
+  asm volatile("" ::: "memory");          \
+  __builtin_amdgcn_s_barrier();           \
+  asm volatile("" ::: "memory");
+
+#pragma unroll 1
+  for (int vb = blockIdx.x; vb < nwg; vb += gridDim.x) {
+    const int wg = xcd_remap(vb, nwg);
+    constexpr int GROUP = MP_G3_GROUP;
+    const int group = wg / (GROUP * gn);
+    const int first_m = group * GROUP;
+    const int gsz = min(gm - first_m, GROUP);
+    const int tm = first_m + (wg % (GROUP * gn)) % gsz;
+    const int tn = (wg % (GROUP * gn)) / gsz;
+    const int m0 = tm * BM, n0 = tn * BN;
+
+    const bf16_t* pa[2];
+    const bf16_t* pb[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      int ra = m0 + 128 * j + 8 * wave + lr;
+      ra = ra < M ? ra : M - 1;
+      int rb = n0 + 64 * ((wave >> 2) + 2 * j) + 8 * (wave & 3) + lr;
+      rb = rb < N ? rb : N - 1;
+      pa[j] = A + (int64_t)ra * lda + lc * 8;
+      pb[j] = B + (int64_t)rb * ldb + lc * 8;
+    }
+    const bool a1_ok0 = m0 + 64 + 8 * wave + lr < M, a1_ok1 = m0 + 192 + 8 * wave + lr < M;
+    const bool b1_ok0 = n0 + 64 * (wave >> 2) + 32 + 8 * (wave & 3) + lr < N;
+    const bool b1_ok1 = n0 + 64 * ((wave >> 2) + 2) + 32 + 8 * (wave & 3) + lr < N;
+    const int64_t a1_off0 = a1_ok0 ? 64 * lda : 0, a1_off1 = a1_ok1 ? 64 * lda : 0;
+    const int64_t b1_off0 = b1_ok0 ? 32 * ldb : 0, b1_off1 = b1_ok1 ? 32 * ldb : 0;
+
+    auto issue = [&](int h, int kt) {
+      char* img = smem + (kt & 1) * BUF + (h == 0 ? 0 : h == 3 ? HALF : h == 1 ? 2 * HALF : 3 * HALF);
+      const int64_t dk = (int64_t)kt * BK;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16_t* src;
+        if (h == 0) src = pa[j] + dk;
+        else if (h == 3) src = pa[j] + dk + (j ? a1_off1 : a1_off0);
+        else if (h == 1) src = pb[j] + dk;
+        else src = pb[j] + dk + (j ? b1_off1 : b1_off0);
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(img + (wave + 8 * j) * 1024), 16,
+                                         0, 0);
+      }
+    };
+
+    f32x4 acc[8][4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+
+    issue(0, 0);
+    issue(1, 0);
+    issue(2, 0);
+    issue(3, 0);
+    if (nk > 1) {
+      issue(0, 1);
+      issue(1, 1);
+      wait_vmcnt<8>();
+    } else {
+      wait_vmcnt<4>();
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+    asm volatile("" ::: "memory");
+
+    bf16x8 af[4][2], b0[2][2], b1[2][2];
+    auto fq = [&](const char* img, int row, int st) -> bf16x8 {
+      return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * ((4 * st + q) ^ swzq(row)));
+    };
+
+#pragma unroll 1
+    for (int t = 0; t < nk; ++t) {
+      const char* buf = smem + (t & 1) * BUF;
+      const bool steady = t + 2 < nk;
+      // sc: this K-tile's four phases each store one stash entry right after their wait;
+      // sp: the previous K-tile's did
+      const int sc = (has_prev && t < SK) ? 1 : 0;
+      const int sp = (has_prev && t >= 1 && t - 1 < SK) ? 1 : 0;
+      // ---- phase 1: A0 x B0.  Target B1(t), issued in phase 1 of t-1 (t = 0: prologue);
+      // younger: 4 half-tiles (8 ops) + the 4 stores of K-tile t-1
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i][s_] = fq(buf, rA + 16 * i, s_);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b0[j][s_] = fq(buf + 2 * HALF, rB + 16 * j, s_);
+      }
+      if (t + 1 < nk) issue(2, t + 1);
+      wait_vm_rt(steady ? 8 + 4 * sp : 0);
+      G4_BAR();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (sc) put(0, t);
+      G4_MFMA(0, b0, 0);
+      G4_BAR();
+      // ---- phase 2: A0 x B1.  Target A1(t) (phase 2 of t-1); younger: 8 DMA ops, the
+      // stores of phases 2-4 of t-1 and of phase 1 of t
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) b1[j][s_] = fq(buf + 3 * HALF, rB + 16 * j, s_);
+      if (t + 1 < nk) issue(3, t + 1);
+      wait_vm_rt(steady ? 8 + 3 * sp + sc : 0);
+      G4_BAR();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (sc) put(1, t);
+      G4_MFMA(0, b1, 2);
+      G4_BAR();
+      // ---- phase 3: A1 x B0; refill A0 of this buffer for K-tile t+2
+#pragma unroll
+      for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i][s_] = fq(buf + HALF, rA + 16 * i, s_);
+      if (steady) issue(0, t + 2);
+      G4_BAR();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (sc) put(2, t);
+      G4_MFMA(4, b0, 0);
+      G4_BAR();
+      // ---- phase 4: A1 x B1; refill B0.  Target B0(t+1) (phase 4 of t-1; t = 0: the last
+      // prologue issue); younger: 8 DMA ops, the store of phase 4 of t-1, phases 1-3 of t
+      if (steady) {
+        issue(1, t + 2);
+        wait_vm_rt(8 + sp + 3 * sc);
+      } else {
+        wait_vmcnt<0>();
+      }
+      G4_BAR();
+      if (sc) put(3, t);
+      G4_MFMA(4, b1, 2);
+      G4_BAR();
+      if (sc) shift();
+    }
+    if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
+    __syncthreads();
+    // short K (< SK K-tiles): the rest of the previous tile
+    if (has_prev) {
+#pragma unroll 1
+      for (int s = nk; s < SK; ++s) {
+        put(0, s);
+        put(1, s);
+        put(2, s);
+        put(3, s);
+        shift();
+      }
+    }
+    // this tile: alpha (+ bias) -> bf16; row blocks SR.. stored now, 0..SR-1 deferred
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int r = m0 + wr * 128 + 16 * i + 4 * q;
+      u32x2 bz = {0u, 0u};
+      if constexpr (EPI == EPI_BIAS) bz = *reinterpret_cast<const u32x2*>(bias + (r < M ? r : 0));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e] * alpha;
+        if constexpr (EPI == EPI_BIAS) {
+          v[0] += __uint_as_float(bz[0] << 16);
+          v[1] += __uint_as_float(bz[0] & 0xffff0000u);
+          v[2] += __uint_as_float(bz[1] << 16);
+          v[3] += __uint_as_float(bz[1] & 0xffff0000u);
+        }
+        const u32x2 o = u32x2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+        if (i < SR) {
+          stash[i < SR ? i : 0][j] = o;
+        } else {
+          const int c = n0 + 64 * wc + 16 * j + (lane & 15);
+          if (r < M && c < N) __builtin_nontemporal_store(o, reinterpret_cast<u32x2*>(C + (int64_t)c * ldc + r));
+        }
+      }
+    }
+    pm0 = m0;
+    pn0 = n0;
+    has_prev = true;
+  }
+#undef G4_MFMA
+#undef G4_BAR
+  if (has_prev) {
+#pragma unroll 1
+    for (int s = 0; s < SK; ++s) {
+      put(0, s);
+      put(1, s);
+      put(2, s);
+      put(3, s);
+      shift();
+    }
+  }
+}
+
+// C[M][N] (bf16, row stride ldc) = alpha * X[M][K] W[N][K]^T (+ bias[N]) on gemm4
+// (kernel space: D = W X^T, Mk = N, Nk = M); one workgroup per CU once the tiles
+// outnumber the CUs
+template <int EPI>
+static int launch4(const void* X, const void* W, void* C, const void* bias, int M, int N, int K, int64_t ldx,
+                   int64_t ldw, int64_t ldc, float alpha, int grid_override, hipStream_t st) {
+  constexpr int LDS = 2 * 4 * 128 * 128;
+  auto kern = gemm4_kernel<EPI>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int nwg = ((N + 255) / 256) * ((M + 255) / 256);
+  int grid = nwg < 256 ? nwg : 256;
+  if (grid_override > 0) grid = grid_override < nwg ? grid_override : nwg;   // tests: several tiles per workgroup
+  kern<<<grid, NT, LDS, st>>>((const bf16_t*)W, (const bf16_t*)X, (bf16_t*)C, (const bf16_t*)bias, N, M, K, ldw,
+                              ldx, ldc, alpha);
+  return (int)hipGetLastError();
+}
+
 
 // ---------------------------------------------------------------------------------------
 // gemms: small-tile NT engine for short-token problems (the reference model's 1024-token
@@ -1245,6 +1555,12 @@ static int launch_splitk_epi(const float* ws, void* C, int M, int N, int64_t ldc
 extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg,
                              int* split_out) {
   int split = 1;
+  // 7: the persistent deferred-store engine (gemm4); 100 + G: gemm4 on a grid of G
+  // workgroups (tests drive several tiles per workgroup through small problems)
+  if (force_cfg == 7 || force_cfg >= 100) {
+    *split_out = 1;
+    return 7;
+  }
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
   if (force_cfg >= 0 && force_cfg < 7) cfg = force_cfg;
   if (force_cfg >= 10) cfg = 0;   // placeholder; the small-engine branches below set it
@@ -1320,6 +1636,21 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
     if (c_f32_accum || split > 1 || cfg == 1) return -3;
     ws = colsum;
   }
+  // plain / bias NT GEMMs of more 256x256 tiles than CUs: the persistent engine that
+  // writes part of each tile's C during the next tile's main loop.  Opt-in
+  // (MIPIPE_GEMM4=1): correct, but 1.2-2x slower than gemm3 -- the 64-VGPR stash does not
+  // fit beside gemm3's 222 VGPRs at 2 waves/SIMD, and the spill reloads in the MFMA loop
+  // drain the DMA pipeline (profiles/r2_probes.md "gemm4")
+  static const bool use4 = [] { const char* e = getenv("MIPIPE_GEMM4"); return e && e[0] == '1'; }();
+  const bool g4_ok = split == 1 && colsum == nullptr && !c_f32_accum && !transA && !transB &&
+                     (epilogue == EPI_NONE || epilogue == EPI_BIAS) && ldc % 4 == 0;
+  const int t256_all = ((M + 255) / 256) * ((N + 255) / 256);
+  if (g4_ok && (cfg == 7 || (use4 && cfg == 5 && force_cfg < 0 && t256_all > 256))) {
+    const int grid = force_cfg >= 100 ? force_cfg - 100 : 0;
+    if (epilogue == EPI_NONE) return launch4<EPI_NONE>(A, B, C, nullptr, M, N, K, lda, ldb, ldc, alpha, grid, st);
+    return launch4<EPI_BIAS>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, grid, st);
+  }
+  if (cfg == 7) return -2;
   float* wsp = (split > 1 || colsum != nullptr) ? ws : nullptr;
   int rc = -2;
   if (!c_f32_accum && split > 1) {

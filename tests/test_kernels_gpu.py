@@ -254,6 +254,80 @@ def test_attention_dropout_consistency():
     assert abs(rel - 1.0) < 0.2
 
 
+def _keep_rate_ok(mask: torch.Tensor, p: float):
+    """Bernoulli(1 - p) keep rate within 5 sigma."""
+    n = mask.numel()
+    rate = mask.float().mean().item()
+    assert abs(rate - (1 - p)) < 5 * math.sqrt(p * (1 - p) / n), (rate, n)
+
+
+@pytest.mark.parametrize("p", [0.1, 0.3])
+def test_attention_dropout_mask_exact(p):
+    """Recover the in-kernel attention dropout mask exactly: q = k = 0 makes P uniform
+    (1/Sk) and V = I (Sk = D) turns O into the kept-mask rows, dO = I turns dV into its
+    transpose.  The forward and backward kernels must regenerate the identical mask, at
+    the requested keep rate, and differently per (batch, head)."""
+    B, S, H, D = 4, 64, 4, 64
+    T = B * S
+    q = torch.zeros(T, H * D, dtype=torch.bfloat16, device=DEV)
+    k = torch.zeros_like(q)
+    eye = torch.eye(S, D, dtype=torch.bfloat16, device=DEV)
+    v = eye.repeat(B, H)                      # every (b, h) block is I
+    o = torch.empty_like(q)
+    lse = torch.empty(B * H * S, device=DEV)
+    ops.attn_fwd(q, k, v, o, lse, B, S, S, H, H, D, False, p_drop=p, seed=1234)
+    do = v.clone()
+    dq, dk, dv = torch.zeros_like(q), torch.zeros_like(q), torch.zeros_like(q)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, S, H, H, D, False, p_drop=p, seed=1234)
+    torch.cuda.synchronize()
+    # [B, S(query), H, S(key)] masks
+    m_f = (o.float().view(B, S, H, D) > 0)
+    m_b = (dv.float().view(B, S, H, D) > 0).transpose(1, 3)   # dV[key, query] -> [B, query, H, key]
+    assert torch.equal(m_f, m_b), "forward and backward dropout masks differ"
+    _keep_rate_ok(m_f, p)
+    # kept entries carry exactly P / (1 - p)
+    kept = o.float().view(B, S, H, D)[m_f]
+    torch.testing.assert_close(kept, torch.full_like(kept, 1.0 / (S * (1 - p))), rtol=1e-2, atol=0)
+    # distinct masks per head and per batch element
+    assert not torch.equal(m_f[:, :, 0], m_f[:, :, 1])
+    assert not torch.equal(m_f[0], m_f[1])
+
+
+@pytest.mark.parametrize("p", [0.1, 0.3])
+def test_norm_dropout_mask_exact(p):
+    """Residual-branch dropout in the fused norm: x = 0, branch = 1 makes s the scaled
+    keep mask; with dy = 0, dres = 1 the backward's branch gradient is the same mask."""
+    T, D = 1024, 768
+    x = torch.zeros(T, D, dtype=torch.bfloat16, device=DEV)
+    br = torch.ones_like(x)
+    w = torch.ones(D, dtype=torch.bfloat16, device=DEV)
+    b = torch.zeros_like(w)
+    y, s, mean, rstd = ops.norm_fwd(x, w, b, br, kind="layernorm", p_drop=p, seed=99)
+    ds, dbr = ops.norm_bwd(torch.zeros_like(x), s, w, mean, rstd, kind="layernorm", dres=torch.ones_like(x),
+                           dw=torch.zeros(D, device=DEV), dbias=torch.zeros(D, device=DEV), p_drop=p, seed=99,
+                           want_branch=True)
+    torch.cuda.synchronize()
+    m_f, m_b = s.float() != 0, dbr.float() != 0
+    assert torch.equal(m_f, m_b), "forward and backward dropout masks differ"
+    _keep_rate_ok(m_f, p)
+    torch.testing.assert_close(s.float()[m_f], torch.full_like(s.float()[m_f], 1 / (1 - p)), rtol=1e-2, atol=0)
+    torch.testing.assert_close(dbr.float()[m_b], torch.full_like(dbr.float()[m_b], 1 / (1 - p)), rtol=1e-2, atol=0)
+
+
+@pytest.mark.parametrize("p", [0.1, 0.3])
+def test_act_dropout_mask_exact(p):
+    """ReLU + dropout (the reference FFN): a = 1 makes the output the scaled keep mask, and
+    act_bwd with dg = 1 must return the identical mask."""
+    T, F = 1024, 3072
+    a = torch.ones(T, F, dtype=torch.bfloat16, device=DEV)
+    out = ops.act_fwd(a, "relu", p_drop=p, seed=5)
+    da = ops.act_bwd(torch.ones_like(a), a, "relu", p_drop=p, seed=5)
+    torch.cuda.synchronize()
+    m_f, m_b = out.float() != 0, da.float() != 0
+    assert torch.equal(m_f, m_b), "forward and backward dropout masks differ"
+    _keep_rate_ok(m_f, p)
+
+
 def test_adamw():
     torch.manual_seed(0)
     n = 10007
@@ -300,6 +374,28 @@ def test_gemm2_configs(cfg, M, N, K, epi):
         k0, k1 = 0.7978845608028654, 0.044715
         t = torch.tanh(k0 * (a + k1 * a ** 3))
         ref = ref * (0.5 * (1 + t) + 0.5 * a * (1 - t * t) * k0 * (1 + 3 * k1 * a * a))
+    close(y, ref)
+
+
+@pytest.mark.parametrize("cfg", [7, 108, 103])
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (1000, 776, 512), (520, 264, 64), (1536, 1280, 128),
+                                   (2048, 512, 1344)])
+@pytest.mark.parametrize("epi", ["none", "bias"])
+def test_gemm4_persistent_deferred_store(cfg, M, N, K, epi):
+    """gemm4 (persistent 256x256 NT, part of each tile's C written during the next tile's
+    main loop) vs f32: 7 = default grid, 100 + G = G workgroups, so small problems walk
+    several tiles per workgroup (deferred stores, short-K flushes, M/N edges)."""
+    from mipipe.ops import kernels as _k
+    torch.manual_seed(0)
+    x, w, b = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1)
+    y = torch.full((M, N), float("nan"), dtype=torch.bfloat16, device=DEV)
+    alpha = 0.5 if K == 512 else 1.0
+    _k._gemm(x.to(DEV), w.to(DEV), y, bias=b.to(DEV) if epi == "bias" else None, epi=1 if epi == "bias" else 0,
+             cfg=cfg, alpha=alpha)
+    ref = alpha * (x.float() @ w.float().t())
+    if epi == "bias":
+        ref = ref + b.float()
+    assert not torch.isnan(y.float()).any(), "unwritten outputs"
     close(y, ref)
 
 
