@@ -42,3 +42,24 @@ def test_supervisor_retries_a_stalled_attempt():
     assert out["attempt"] == 1 and out["n_gpus"] == 2 and out["value"] > 0
     assert out["config"]["parallelism"] == "pp2"
     assert "attempt 0" in r.stderr
+
+
+def test_bench_eight_ranks_gpt2_small_layout():
+    """The N = 8 launch the driver makes (bench.py --gpus 8 self-launch under
+    torch.distributed.run, supervisor, PP = 8 over GPT-2 small's 12 layers with the
+    distributed head, m = 2P = 16) completes on CPU/gloo and prints one valid line."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MIPIPE_BENCH_ATTEMPT_S="200", MASTER_PORT=str(free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1", "--mbs", "1",
+           "--seq", "32", "--vocab", "512"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    c = out["config"]
+    assert out["n_gpus"] == 8 and out["value"] > 0 and c["parallelism"] == "pp8" and c["microbatches"] == 16
+    assert c["model"] == "gpt2-small" and len(c["layer_split"]) == 8
+    assert sum(b - a for a, b in c["layer_split"]) == 12
+    assert c["head"].startswith("distributed") and out["bubble_fraction"] is not None
