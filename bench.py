@@ -178,6 +178,16 @@ def supervise(a, argv) -> int:
 
 
 # ------------------------------------------------------------------------------ benchmark
+def _plain_summary():
+    """Plain forward / dX GEMM shapes per backend (ops.kernels MIPIPE_GEMM=auto timing)."""
+    from mipipe.ops import kernels as K
+    ch = K.plain_gemm_choices()
+    if not ch:
+        return None
+    return {"policy": K.GEMM_BACKEND, "hipblaslt": sorted(k for k, v in ch.items() if v == "blas"),
+            "mipipe": sum(1 for v in ch.values() if v == "hip")}
+
+
 def run(a) -> None:
     import torch
     import torch.distributed as dist
@@ -321,6 +331,7 @@ def run(a) -> None:
                    "p2p_fallback": rt.p2p.fallback_reason or None,
                    "recompute": trainer.recompute,
                    "recv_arena_mb": round(rt.recv_arena_bytes / 2 ** 20, 1),
+                   "plain_gemms": _plain_summary(),
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
                    else "last stage",
                    "head_lag": getattr(trainer, "head_lag", None),

@@ -16,9 +16,45 @@ ACT = {"none": 0, "gelu_tanh": 1, "gelu": 1, "relu": 2}
 EPI_NONE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_RELU, EPI_BIAS_RES, EPI_RES, EPI_DGELU, EPI_DRELU = range(8)
 LOG2E = 1.4426950408889634
 
-# GEMM backend for plain (epilogue-free) GEMMs on GPU: "hip" (our MFMA kernel) or "blas"
-# (hipBLASLt through torch).  Fused-epilogue GEMMs always use the HIP kernel.
+# GEMM backend for plain (epilogue-free) GEMMs on GPU: "hip" (default: our MFMA engines),
+# "blas" (hipBLASLt through torch, also for the dW GEMMs) or "auto": each plain forward /
+# dX GEMM shape is timed once on both (outside graph capture) and keeps the faster.
+# hipBLASLt wins some isolated K = 768 - 3072 NT shapes by 5-12 %
+# (profiles/r2_kernel_microbench.json) but not inside the GPT-2 / reference steps
+# (tools/ab_plain_gemm.sh: 883.6K / 889.4K tok/s auto vs 889.9K / 888.1K hip), so "auto"
+# stays opt-in.  Fused-epilogue GEMMs always use the HIP kernels.
 GEMM_BACKEND = os.environ.get("MIPIPE_GEMM", "hip")
+_PLAIN_BEST: dict = {}
+
+
+def _plain_pick(key, run_hip, run_lib) -> str:
+    """Backend of one plain GEMM shape: decided by timing both (3 runs each after a warm
+    run, CUDA events) the first time the shape is seen outside graph capture."""
+    if GEMM_BACKEND != "auto":
+        return GEMM_BACKEND
+    d = _PLAIN_BEST.get(key)
+    if d is not None:
+        return d
+    if torch.cuda.is_current_stream_capturing():
+        return "hip"
+    t = {}
+    for name, fn in (("hip", run_hip), ("blas", run_lib)):
+        fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(3):
+            fn()
+        e.record()
+        e.synchronize()
+        t[name] = s.elapsed_time(e)
+    d = "blas" if t["blas"] < 0.97 * t["hip"] else "hip"
+    _PLAIN_BEST[key] = d
+    return d
+
+
+def plain_gemm_choices() -> dict:
+    """{"fwd|dx MxNxK": backend} of the plain GEMM shapes decided so far (bench JSON)."""
+    return {f"{k[0]} {k[1]}x{k[2]}x{k[3]}": v for k, v in sorted(_PLAIN_BEST.items())}
 # GEMM engine: 2 = 8-wave glds engine (gemm2.hip) with fallback to 1 (gemm.hip) for
 # combinations v2 does not instantiate; 1 = always gemm.hip.
 GEMM_V = int(os.environ.get("MIPIPE_GEMM_V", "2"))
@@ -297,10 +333,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
             _gemm(x, w, out, bias=bias, residual=residual, epi=EPI_BIAS_RES if bias is not None else EPI_RES)
         elif bias is not None:
             _gemm(x, w, out, bias=bias, epi=EPI_BIAS)
-        elif GEMM_BACKEND == "blas":
-            torch.mm(x, w.t(), out=out)
         else:
-            _gemm(x, w, out)
+            run_hip = lambda: _gemm(x, w, out)
+            run_lib = lambda: torch.mm(x, w.t(), out=out)
+            (run_lib if _plain_pick(("fwd", T, N, K), run_hip, run_lib) == "blas" else run_hip)()
         return out, aux
     y = x.float() @ w.float().t()
     if bias is not None:
@@ -336,6 +372,18 @@ def _act_grad_cpu(x, act):
     return torch.ones_like(x)
 
 
+def _plain_dx_hip(dy, wt, out):
+    T, K = out.shape
+    N = dy.shape[1]
+    if (T // 256) * (K // 192) < 128 and N >= 4096:
+        acc = torch.zeros(T, K, device=dy.device, dtype=torch.float32)
+        _gemm(dy, wt, acc, accum=True)
+        out.copy_(acc)
+    else:
+        _gemm(dy, wt, out)
+    return out
+
+
 def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tensor] = None, act: str = "none",
               out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
               wt: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None, p_drop: float = 0.0,
@@ -347,6 +395,10 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
     K = w.shape[1]
     if out is None:
         out = torch.empty(T, K, device=dy.device, dtype=dy.dtype)
+    if (_gpu(dy) and wt is not None and act == "none" and residual is None and colsum is None and
+            _plain_pick(("dx", T, K, N), lambda: _plain_dx_hip(dy, wt, out), lambda: torch.mm(dy, w, out=out)) == "blas"):
+        torch.mm(dy, w, out=out)
+        return out
     if _gpu(dy) and wt is not None and GEMM_BACKEND != "blas":
         if act == "none" and residual is None and (T // 256) * (K // 192) < 128 and N >= 4096:
             # few output tiles, long reduction (a distributed-head chunk: [Tc, D] = dl[Tc, V] W):
