@@ -544,8 +544,11 @@ class Block:
         return y
 
     def _mha_bwd(self, prefix, dout, xq, xkv, B, S, seed, st, key, self_attn, wjobs, dres_q, dres_kv):
-        """Returns (dxq, dxkv) with the residual grads folded in.  The out_proj bias grad
-        (column sums of ``dout``) was accumulated by the norm backward that produced it."""
+        """Self-attention: returns (dx, None), the residual grad folded in.  Cross-attention:
+        returns (dxq, dkv) -- the K/V projections' input gradient is left to the caller,
+        which folds it into the block input's gradient as a residual GEMM epilogue (no
+        separate add).  The out_proj bias grad was accumulated by the norm backward that
+        produced ``dout``."""
         cfg = self.cfg
         H, Dh, d = cfg.n_heads, cfg.head_dim, cfg.d_model
         W = self.w(prefix + ".in_proj_weight")
@@ -564,21 +567,25 @@ class Block:
             dq = torch.empty_like(q)
             dkv = torch.empty_like(kv)
             dk, dv = dkv[:, :d], dkv[:, d:]
+        # the in_proj bias grads stay weight-gradient jobs (colsum kernels off the critical
+        # path): the attention kernels' fused column sums (dbias=) cost 5 % of the reference
+        # step here (tools/ab_ref_dbias.sh: 574-579K vs 609-610K tok/s, L8H8)
         ops.attn_bwd(q, k, v, o, do, st[key + "lse"], dq, dk, dv, B, S, S, H, H, Dh, False, p_drop=cfg.dropout,
                      seed=seed)
         if self_attn:
-            wjobs.append(ops.DW(dqkv, xq, gW))
             wjobs.append(lambda dqkv=dqkv: ops.colsum(dqkv, gb))
+        else:
+            wjobs.append(lambda dq=dq: ops.colsum(dq, gb[:d]))
+            wjobs.append(lambda dkv=dkv: ops.colsum(dkv, gb[d:]))
+        if self_attn:
+            wjobs.append(ops.DW(dqkv, xq, gW))
             dx = ops.linear_dx(dqkv, W, residual=dres_q, wt=self.wt(prefix + ".in_proj_weight"))
             return dx, None
         wjobs.append(ops.DW(dq, xq, gW[:d]))
-        wjobs.append(lambda dq=dq: ops.colsum(dq, gb[:d]))
         wjobs.append(ops.DW(dkv, xkv, gW[d:]))
-        wjobs.append(lambda dkv=dkv: ops.colsum(dkv, gb[d:]))
         WT = self.wt(prefix + ".in_proj_weight")
         dxq = ops.linear_dx(dq, W[:d], residual=dres_q, wt=None if WT is None else WT[:, :d])
-        dxkv = ops.linear_dx(dkv, W[d:], residual=dres_kv, wt=None if WT is None else WT[:, d:])
-        return dxq, dxkv
+        return dxq, dkv
 
     def _ref_backward(self, dy, B, S, st, sd, wjobs):
         cfg = self.cfg
@@ -601,15 +608,19 @@ class Block:
                                 dbias=self.g("norm2.bias"), p_drop=p, seed=_seed(sd, 4), want_branch=True,
                                 colsum_branch=self.g("multihead_attn.out_proj.bias"))
         h, x1 = st["x"], st["x1"]
-        dx1, dh_mem = self._mha_bwd("multihead_attn", dca, x1, h, B, S, _seed(sd, 3), st, "ca_", False, wjobs,
-                                    dres_q=ds2, dres_kv=None)
+        dx1, dkv_mem = self._mha_bwd("multihead_attn", dca, x1, h, B, S, _seed(sd, 3), st, "ca_", False, wjobs,
+                                     dres_q=ds2, dres_kv=None)
         # norm1(h + drop(sa))
         ds1, dsa = ops.norm_bwd(dx1, st["s1"], self.w("norm1.weight"), st["mu1"], st["rs1"], dw=self.g("norm1.weight"),
                                 dbias=self.g("norm1.bias"), p_drop=p, seed=_seed(sd, 2), want_branch=True,
                                 colsum_branch=self.g("self_attn.out_proj.bias"))
-        dres = ds1 + dh_mem
-        dh, _ = self._mha_bwd("self_attn", dsa, h, h, B, S, _seed(sd, 1), st, "sa_", True, wjobs, dres_q=dres,
+        dh, _ = self._mha_bwd("self_attn", dsa, h, h, B, S, _seed(sd, 1), st, "sa_", True, wjobs, dres_q=ds1,
                               dres_kv=None)
+        # memory = h (helper:52): the cross-attention K/V projections' input gradient
+        # accumulates into dh through the residual epilogue of their dX GEMM, in place
+        d = cfg.d_model
+        W, WT = self.w("multihead_attn.in_proj_weight"), self.wt("multihead_attn.in_proj_weight")
+        ops.linear_dx(dkv_mem, W[d:], residual=dh, out=dh, wt=None if WT is None else WT[:, d:])
         return dh
 
 
