@@ -47,7 +47,7 @@ class TrainSection:
     recompute: Union[bool, str] = False   # True, False or "auto" (engine.plan_recompute: HBM plan)
     graphs: Optional[bool] = None       # HIP-graph replay + native stage runner (None: on for GPU)
     seed: int = 0
-    data: str = "synthetic"             # synthetic | path to a uint16/int32 token file (memory-mapped)
+    data: str = "synthetic"             # synthetic | pattern[:K] (learnable permutation walk) | path to a uint16/int32 token file (memory-mapped)
     log_every: int = 10
     metrics_file: Optional[str] = None  # JSONL, one record per logged step
     ckpt_dir: Optional[str] = None

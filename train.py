@@ -30,22 +30,39 @@ def parse():
 
 
 class TokenData:
-    """Synthetic uniform tokens, or random windows of a memory-mapped token file
-    (uint16 ``.bin`` / int32 ``.i32``), deterministic in (step, dp rank)."""
+    """Synthetic uniform tokens, a learnable synthetic stream (``pattern[:K]``: every
+    sequence walks a fixed random permutation of K tokens, x[t+1] = perm[x[t]], from a
+    random start -- a model that learns the K-entry successor table drives the loss to 0),
+    or random windows of a memory-mapped token file (uint16 ``.bin`` / int32 ``.i32``);
+    deterministic in (step, dp rank)."""
 
     def __init__(self, spec: str, vocab: int, n_seq: int, seq: int, device, dp_rank: int, seed: int):
         import numpy as np
         self.spec, self.vocab, self.n, self.S = spec, vocab, n_seq, seq
         self.device, self.dp_rank, self.seed = device, dp_rank, seed
         self.mm = None
-        if spec != "synthetic":
+        self.perm = None
+        if spec.startswith("pattern"):
+            import torch
+            k = int(spec.split(":")[1]) if ":" in spec else min(vocab, 4096)
+            g = torch.Generator().manual_seed(seed + 7)
+            self.perm = torch.randperm(min(k, vocab), generator=g).to(device)
+        elif spec != "synthetic":
             dt = np.int32 if spec.endswith(".i32") else np.uint16
             self.mm = np.memmap(spec, dtype=dt, mode="r")
 
     def batch(self, step: int):
         import numpy as np
         import torch
-        if self.mm is None:
+        if self.perm is not None:
+            g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + step * 131 + self.dp_rank)
+            cur = torch.randint(0, self.perm.numel(), (self.n,), device=self.device, generator=g)
+            cols = [cur]
+            for _ in range(self.S):
+                cur = self.perm[cur]
+                cols.append(cur)
+            x = torch.stack(cols, 1)
+        elif self.mm is None:
             g = torch.Generator(device=self.device).manual_seed(self.seed * 1000003 + step * 131 + self.dp_rank)
             x = torch.randint(0, self.vocab, (self.n, self.S + 1), device=self.device, generator=g)
         else:
