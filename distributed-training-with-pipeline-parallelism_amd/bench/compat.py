@@ -146,7 +146,9 @@ def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_siz
                                                     mbs=batch_size // num_microbatches, seq_len=seq_length))
             else:
                 model = Transformer(args)
-                stages.append(manual_model_split(model, stage_idx, num_stages, dev))
+                st = manual_model_split(model, stage_idx, num_stages, dev)
+                st.graphs = use_gpu   # the user module's fwd/bwd replayed as HIP graphs per microbatch slot
+                stages.append(st)
         cls = get_schedule_class(schedule_type)
         schedule = cls(stages if spw > 1 or schedule_type == "Interleaved1F1B" else stages[0],
                        n_microbatches=num_microbatches, loss_fn=loss_fn)

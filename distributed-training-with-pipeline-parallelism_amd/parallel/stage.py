@@ -97,7 +97,8 @@ class PipelineStage(StageBase):
     """
 
     def __init__(self, submodule: nn.Module, stage_index: int, num_stages: int, device: torch.device,
-                 input_args: Any = None, output_args: Any = None, group=None, dw_builder=None):
+                 input_args: Any = None, output_args: Any = None, group=None, dw_builder=None, *,
+                 graphs: bool = False):
         if not 0 <= stage_index < num_stages:
             raise ValueError(f"stage_index {stage_index} out of range for {num_stages} stages")
         self.submod = submodule
@@ -112,6 +113,14 @@ class PipelineStage(StageBase):
         self._fwd_cache: Dict[int, Tuple[Tuple[torch.Tensor, ...], Tuple[torch.Tensor, ...]]] = {}
         self._loss_cache: Dict[int, torch.Tensor] = {}
         self.dp_group = None
+        # HIP graphs for the user module (GPU only): one graphed forward/backward pair per
+        # microbatch slot (torch.cuda.make_graphed_callables), so microbatches in flight
+        # never share the static activation buffers.  Launch-bound short-token stages (the
+        # reference's 1024-token microbatches: hundreds of small ATen kernels) replay each
+        # direction as one graph.  Captured lazily on the first forward of each slot.
+        self.graphs = bool(graphs)
+        self._graph_fns: Dict[int, Callable] = {}
+        self._orig_forward: Optional[Callable] = None
 
     # reference-visible attributes
     @property
@@ -131,14 +140,39 @@ class PipelineStage(StageBase):
                 a = a.detach().requires_grad_(True)
             inputs.append(a)
         inputs = tuple(inputs)
+        fwd = self._graphed_fn(mb, inputs) if self.graphs and self.device.type == "cuda" else self.submod
         with torch.enable_grad():
-            out = _as_tuple(self.submod(*inputs))
+            out = _as_tuple(fwd(*inputs))
             loss = None
             if self.is_last and loss_fn is not None:
                 loss = loss_fn(out[0] if len(out) == 1 else out, target)
                 self._loss_cache[mb] = loss * loss_scale if loss_scale != 1.0 else loss
         self._fwd_cache[mb] = (inputs, out)
         return tuple(o.detach() for o in out), loss
+
+    def _graphed_fn(self, mb: int, inputs: Tuple[torch.Tensor, ...]) -> Callable:
+        fn = self._graph_fns.get(mb)
+        if fn is None:
+            mod = self.submod
+            # make_graphed_callables patches module.forward with the graphed function:
+            # keep the original for the next slot's capture and for eager calls
+            if self._orig_forward is None:
+                self._orig_forward = mod.forward
+            mod.forward = self._orig_forward
+            # the graphed backward hands its static grad buffers to AccumulateGrad, which
+            # would adopt one as .grad (no copy) while .grad is None -- and the next replay
+            # of that slot would overwrite it: give every parameter its own .grad first
+            for p in mod.parameters():
+                if p.requires_grad and p.grad is None:
+                    p.grad = torch.zeros_like(p)
+            sample = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in inputs)
+            # warmup iterations use autograd.grad (no .grad accumulation); the module's
+            # dropout draws from the graph-registered generator state on every replay
+            torch.cuda.make_graphed_callables(mod, sample, num_warmup_iters=3)
+            fn = mod.forward
+            mod.forward = self._orig_forward
+            self._graph_fns[mb] = fn
+        return fn
 
     def backward_mb(self, mb, grad_outputs):
         inputs, out = self._fwd_cache.pop(mb)

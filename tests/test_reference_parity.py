@@ -99,3 +99,54 @@ def test_trainer_reference_export_import_with_distributed_head():
     out = export_reference_stage(tr)
     for k, v in full.state_dict().items():
         assert torch.equal(out[k], v), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_graphed_autograd_stage_matches_eager(dropout):
+    """PipelineStage(graphs=True): the reference's own f32 nn.Module replayed as one HIP
+    graph per direction and microbatch slot gives the eager stage's loss and gradients
+    (dropout 0: to f32 tolerance over 3 steps of 4 microbatches; dropout 0.1: finite,
+    different masks per replay)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mipipe.parallel.api import Schedule1F1B
+    dev = torch.device("cuda", 0)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    a = ModelArgs(dim=128, n_layers=2, n_heads=4, vocab_size=256, dim_feedforward=256, dropout=dropout)
+    torch.manual_seed(0)
+    base = Transformer(a)
+    g = torch.Generator().manual_seed(1)
+    xs = [torch.randint(0, 256, (16, 32), generator=g).to(dev) for _ in range(3)]
+    ys = [torch.randint(0, 256, (16, 32), generator=g).to(dev) for _ in range(3)]
+    res = {}
+    for graphs in (False, True, "eager2"):
+        model = Transformer(a)
+        model.load_state_dict(base.state_dict())
+        stage = manual_model_split(model, 0, 1, dev)
+        stage.graphs = graphs is True
+        sched = Schedule1F1B(stage, n_microbatches=4, loss_fn=tokenwise_loss_fn(256))
+        losses = []
+        for x, y in zip(xs, ys):
+            ls = []
+            sched.step(x, target=y, losses=ls)
+            losses.append(torch.stack([l.detach() for l in ls]).cpu())
+        grads = {n: p.grad.detach().cpu().clone() for n, p in stage.submod.named_parameters()}
+        res[graphs] = (torch.stack(losses), grads)
+        assert (len(stage._graph_fns) == 4) == (graphs is True)
+    (l0, g0), (l1, g1), (_, g2) = res[False], res[True], res["eager2"]
+    assert torch.isfinite(l1).all()
+    if dropout == 0.0:
+        torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-5)
+        bad = []
+        for n in g0:
+            # tolerance: a few times the eager-vs-eager spread (atomic-order effects) + f32 noise
+            spread = (g2[n] - g0[n]).abs().max().item()
+            dev_g = (g1[n] - g0[n]).abs().max().item()
+            scale = g0[n].abs().max().item()
+            print(n, f"eager-eager {spread:.3g} graph-eager {dev_g:.3g} |g| {scale:.3g}")
+            if dev_g > 4 * spread + 1e-5 * max(1e-2, scale):
+                bad.append((n, dev_g, spread, scale))
+        assert not bad, bad
+    else:
+        assert not torch.equal(l1[0], l1[1])

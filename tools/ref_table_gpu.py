@@ -104,7 +104,8 @@ def main_fp32(a):
     (nn.TransformerDecoderLayer, f32, dropout 0.1) split by manual_model_split into one
     stage, Schedule1F1B(m=4) from mipipe.parallel.api, run_train_iterations' 2 warmup + 5
     timed fwd+bwd steps (no optimizer, as helper:98-143) -- on one MI355X (ATen f32 compute
-    through hipBLASLt / MIOpen; the HIP kernels of this framework are bf16-only)."""
+    through hipBLASLt / MIOpen; the HIP kernels of this framework are bf16-only), with the
+    stage replayed as HIP graphs (PipelineStage(graphs=True); --no-graphs: eager)."""
     import torch
     import mipipe  # noqa: F401
     from mipipe.bench.compat import run_train_iterations
@@ -121,6 +122,7 @@ def main_fp32(a):
             torch.manual_seed(L * 100 + H)
             args = ModelArgs(n_layers=L, n_heads=H)
             stage = manual_model_split(Transformer(args), 0, 1, dev)
+            stage.graphs = not a.no_graphs   # one HIP graph per direction and microbatch slot
             sched = Schedule1F1B(stage, n_microbatches=m, loss_fn=tokenwise_loss_fn(args.vocab_size))
             x = torch.randint(0, args.vocab_size, (B, S), device=dev)
             y = torch.randint(0, args.vocab_size, (B, S), device=dev)
@@ -138,7 +140,8 @@ def main_fp32(a):
             torch.cuda.empty_cache()
     summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
                          "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, **f32** (the reference's precision; ATen "
-                         "compute, TF32 off), fwd+bwd only (no optimizer), reference-compatible API",
+                         "compute, TF32 off), fwd+bwd only (no optimizer), reference-compatible API, "
+                         + ("eager" if a.no_graphs else "HIP graphs per microbatch slot (PipelineStage(graphs=True))"),
                "rows": out}
     if a.json:
         with open(a.json, "w") as f:
