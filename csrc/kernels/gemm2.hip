@@ -1447,7 +1447,14 @@ static int choose(int M, int N, int K, bool acc, bool outer, int* split_out) {
     const float area = (float)(CFGS[c].bm * CFGS[c].bn) / (256.f * 256.f) * (c == 3 ? 2.f : 1.f);
     // bf16 outputs split too (f32 slabs + one reduce pass that applies the epilogue):
     // small-M problems (1024-token microbatches) otherwise fill 24-48 of 256 CUs
-    const int max_split = acc ? (kt / 4 < 32 ? kt / 4 : 32) : (kt / 3 < 8 ? kt / 3 : 8);
+    // MIPIPE_DW_MAXSPLIT: cap on the f32-accumulate split-K factor (default 32)
+    static const int acc_cap = [] {
+      const char* e = getenv("MIPIPE_DW_MAXSPLIT");
+      const int v = e ? atoi(e) : 32;
+      return v > 0 ? v : 32;
+    }();
+    const int acc_max = kt / 4 < acc_cap ? kt / 4 : acc_cap;
+    const int max_split = acc ? acc_max : (kt / 3 < 8 ? kt / 3 : 8);
     for (int s = 1; s <= (max_split > 1 ? max_split : 1); ++s) {
       const int work = tiles * s;
       const int rounds = (work + slots - 1) / slots;
