@@ -1208,6 +1208,163 @@ static int launch4(const void* X, const void* W, void* C, const void* bias, int 
 
 
 // ---------------------------------------------------------------------------------------
+// gemm5 (probe, opt-in: 0.7-0.8x gemm3, profiles/r2_probes.md): 256x256 NT with 4 waves, ONE wave per SIMD (512 registers: a 128x128
+// accumulator per wave in 256 AGPRs), instead of gemm3's 8 waves in ping-pong pairs.
+// Per K-tile (BK = 64) a wave reads 32 KiB of fragments (gemm3: 24 KiB x 8 waves) and
+// issues 128 MFMAs; fragments are register double-buffered by 32-deep k-step, so the
+// ds_reads of the next k-step (and the next K-tile's DMA) interleave with the current
+// k-step's MFMAs (sched_group_barrier).  2 LDS buffers, one barrier per K-tile.
+// ---------------------------------------------------------------------------------------
+template <int EPI>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm5_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
+             const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+             float* __restrict__ WS, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr,
+             int64_t ldx, float alpha, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  constexpr int BM = 256, BN = 256, NTH5 = 256;
+  constexpr int IMG = 256 * 128;          // one operand image: 256 rows x 64 k (128 B rows)
+  constexpr int BUF = 2 * IMG;            // A | B
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int wg = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GROUP = MP_G3_GROUP;
+  const int group = wg / (GROUP * gn);
+  const int first_m = group * GROUP;
+  const int gsz = min(gm - first_m, GROUP);
+  const int tm = first_m + (wg % (GROUP * gn)) % gsz;
+  const int tn = (wg % (GROUP * gn)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63, q = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nk = K / BK;
+
+  // DMA: 64 pieces of 1 KiB per K-tile (A rows 0..255 = pieces 0..31, B = 32..63); wave w
+  // issues pieces w, w + 4, ..., each lane 16 bytes: image row 8 p' + (lane >> 3), physical
+  // chunk lane & 7 <- logical chunk (lane & 7) ^ swzq(row)
+  const int lr = lane >> 3;
+  const bf16_t* src[16];
+  int dst[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int piece = wave + 4 * u;                  // 0..63
+    const bool isb = piece >= 32;
+    const int prow = (piece & 31) * 8 + lr;          // image row
+    const int lc = (lane & 7) ^ swzq(prow);
+    int gr = (isb ? n0 : m0) + prow;
+    const int lim = isb ? N : M;
+    gr = gr < lim ? gr : lim - 1;
+    src[u] = (isb ? B : A) + (int64_t)gr * (isb ? ldb : lda) + lc * 8;
+    dst[u] = (isb ? IMG : 0) + (piece & 31) * 1024;
+  }
+  auto issue = [&](int kt) {
+    char* base = smem + (kt & 1) * BUF;
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      __builtin_amdgcn_global_load_lds((const void*)(src[u] + (int64_t)kt * BK),
+                                       (__attribute__((address_space(3))) void*)(base + dst[u]), 16, 0, 0);
+  };
+  auto fq = [&](const char* img, int row, int st) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * ((4 * st + q) ^ swzq(row)));
+  };
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{};
+
+  const int rA = wr * 128 + (lane & 15), rB = wc * 128 + (lane & 15);
+  bf16x8 a0[8], b0[8], a1[8], b1[8];
+
+  issue(0);
+  if (nk > 1) issue(1);
+  if (nk > 1) wait_vmcnt<16>(); else wait_vmcnt<0>();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    a0[i] = fq(smem, rA + 16 * i, 0);
+    b0[i] = fq(smem + IMG, rB + 16 * i, 0);
+  }
+
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    // (A) k-step 0 MFMAs; the k-step 1 fragments of this K-tile load meanwhile
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a1[i] = fq(buf, rA + 16 * i, 1);
+      b1[i] = fq(buf + IMG, rB + 16 * i, 1);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a0[i], b0[j], acc[i][j]);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+    }
+    // (B) every wave done reading this buffer, the next K-tile landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_vmcnt<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // (C, D) DMA of K-tile t+2 into this buffer; k-step 1 MFMAs while the next K-tile's
+    // k-step 0 fragments load
+    if (t + 2 < nk) issue(t + 2);
+    const char* nbuf = smem + ((t + 1) & 1) * BUF;
+    if (t + 1 < nk) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        a0[i] = fq(nbuf, rA + 16 * i, 0);
+        b0[i] = fq(nbuf + IMG, rB + 16 * i, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = mfma16(a1[i], b1[j], acc[i][j]);
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x8, 4, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue<BM, BN, 2, 2, EPI, false, NTH5>(Stage16<8, 8>{acc, wc * 128, lane}, smem, m0, n0, wr, Cv, bias, R, AUX,
+                                           WS, M, N, ldc, ldr, ldx, alpha, 1, p_drop, seed);
+}
+
+template <int EPI>
+static int launch5(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
+                   int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
+                   float p_drop, uint64_t seed, hipStream_t st) {
+  constexpr int LDS_MAIN = 2 * 2 * 256 * 128;
+  constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
+  constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
+  auto kern = gemm5_kernel<EPI>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int nwg = ((M + 255) / 256) * ((N + 255) / 256);
+  kern<<<nwg, 256, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (const bf16_t*)R,
+                              (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
+  return (int)hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------------------
 // gemms: small-tile NT engine for short-token problems (the reference model's 1024-token
 // microbatches: M = 1024, N = 768..2304).  A 256x256 grid there has 12-36 tiles for 256
 // CUs, and split-K to fill the chip costs an f32 slab round trip plus a reduce/epilogue
@@ -1492,6 +1649,9 @@ static int dispatch(int cfg, const void* A, const void* B, void* C, const void* 
     if (cfg == 12) return launchs<32, 32, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    if constexpr (!ACC) {
+      if (cfg == 8) return launch5<EPI>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
+    }
   }
   switch (cfg) {
     case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
@@ -1568,6 +1728,13 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
     *split_out = 1;
     return 7;
   }
+  // 8: the 4-wave / one-wave-per-SIMD 256x256 NT engine (gemm5 probe; MIPIPE_GEMM5=1 uses
+  // it wherever gemm3's M16 build would run without split-K)
+  static const bool use5 = [] { const char* e = getenv("MIPIPE_GEMM5"); return e && e[0] == '1'; }();
+  if (force_cfg == 8) {
+    *split_out = 1;
+    return 8;
+  }
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
   if (force_cfg >= 0 && force_cfg < 7) cfg = force_cfg;
   if (force_cfg >= 10) cfg = 0;   // placeholder; the small-engine branches below set it
@@ -1623,6 +1790,7 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
       split = 1;
     }
   }
+  if (use5 && cfg == 5 && split == 1 && !c_f32_accum && force_cfg < 0) cfg = 8;
   *split_out = split;
   return cfg;
 }

@@ -347,7 +347,7 @@ def test_adamw():
     assert abs(ss.item() - (g.double() ** 2).sum().item()) / ss.item() < 1e-4
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 10, 11, 12])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 8, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, "bias_gelu"), (1000, 2304, 256, "bias"), (256, 384, 128, "res"),
                                        (520, 136, 64, "none"), (512, 768, 3072, "dgelu"), (1000, 1000, 640, "none"),
                                        (768, 512, 128, "bias")])

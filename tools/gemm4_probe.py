@@ -1,4 +1,4 @@
-"""gemm4 (persistent, deferred C stores) vs gemm3 (cfg 5) vs hipBLASLt on the NT shapes it
+"""gemm4 (persistent, deferred C stores), gemm5 (4 waves, one per SIMD) vs gemm3 (cfg 5) vs hipBLASLt on the NT shapes it
 takes by default (plain / bias GEMMs of more than 256 256x256 tiles).  One MI355X."""
 import sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -31,11 +31,14 @@ for name, M, N, K, bias in SHAPES:
     y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     y3 = torch.empty_like(y)
     res = {}
-    for tag, cfg, out in (("g3", 5, y3), ("g4", 7, y)):
+    y5 = torch.empty_like(y)
+    for tag, cfg, out in (("g3", 5, y3), ("g4", 7, y), ("g5", 8, y5)):
         res[tag] = bench(lambda: _k._gemm(x, w, out, bias=b, epi=bias, cfg=cfg))
     res["lib"] = bench(lambda: torch.nn.functional.linear(x, w, b))
     err = (y.float() - y3.float()).abs().max().item()
+    err5 = (y5.float() - y3.float()).abs().max().item()
     fl = 2.0 * M * N * K
     print(f"{name:16s} M={M} N={N} K={K}: gemm3 {res['g3']:8.1f} us ({fl / res['g3'] / 1e6:6.0f} TF)  "
           f"gemm4 {res['g4']:8.1f} us ({fl / res['g4'] / 1e6:6.0f} TF)  hipBLASLt {res['lib']:8.1f} us "
-          f"({fl / res['lib'] / 1e6:6.0f} TF)  max|g4-g3| {err:.3g}", flush=True)
+          f"({fl / res['lib'] / 1e6:6.0f} TF)  gemm5 {res['g5']:8.1f} us ({fl / res['g5'] / 1e6:6.0f} TF)  "
+          f"max|g4-g3| {err:.3g} max|g5-g3| {err5:.3g}", flush=True)
