@@ -15,8 +15,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(n, *args, port):
-    env = dict(os.environ, MIPIPE_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+def _run(n, *args, port, backend="gloo"):
+    env = dict(os.environ, MIPIPE_DIST_BACKEND=backend, OMP_NUM_THREADS="2")
+    if backend != "gloo":
+        env.pop("MIPIPE_DIST_BACKEND")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "tools", "mp_gpu_check.py")] + list(args)
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=ROOT)
@@ -64,3 +66,32 @@ def test_multirank_gpu_interleaved_matches_single(reference8, n, graphs, split):
                "--split-head", str(split), port=29860 + n + 10 * graphs + 20 * split)
     assert res["losses"] == pytest.approx(reference8, rel=2e-3)
     assert res["native_runner"] == bool(graphs), res["native_reason"]
+
+
+@pytest.mark.parametrize("n,schedule,graphs,split,dp", [(2, "1F1B", 1, 1, 1), (4, "1F1B", 1, 1, 1),
+                                                        (4, "GPipe", 0, 0, 1), (8, "1F1B", 1, 1, 2)])
+def test_rccl_one_gpu_per_rank_matches_single(reference, n, schedule, graphs, split, dp):
+    """The real multi-GPU path: one rank per GPU, RCCL (nccl backend) with the native p2p
+    engine, HIP graphs + the native tape.  Needs n GPUs in one node (skipped on the
+    one-GPU box: two RCCL ranks cannot share a device, tools/rccl_shared_gpu_probe.py)."""
+    if torch.cuda.device_count() < n:
+        pytest.skip(f"needs {n} GPUs")
+    res = _run(n, "--schedule", schedule, "--graphs", str(graphs), "--split-head", str(split), "--dp", str(dp),
+               port=29850 + n + 10 * graphs + 20 * split + 40 * dp, backend="nccl")
+    assert res["losses"] == pytest.approx(reference, rel=2e-3)
+    assert res["p2p"] == "native", res
+    assert res["native_runner"] == bool(graphs), res["native_reason"]
+
+
+@pytest.mark.parametrize("schedule,v", [("1F1B", 1), ("ZBH1", 1)])
+def test_rccl_pp8_matches_single(reference8, schedule, v):
+    """PP = 8 over 8 GPUs (one layer per stage), RCCL + native p2p + graphs.  Skipped
+    below 8 GPUs."""
+    if torch.cuda.device_count() < 8:
+        pytest.skip("needs 8 GPUs")
+    args = ["--layers", "8", "--schedule", schedule, "--graphs", "1", "--split-head", "1"]
+    if v > 1:
+        args += ["--vstages", str(v)]
+    res = _run(8, *args, port=29890 + v, backend="nccl")
+    assert res["losses"] == pytest.approx(reference8, rel=2e-3)
+    assert res["p2p"] == "native", res

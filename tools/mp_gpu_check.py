@@ -56,7 +56,8 @@ def main():
     if rank == 0:
         print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses,
                           "native_runner": tr.runtime.native_runner is not None,
-                          "native_reason": tr.runtime.native_reason}), flush=True)
+                          "native_reason": tr.runtime.native_reason,
+                          "p2p": getattr(tr.runtime.p2p, "kind", None)}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
