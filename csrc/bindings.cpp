@@ -20,6 +20,8 @@ int mp_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out
 int mp_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int T, int S, int D, int pos_offset,
                  hipStream_t st);
 int mp_sumsq(const float* g, int64_t n, float* out, hipStream_t st);
+int mp_gemm_f32(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int64_t lda,
+                int a_kc, int64_t ldb, int b_nc, int64_t ldc, float alpha, int accumulate, hipStream_t st);
 int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, hipStream_t st);
 int mp_adamw(float* p, float* g, float* m, float* v, void* w16, int64_t n, int64_t n_decay, float lr, float b1,
              float b2, float eps, float wd, int step, const float* sumsq, float max_norm, float grad_scale,
@@ -429,6 +431,33 @@ namespace mipipe_runtime {
 void register_runner(pybind11::module& m);
 }
 
+// f32 MFMA GEMM: C (+)= alpha * A @ B (+ bias); A [M,K], B [K,N] 2-D views with either inner
+// stride 1; returns 1 if done, 0 if the layout is not supported (caller falls back)
+int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> bias, double alpha,
+                 bool accumulate) {
+  TORCH_CHECK(A.scalar_type() == torch::kFloat32 && B.scalar_type() == torch::kFloat32 &&
+                  C.scalar_type() == torch::kFloat32, "gemm_f32: f32 tensors");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_f32: 2-D");
+  const int M = A.size(0), K = A.size(1), N = B.size(1);
+  TORCH_CHECK(B.size(0) == K && C.size(0) == M && C.size(1) == N, "gemm_f32: shape mismatch");
+  if (C.stride(1) != 1) return 0;
+  int a_kc, b_nc;
+  int64_t lda, ldb;
+  if (A.stride(1) == 1) { a_kc = 1; lda = A.stride(0); }
+  else if (A.stride(0) == 1) { a_kc = 0; lda = A.stride(1); }
+  else return 0;
+  if (B.stride(1) == 1) { b_nc = 1; ldb = B.stride(0); }
+  else if (B.stride(0) == 1) { b_nc = 0; ldb = B.stride(1); }
+  else return 0;
+  if (bias.has_value()) TORCH_CHECK(bias->is_contiguous() && bias->numel() == N, "gemm_f32: bias [N]");
+  const int rc = mp_gemm_f32(A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(),
+                             bias.has_value() ? bias->data_ptr<float>() : nullptr, M, N, K, lda, a_kc, ldb, b_nc,
+                             C.stride(0), (float)alpha, accumulate ? 1 : 0, cur_stream());
+  if (rc == -1) return 0;
+  check(rc, "gemm_f32");
+  return 1;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mipipe_comm::register_rccl(m);
   mipipe_runtime::register_runner(m);
@@ -439,6 +468,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("sumsq", &sumsq);
+  m.def("gemm_f32", &gemm_f32);
   m.def("adamw", &adamw);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("act_fwd", &act_fwd);

@@ -1,0 +1,158 @@
+// f32 GEMM on the f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, f32
+// accumulate, 64 FLOP/clk/SIMD -- gfx950 has no xf32/TF32 fast path; cdna guide §3
+// "FP32-input MFMA").  SURVEY §7.1 gemm_f32.hip: the reference's own workload runs in
+// f32 (helper:36-46, no autocast), and this is the matmul of the reference-precision
+// path (ops.linear_f32 / ops.f32_linears(): every nn.Linear / MultiheadAttention
+// projection of an f32 module, forward and both backward GEMMs).
+//
+//   C[M][N] (f32, row stride ldc) = alpha * A B (+ bias[N]) (+ C if accumulate)
+//   A(m, k) = A[m * lda + k] (A_KC: K-contiguous) or A[k * lda + m] (M-contiguous)
+//   B(k, n) = B[k * ldb + n] (B_NC: N-contiguous) or B[n * ldb + k] (K-contiguous)
+//
+// 128x128 tile, BK = 32, 256 threads (2 x 2 waves of 64x64 = 2 x 2 blocks of 32x32).  Both
+// operands are staged k-major in LDS ([k][m], [k][n], padded rows), so a 32x32x2 fragment
+// read (lane l: row/col base + l % 32, k = kk + l / 32) is one conflict-free ds_read_b32
+// per operand.  Global -> register prefetch of K-tile t+1 overlaps the MFMAs of tile t;
+// two LDS buffers, one barrier per K-tile.
+#include "mp_common.h"
+
+using namespace mp;
+
+namespace gf32 {
+
+constexpr int BM = 128, BN = 128, BK = 32, NTH = 256, PAD = 4;
+constexpr int LDA_S = BM + PAD, LDB_S = BN + PAD;
+
+template <bool A_KC, bool B_NC>
+__global__ void __launch_bounds__(NTH, 2) gemm_f32_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                          float* __restrict__ C, const float* __restrict__ bias,
+                                                          int M, int N, int K, int64_t lda, int64_t ldb,
+                                                          int64_t ldc, float alpha, int accumulate) {
+  __shared__ __attribute__((aligned(16))) float As[2][BK][LDA_S];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB_S];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hl = lane >> 5;
+  const int wave = tid >> 6, wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int gn = (N + BN - 1) / BN;
+  const int m0 = (blockIdx.x / gn) * BM, n0 = (blockIdx.x % gn) * BN;
+  const int nk = (K + BK - 1) / BK;
+
+  // 1024 float4 per operand tile, 4 per thread
+  float4 ra[4], rb[4];
+  auto load = [&](int kt) {
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = tid + NTH * u;
+      // A
+      if constexpr (A_KC) {         // rows m, 8 float4 along k
+        const int r = idx >> 3, k = k0 + (idx & 7) * 4;
+        const int m = m0 + r;
+        ra[u] = (m < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)m * lda + k) : float4{0, 0, 0, 0};
+      } else {                      // k-rows, 32 float4 along m
+        const int kr = idx >> 5, m = m0 + (idx & 31) * 4;
+        const int k = k0 + kr;
+        ra[u] = (m < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)k * lda + m) : float4{0, 0, 0, 0};
+      }
+      // B
+      if constexpr (B_NC) {         // k-rows, 32 float4 along n
+        const int kr = idx >> 5, n = n0 + (idx & 31) * 4;
+        const int k = k0 + kr;
+        rb[u] = (n < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)k * ldb + n) : float4{0, 0, 0, 0};
+      } else {                      // rows n, 8 float4 along k
+        const int r = idx >> 3, k = k0 + (idx & 7) * 4;
+        const int n = n0 + r;
+        rb[u] = (n < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)n * ldb + k) : float4{0, 0, 0, 0};
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int idx = tid + NTH * u;
+      if constexpr (A_KC) {
+        const int r = idx >> 3, kq = (idx & 7) * 4;
+        As[buf][kq + 0][r] = ra[u].x;
+        As[buf][kq + 1][r] = ra[u].y;
+        As[buf][kq + 2][r] = ra[u].z;
+        As[buf][kq + 3][r] = ra[u].w;
+      } else {
+        *reinterpret_cast<float4*>(&As[buf][idx >> 5][(idx & 31) * 4]) = ra[u];
+      }
+      if constexpr (B_NC) {
+        *reinterpret_cast<float4*>(&Bs[buf][idx >> 5][(idx & 31) * 4]) = rb[u];
+      } else {
+        const int r = idx >> 3, kq = (idx & 7) * 4;
+        Bs[buf][kq + 0][r] = rb[u].x;
+        Bs[buf][kq + 1][r] = rb[u].y;
+        Bs[buf][kq + 2][r] = rb[u].z;
+        Bs[buf][kq + 3][r] = rb[u].w;
+      }
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x16{};
+
+  load(0);
+  store(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    if (t + 1 < nk) load(t + 1);           // in flight during this tile's MFMAs
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      float a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[i] = As[buf][kk + hl][wm + 32 * i + l32];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = Bs[buf][kk + hl][wn + 32 * j + l32];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (t + 1 < nk) store(buf ^ 1);        // the other buffer: last read one barrier ago
+    __syncthreads();
+  }
+  // acc[i][j] element r -> row wm + 32 i + (r & 3) + 8 (r >> 2) + 4 hl, column wn + 32 j + l32
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = n0 + wn + 32 * j + l32;
+      if (col >= N) continue;
+      const float bv = bias != nullptr ? bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (row < M) {
+          float* cp = C + (int64_t)row * ldc + col;
+          const float v = alpha * acc[i][j][r] + bv;
+          *cp = accumulate ? *cp + v : v;
+        }
+      }
+    }
+}
+
+}  // namespace gf32
+
+// returns -1 if the operand layouts do not fit (inner stride != 1 / float4 alignment)
+extern "C" int mp_gemm_f32(const float* A, const float* B, float* C, const float* bias, int M, int N, int K,
+                           int64_t lda, int a_kc, int64_t ldb, int b_nc, int64_t ldc, float alpha, int accumulate,
+                           hipStream_t st) {
+  using namespace gf32;
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 4 || M % 4 || N % 4 || lda % 4 || ldb % 4) return -1;
+  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
+  const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+#define MP_F32(AK, BNC)                                                                                  \
+  gemm_f32_kernel<AK, BNC><<<grid, NTH, 0, st>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, accumulate)
+  if (a_kc && b_nc) MP_F32(true, true);
+  else if (a_kc) MP_F32(true, false);
+  else if (b_nc) MP_F32(false, true);
+  else MP_F32(false, false);
+#undef MP_F32
+  return (int)hipGetLastError();
+}

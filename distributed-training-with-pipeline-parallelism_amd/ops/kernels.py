@@ -1,6 +1,7 @@
 """Op wrappers: GPU -> HIP kernels in ``_C.so``; CPU -> PyTorch f32 reference math."""
 from __future__ import annotations
 
+import contextlib
 import importlib.util
 import math
 import os
@@ -451,6 +452,75 @@ def linear_dw(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, alpha: float 
         return dw
     dw += alpha * (dy.float().t() @ x.float())
     return dw
+
+
+# ======================================================================================
+# f32 linears on the f32-input MFMA (csrc/kernels/gemm_f32.hip) -- the reference-precision
+# path for autograd modules (the reference's own f32 model, helper:36-46)
+# ======================================================================================
+class _LinearF32(torch.autograd.Function):
+    """y = x W^T + b with the forward and both backward GEMMs on gemm_f32 (exact f32
+    products, f32 accumulate); any layout the kernel does not take falls back to ATen."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        out = torch.empty(x2.shape[0], w.shape[0], device=x.device, dtype=torch.float32)
+        if not _ext().gemm_f32(x2, w.t(), out, b, 1.0, False):
+            out = torch.addmm(b, x2, w.t()) if b is not None else torch.mm(x2, w.t())
+        ctx.save_for_backward(x2, w)
+        ctx.has_b = b is not None
+        ctx.in_shape = x.shape
+        return out.view(*x.shape[:-1], w.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, w = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1])
+        if g2.stride(1) != 1:
+            g2 = g2.contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty(g2.shape[0], w.shape[1], device=gy.device, dtype=torch.float32)
+            if not _ext().gemm_f32(g2, w, dx, None, 1.0, False):
+                dx = torch.mm(g2, w)
+            dx = dx.view(ctx.in_shape)
+        if ctx.needs_input_grad[1]:
+            dw = torch.empty_like(w)
+            if not _ext().gemm_f32(g2.t(), x2, dw, None, 1.0, False):
+                dw = torch.mm(g2.t(), x2)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = g2.sum(0)
+        return dx, dw, db
+
+
+def linear_f32(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """F.linear for f32 CUDA tensors on the f32 MFMA GEMM (autograd-aware)."""
+    return _LinearF32.apply(x, w, b)
+
+
+@contextlib.contextmanager
+def f32_linears():
+    """Within the block, ``torch.nn.functional.linear`` on f32 GPU tensors runs on
+    :func:`linear_f32`: every nn.Linear and every nn.MultiheadAttention projection
+    (torch's multi_head_attention_forward calls the module-level ``linear``) of an f32
+    module, forward and backward.  Other dtypes / CPU keep ATen."""
+    import torch.nn.functional as F
+    orig = F.linear
+    if not ext_available():
+        yield
+        return
+
+    def lin(input, weight, bias=None):
+        if (input.is_cuda and input.dtype == torch.float32 and weight.dtype == torch.float32 and
+                (bias is None or bias.dtype == torch.float32)):
+            return _LinearF32.apply(input, weight, bias)
+        return orig(input, weight, bias)
+    F.linear = lin
+    try:
+        yield
+    finally:
+        F.linear = orig
 
 
 # MIPIPE_WGRAD_GROUP=0: every weight-gradient GEMM of a job list in its own launch

@@ -571,3 +571,45 @@ def test_gemm_dropout_epilogues_match_act_kernels(cfg):
     da_ref = ops.act_bwd(dg, aux, "relu", dbias=cs_ref, p_drop=p, seed=99)
     close(da, da_ref, atol=2e-2, rtol=2e-2)
     close(cs, cs_ref, atol=0.5, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 2304, 768), (256, 128, 32), (1000, 776, 516), (132, 260, 100)])
+@pytest.mark.parametrize("a_t,b_t", [(False, False), (False, True), (True, False), (True, True)])
+def test_gemm_f32_mfma(M, N, K, a_t, b_t):
+    """gemm_f32 (v_mfma_f32_32x32x2_f32) vs an f64 reference, every operand layout
+    (K- or M-contiguous A, N- or K-contiguous B), tile edges, bias, accumulate."""
+    torch.manual_seed(0)
+    A = torch.randn(M, K, dtype=torch.float64)
+    B = torch.randn(K, N, dtype=torch.float64)
+    bias = torch.randn(N, dtype=torch.float64)
+    Ag = (A.t().contiguous().to(DEV).float().t() if a_t else A.to(DEV).float())
+    Bg = (B.t().contiguous().to(DEV).float().t() if b_t else B.to(DEV).float())
+    C = torch.full((M, N), 0.5, device=DEV)
+    assert _ext_call(Ag, Bg, C, bias.float().to(DEV), 0.75, True) == 1
+    ref = 0.5 + 0.75 * (A @ B) + bias
+    err = (C.double().cpu() - ref).abs().max().item()
+    scale = (A.abs() @ B.abs()).max().item()
+    assert err < 2e-6 * scale, (err, scale)
+
+
+def _ext_call(A, B, C, bias, alpha, acc):
+    return ops.load_ext().gemm_f32(A, B, C, bias, alpha, acc)
+
+
+def test_linear_f32_autograd_matches_aten():
+    torch.manual_seed(0)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    x = torch.randn(8, 128, 768, device=DEV, requires_grad=True)
+    w = torch.randn(2048, 768, device=DEV, requires_grad=True)
+    b = torch.randn(2048, device=DEV, requires_grad=True)
+    gy = torch.randn(8, 128, 2048, device=DEV)
+    y = ops.linear_f32(x, w, b)
+    y.backward(gy)
+    g1 = [t.grad.clone() for t in (x, w, b)]
+    for t in (x, w, b):
+        t.grad = None
+    y2 = torch.nn.functional.linear(x, w, b)
+    y2.backward(gy)
+    torch.testing.assert_close(y, y2, rtol=1e-5, atol=1e-4)
+    for a_, b_ in zip(g1, (x.grad, w.grad, b.grad)):
+        torch.testing.assert_close(a_, b_, rtol=1e-5, atol=2e-3)

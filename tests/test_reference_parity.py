@@ -150,3 +150,37 @@ def test_graphed_autograd_stage_matches_eager(dropout):
         assert not bad, bad
     else:
         assert not torch.equal(l1[0], l1[1])
+
+
+@pytest.mark.gpu
+def test_f32_kernel_stage_matches_aten():
+    """PipelineStage.f32_kernels: the reference's own f32 module with every linear and
+    attention projection on the f32 MFMA GEMM (graphs on) vs ATen f32 (TF32 off)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from mipipe.parallel.api import Schedule1F1B
+    dev = torch.device("cuda", 0)
+    torch.backends.cuda.matmul.allow_tf32 = False
+    a = ModelArgs(dim=256, n_layers=2, n_heads=4, vocab_size=512, dim_feedforward=512, dropout=0.0)
+    torch.manual_seed(0)
+    base = Transformer(a)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randint(0, 512, (16, 64), generator=g).to(dev)
+    y = torch.randint(0, 512, (16, 64), generator=g).to(dev)
+    res = {}
+    for f32k in (False, True):
+        model = Transformer(a)
+        model.load_state_dict(base.state_dict())
+        stage = manual_model_split(model, 0, 1, dev)
+        stage.graphs = True
+        stage.f32_kernels = f32k
+        sched = Schedule1F1B(stage, n_microbatches=4, loss_fn=tokenwise_loss_fn(512))
+        ls = []
+        sched.step(x, target=y, losses=ls)
+        res[f32k] = (torch.stack([l.detach() for l in ls]).cpu(),
+                     {n: p.grad.detach().cpu().clone() for n, p in stage.submod.named_parameters()})
+    (l0, g0), (l1, g1) = res[False], res[True]
+    torch.testing.assert_close(l1, l0, rtol=1e-5, atol=1e-5)
+    for n in g0:
+        scale = g0[n].abs().max().item()
+        assert (g1[n] - g0[n]).abs().max().item() <= 1e-4 * max(scale, 1e-3), n
