@@ -45,8 +45,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-graphs", action="store_true")
-    ap.add_argument("--aten-f32", action="store_true",
-                    help="fp32: keep ATen (hipBLASLt) for the linears instead of the f32 MFMA GEMM (gemm_f32.hip)")
+    ap.add_argument("--f32-kernels", action="store_true",
+                    help="fp32: the linears / attention projections on this framework's f32 MFMA GEMM (gemm_f32.hip) "
+                         "instead of ATen (hipBLASLt); 2.3x slower today (profiles/r2_probes.md)")
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
                     help="bf16: the native HIP path (PipelineTrainer, AdamW included); fp32: the reference's own "
                          "nn.Module model in f32 on the GPU through the reference-compatible schedule API "
@@ -125,7 +126,7 @@ def main_fp32(a):
             args = ModelArgs(n_layers=L, n_heads=H)
             stage = manual_model_split(Transformer(args), 0, 1, dev)
             stage.graphs = not a.no_graphs   # one HIP graph per direction and microbatch slot
-            stage.f32_kernels = not a.aten_f32   # linears / attention projections on the f32 MFMA GEMM
+            stage.f32_kernels = a.f32_kernels   # linears / attention projections on the f32 MFMA GEMM
             sched = Schedule1F1B(stage, n_microbatches=m, loss_fn=tokenwise_loss_fn(args.vocab_size))
             x = torch.randint(0, args.vocab_size, (B, S), device=dev)
             y = torch.randint(0, args.vocab_size, (B, S), device=dev)
@@ -145,8 +146,8 @@ def main_fp32(a):
                          "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, **f32** (the reference's precision; ATen "
                          "compute, TF32 off), fwd+bwd only (no optimizer), reference-compatible API, "
                          + ("eager" if a.no_graphs else "HIP graphs per microbatch slot (PipelineStage(graphs=True))")
-                         + (", linears on ATen f32" if a.aten_f32 else
-                            ", every linear / attention projection on the f32 MFMA GEMM (gemm_f32.hip)"),
+                         + (", every linear / attention projection on the f32 MFMA GEMM (gemm_f32.hip)"
+                            if a.f32_kernels else ", linears on ATen f32"),
                "rows": out}
     if a.json:
         with open(a.json, "w") as f:
