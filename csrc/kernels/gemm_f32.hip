@@ -13,7 +13,7 @@
 // operands are staged k-major in LDS ([k][m], [k][n], padded rows), so a 32x32x2 fragment
 // read (lane l: row/col base + l % 32, k = kk + l / 32) is one conflict-free ds_read_b32
 // per operand.  Global -> register prefetch of K-tile t+1 overlaps the MFMAs of tile t;
-// two LDS buffers, one barrier per K-tile.
+// two LDS buffers, one barrier per K-tile.  Grids of few tiles split K (f32 atomics into C).
 #include "mp_common.h"
 
 using namespace mp;
@@ -34,12 +34,17 @@ __global__ void __launch_bounds__(NTH, 2) gemm_f32_kernel(const float* __restric
   const int wave = tid >> 6, wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const int gn = (N + BN - 1) / BN;
   const int m0 = (blockIdx.x / gn) * BM, n0 = (blockIdx.x % gn) * BN;
-  const int nk = (K + BK - 1) / BK;
+  // split-K (blockIdx.y of gridDim.y): K-tiles [kt0, kt0 + nk); partial sums are added to C
+  // with f32 atomics (C zeroed by the host unless accumulating), the bias by split 0
+  const int ktiles = (K + BK - 1) / BK;
+  const int nsplit = gridDim.y;
+  const int kt0 = (int)blockIdx.y * ktiles / nsplit;
+  const int nk = ((int)blockIdx.y + 1) * ktiles / nsplit - kt0;
 
   // 1024 float4 per operand tile, 4 per thread
   float4 ra[4], rb[4];
   auto load = [&](int kt) {
-    const int k0 = kt * BK;
+    const int k0 = (kt0 + kt) * BK;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int idx = tid + NTH * u;
@@ -123,14 +128,15 @@ __global__ void __launch_bounds__(NTH, 2) gemm_f32_kernel(const float* __restric
     for (int j = 0; j < 2; ++j) {
       const int col = n0 + wn + 32 * j + l32;
       if (col >= N) continue;
-      const float bv = bias != nullptr ? bias[col] : 0.f;
+      const float bv = (bias != nullptr && blockIdx.y == 0) ? bias[col] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
         if (row < M) {
           float* cp = C + (int64_t)row * ldc + col;
           const float v = alpha * acc[i][j][r] + bv;
-          *cp = accumulate ? *cp + v : v;
+          if (nsplit > 1) atomicAdd(cp, v);
+          else *cp = accumulate ? *cp + v : v;
         }
       }
     }
@@ -147,8 +153,16 @@ extern "C" int mp_gemm_f32(const float* A, const float* B, float* C, const float
   if (K % 4 || M % 4 || N % 4 || lda % 4 || ldb % 4) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
   const int grid = ((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  // few output tiles: split K so that ~256 workgroups (two per CU) run, >= 2 K-tiles each
+  const int ktiles = (K + BK - 1) / BK;
+  int split = 1;
+  while (split < 8 && grid * split * 2 <= 256 && ktiles / (split * 2) >= 2) split *= 2;
+  if (split > 1 && !accumulate) {
+    const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, st);
+    if (e != hipSuccess) return (int)e;
+  }
 #define MP_F32(AK, BNC)                                                                                  \
-  gemm_f32_kernel<AK, BNC><<<grid, NTH, 0, st>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, accumulate)
+  gemm_f32_kernel<AK, BNC><<<dim3(grid, split), NTH, 0, st>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, accumulate)
   if (a_kc && b_nc) MP_F32(true, true);
   else if (a_kc) MP_F32(true, false);
   else if (b_nc) MP_F32(false, true);
