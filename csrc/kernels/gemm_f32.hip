@@ -159,10 +159,10 @@ extern "C" int mp_gemm_f32(const float* A, const float* B, float* C, const float
   if (M <= 0 || N <= 0) return 0;
   if (K % 4 || M % 4 || N % 4 || lda % 4 || ldb % 4) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
-  // 128x128 tiles when they fill the chip twice over; else 64x64 tiles; split-K (f32
+  // 128x128 tiles when they fill the chip four times over; else 64x64 tiles; split-K (f32
   // atomics) while the grid is under 1.5 workgroups per CU and each split keeps >= 4 K-tiles
   const int g128 = ((M + 127) / 128) * ((N + 127) / 128);
-  const bool big = g128 >= 512;
+  const bool big = g128 >= 1024;
   const int T = big ? 128 : 64;
   const int grid = ((M + T - 1) / T) * ((N + T - 1) / T);
   const int ktiles = (K + BK - 1) / BK;
