@@ -18,12 +18,17 @@ from C++; p2p on the native RCCL engine (one communicator + stream per direction
 csrc/comm/rccl_p2p.h), pre-flight pinged at init with an in-process fallback to torch p2p.
 The JSON reports which path ran (``hip_graphs``, ``native_runner``, ``p2p``).
 
-Hang safety (N>1): every rank runs the benchmark in a child process under a supervisor.
-The child arms a watchdog over init, warmup, every timed step and the bubble step (on a
-stall it prints the program grid + all stacks and exits non-zero); the process-group
-timeout is 300 s.  If an attempt fails on any rank, all supervisors retry in a more
-conservative mode (torch p2p, then no HIP graphs) on a fresh rendezvous port; the
-``attempt`` field says which one produced the number.  Supervisors never touch the GPU.
+Hang safety (N>1): the pipeline program is PROVEN hang-free before it runs
+(PipelineRuntime._prove: every collective after the step's p2p, serial queue model), and
+every rank runs the benchmark in a child process under a supervisor.  The child arms a
+watchdog over init, warmup, every timed step and the bubble step (on a stall it prints the
+program grid + all stacks and exits non-zero); the process-group timeout is 300 s.  If an
+attempt fails on any rank, all supervisors retry in a more conservative mode (torch p2p,
+then no HIP graphs) on a fresh rendezvous port; the ``attempt`` field says which one
+produced the number.  One global deadline (MIPIPE_BENCH_DEADLINE_S, default 540 s, under
+the driver's 600 s) bounds all attempts together: each gets at most what is left of it
+(and at most MIPIPE_BENCH_ATTEMPT_S, default 240 s), its watchdogs are clamped to that,
+and no attempt starts with less than 30 s left.  Supervisors never touch the GPU.
 
 The measured bubble comes from one extra profiled step replayed from the same native tape
 (timing events around every graph on the compute stream): ``1 - sum(busy_r) / (P * step)``
@@ -103,17 +108,32 @@ def _wait_file(path: str, timeout_s: float):
     return None
 
 
+DEADLINE_S = 540.0       # all attempts together (the driver kills the bench at 600 s)
+ATTEMPT_CAP_S = 240.0    # one attempt at most
+MIN_ATTEMPT_S = 30.0     # no attempt starts with less than this left
+
+
+def attempt_budget(elapsed: float, deadline: float = DEADLINE_S, cap: float = ATTEMPT_CAP_S) -> float:
+    """Seconds the next attempt may run (0: none may start) -- what is left of the global
+    deadline, less a 5 s margin for killing a child, capped per attempt."""
+    left = deadline - elapsed - 5.0
+    return 0.0 if left < MIN_ATTEMPT_S else min(cap, left)
+
+
 def supervise(a, argv) -> int:
     """Run the benchmark in a child process per attempt (module docstring).  Rank 0 decides
-    after each attempt (did its child print the JSON line?) and publishes the verdict in a
-    per-launch directory; the other ranks follow it.  Never initialises the GPU."""
+    after each attempt (did its child print the JSON line?  is there time for another?)
+    and publishes the verdict (done | retry | giveup) in a per-launch directory; the other
+    ranks follow it.  Never initialises the GPU."""
+    t_start = time.monotonic()
     rank = int(os.environ.get("RANK", "0"))
     base_port = int(os.environ.get("MASTER_PORT", "29500"))
     d = _attempt_dir()
     attempts = ATTEMPTS[: max(1, a.max_attempts)]
     if a.graphs is not None or os.environ.get("MIPIPE_P2P"):
         attempts = [(os.environ.get("MIPIPE_P2P", "auto"), 1 if a.graphs is None else a.graphs)] + attempts[1:]
-    per_attempt_s = float(os.environ.get("MIPIPE_BENCH_ATTEMPT_S", "280"))
+    deadline = float(os.environ.get("MIPIPE_BENCH_DEADLINE_S", str(DEADLINE_S)))
+    cap = float(os.environ.get("MIPIPE_BENCH_ATTEMPT_S", str(ATTEMPT_CAP_S)))
     current = {"proc": None}
 
     def on_term(signum, frame):   # the launcher tears the job down: take the child with us
@@ -125,8 +145,11 @@ def supervise(a, argv) -> int:
     signal.signal(signal.SIGTERM, on_term)
     signal.signal(signal.SIGINT, on_term)
     for k, (p2p, graphs) in enumerate(attempts):
+        per_attempt_s = attempt_budget(time.monotonic() - t_start, deadline, cap)
+        if per_attempt_s <= 0:      # (rank 0 published "giveup" for the previous attempt)
+            break
         env = dict(os.environ, MIPIPE_BENCH_CHILD="1", MIPIPE_P2P=p2p, MIPIPE_BENCH_ATTEMPT=str(k),
-                   MASTER_PORT=str(base_port + 1 + k))
+                   MASTER_PORT=str(base_port + 1 + k), MIPIPE_BENCH_ATTEMPT_S=f"{per_attempt_s:.0f}")
         env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # fresh rendezvous store per attempt
         cmd = [sys.executable, os.path.abspath(__file__)] + list(argv) + ["--graphs", str(graphs)]
         printed = False
@@ -163,17 +186,21 @@ def supervise(a, argv) -> int:
         rc = proc.wait()
         if rank == 0:
             th.join(timeout=10)
-            verdict = "done" if printed else "retry"
+            more = k + 1 < len(attempts) and attempt_budget(time.monotonic() - t_start, deadline, cap) > 0
+            verdict = "done" if printed else ("retry" if more else "giveup")
             with open(os.path.join(d, f"attempt{k}.verdict.tmp"), "w") as f:
                 f.write(verdict)
             os.replace(os.path.join(d, f"attempt{k}.verdict.tmp"), os.path.join(d, f"attempt{k}.verdict"))
         else:
-            verdict = _wait_file(os.path.join(d, f"attempt{k}.verdict"), per_attempt_s)
+            verdict = _wait_file(os.path.join(d, f"attempt{k}.verdict"), 30.0)
         if verdict == "done":
             return 0
         sys.stderr.write(f"[bench supervisor] rank {rank}: attempt {k} (p2p={p2p}, graphs={graphs}) failed "
-                         f"(rc={rc}); {'retrying' if k + 1 < len(attempts) else 'giving up'}\n")
+                         f"(rc={rc}); {'retrying' if verdict == 'retry' else 'giving up'} "
+                         f"({time.monotonic() - t_start:.0f}s of the {deadline:.0f}s deadline used)\n")
         sys.stderr.flush()
+        if verdict != "retry":
+            break
     return 1
 
 
@@ -202,6 +229,10 @@ def run(a) -> None:
     attempt = int(os.environ.get("MIPIPE_BENCH_ATTEMPT", "0"))
     step_to = a.step_timeout if a.step_timeout is not None else 60.0
     init_to = max(180.0, 3 * step_to)
+    budget = float(os.environ.get("MIPIPE_BENCH_ATTEMPT_S", "0") or 0)
+    if budget > 0:      # under the supervisor: every watchdog inside this attempt's budget
+        init_to = min(init_to, max(10.0, budget - 10.0))
+        step_to = min(step_to, init_to)
     describe = {"fn": lambda: "(initialising: no program yet)"}
     wd = Watchdog(init_to, describe=lambda: describe["fn"]())
     with wd.step(init_to):
@@ -329,6 +360,9 @@ def run(a) -> None:
                    "p2p": rt.p2p.kind,
                    "p2p_channels": rt.p2p.channels if rt.p2p.kind == "native" else None,
                    "p2p_fallback": rt.p2p.fallback_reason or None,
+                   "collectives": trainer.coll.kind,
+                   "collective_placement": rt.coll_placement,
+                   "head_zero": bool(getattr(trainer, "head_zero", False)) and trainer.head is not None,
                    "recompute": trainer.recompute,
                    "recv_arena_mb": round(rt.recv_arena_bytes / 2 ** 20, 1),
                    "plain_gemms": _plain_summary(),

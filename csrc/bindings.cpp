@@ -58,6 +58,9 @@ int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, 
 int mp_gemm_tt_grouped(int n, const void* const* A, const void* const* B, float* const* C, const int* M, const int* N,
                        const int* K, const int64_t* lda, const int64_t* ldb, const int64_t* ldc, float alpha,
                        hipStream_t st);
+int mp_probe_spin(unsigned* flag, unsigned expect, int64_t timeout_us, unsigned* result, hipStream_t waiter);
+int mp_probe_set(unsigned* flag, unsigned value, hipStream_t setter);
+int mp_probe_clock_khz();
 int mp_gemm(const void* A, const void* B, void* C, const void* bias, const void* residual, void* aux, int M, int N,
             int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ld_res, int64_t ld_aux, int transA, int transB,
             int epilogue, int c_f32_accum, float alpha, hipStream_t st);
@@ -422,6 +425,25 @@ void set_dropout_step(int64_t step) {
   check(mp_set_drop_step_gemm(v, cur_stream()), "set_drop_step");
 }
 
+// hardware-queue probe (csrc/kernels/probe.hip, parallel/queues.py): enqueue the bounded
+// spinner on stream `waiter` / the flag store on stream `setter` (raw HIP stream handles;
+// 0 = the current stream).  flag: int32 [1], result: int32 [2] device tensors.
+void probe_spin(torch::Tensor flag, int64_t expect, int64_t timeout_us, torch::Tensor result, int64_t waiter) {
+  req(flag, torch::kInt32, "flag");
+  req(result, torch::kInt32, "result");
+  TORCH_CHECK(result.numel() >= 2 && timeout_us > 0 && timeout_us <= 2000000, "probe_spin: result[2], timeout <= 2 s");
+  hipStream_t s = waiter ? reinterpret_cast<hipStream_t>(waiter) : cur_stream();
+  check(mp_probe_spin(reinterpret_cast<unsigned*>(flag.data_ptr()), (unsigned)expect, timeout_us,
+                      reinterpret_cast<unsigned*>(result.data_ptr()), s),
+        "probe_spin");
+}
+
+void probe_set(torch::Tensor flag, int64_t value, int64_t setter) {
+  req(flag, torch::kInt32, "flag");
+  hipStream_t s = setter ? reinterpret_cast<hipStream_t>(setter) : cur_stream();
+  check(mp_probe_set(reinterpret_cast<unsigned*>(flag.data_ptr()), (unsigned)value, s), "probe_set");
+}
+
 }  // namespace
 
 namespace mipipe_comm {
@@ -491,4 +513,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_dropout_step", &set_dropout_step);
   m.def("create_stream", &create_stream, pybind11::arg("device"), pybind11::arg("priority") = 0);
   m.def("transpose_batched", &transpose_batched);
+  m.def("probe_spin", &probe_spin, pybind11::arg("flag"), pybind11::arg("expect"), pybind11::arg("timeout_us"),
+        pybind11::arg("result"), pybind11::arg("waiter") = 0);
+  m.def("probe_set", &probe_set, pybind11::arg("flag"), pybind11::arg("value"), pybind11::arg("setter") = 0);
+  m.def("probe_clock_khz", []() { return mp_probe_clock_khz(); });
 }

@@ -11,10 +11,15 @@
 //   POST   e, c, ops one grouped ncclSend/ncclRecv on channel c (0: activations down the
 //                    pipeline, 1: gradients up) of the RCCL engine -- that direction's own
 //                    communicator and stream, ordered after the compute stream
-//                    (RcclP2P::post_raw); fills a slot
+//                    (RcclEngine::post_raw); fills a slot
+//   COLL   e, c, op  one collective (all-reduce / reduce-scatter / all-gather) on channel c
+//                    of an engine (the pipeline's or the DP group's): the gradient
+//                    reductions of REDUCE_GRAD and of the distributed head, ordered after
+//                    the compute stream on the collective stream slot; fills a slot
 //   WAIT   slot      the compute stream waits for that group's completion event
-//   CALL   fn        a Python callable (anything not expressible above: gloo transfers,
-//                    DP all-reduce through torch.distributed) -- the GIL is taken only here
+//   CALL   fn        a Python callable (anything not expressible above: gloo transfers and
+//                    collectives on CPU) -- the GIL is taken only here; a GPU tape with the
+//                    native engines holds none
 //   SYNC   w, s      stream w waits for everything issued so far on stream s (an event)
 //
 // GRAPH and COPY carry the stream they were issued on (0 = the compute stream): with
@@ -40,13 +45,13 @@
 #include <utility>
 #include <vector>
 
-#include "../comm/rccl_p2p.h"
+#include "../comm/rccl_engine.h"
 
 namespace py = pybind11;
 
 namespace mipipe_runtime {
 
-using mipipe_comm::RcclP2P;
+using mipipe_comm::RcclEngine;
 
 #define MP_HIPCHK(x)                                                                         \
   do {                                                                                       \
@@ -56,7 +61,7 @@ using mipipe_comm::RcclP2P;
 
 class StageRunner {
  public:
-  enum Kind { GRAPH = 0, COPY = 1, POST = 2, WAIT = 3, CALL = 4, SYNC = 5 };
+  enum Kind { GRAPH = 0, COPY = 1, POST = 2, WAIT = 3, CALL = 4, SYNC = 5, COLL = 6 };
 
   explicit StageRunner(int device) : device_(device) {}
 
@@ -97,11 +102,29 @@ class StageRunner {
                    const std::vector<std::tuple<int64_t, int64_t, int64_t, int64_t>>& recvs) {
     Instr i;
     i.kind = POST;
-    i.engine = engine.cast<RcclP2P*>();
+    i.engine = engine.cast<RcclEngine*>();
     i.keep = engine;
     i.channel = channel;
     for (const auto& [p, n, t, peer] : sends) i.sends.push_back({reinterpret_cast<void*>(p), (size_t)n, nccl(t), (int)peer});
     for (const auto& [p, n, t, peer] : recvs) i.recvs.push_back({reinterpret_cast<void*>(p), (size_t)n, nccl(t), (int)peer});
+    i.slot = nslots_++;
+    tape_.push_back(std::move(i));
+    return tape_.back().slot;
+  }
+
+  // one collective: op (CollOp), send / recv device pointers, count (elements per the
+  // RCCL call's convention), dtype code as in add_post.  Returns the slot a WAIT names.
+  int64_t add_coll(py::object engine, int channel, int op, int64_t send, int64_t recv, int64_t count, int64_t dtype) {
+    Instr i;
+    i.kind = COLL;
+    i.engine = engine.cast<RcclEngine*>();
+    i.keep = engine;
+    i.channel = channel;
+    i.a = send;
+    i.b = recv;
+    i.c = count;
+    i.op = op;
+    i.dtype = nccl(dtype);
     i.slot = nslots_++;
     tape_.push_back(std::move(i));
     return tape_.back().slot;
@@ -128,7 +151,7 @@ class StageRunner {
   void run() {
     hipStream_t st = c10::hip::getCurrentHIPStream(device_).stream();
     std::vector<int64_t> handles(nslots_, -1);
-    std::vector<RcclP2P*> engines(nslots_, nullptr);
+    std::vector<RcclEngine*> engines(nslots_, nullptr);
     const bool prof = profile_;
     if (prof) prepare_events();
     while ((int64_t)sync_ev_.size() < nsync_) {
@@ -160,6 +183,11 @@ class StageRunner {
           break;
         case POST:
           handles[i.slot] = i.engine->post_raw(i.channel, i.sends, i.recvs, st);
+          engines[i.slot] = i.engine;
+          break;
+        case COLL:
+          handles[i.slot] = i.engine->coll_raw(i.channel, i.op, reinterpret_cast<void*>(i.a),
+                                               reinterpret_cast<void*>(i.b), (size_t)i.c, i.dtype, st);
           engines[i.slot] = i.engine;
           break;
         case WAIT:
@@ -217,6 +245,13 @@ class StageRunner {
       if (i.kind == POST) k.push_back(i.channel);
     return k;
   }
+  // (channel, op) of every COLL, in tape order
+  std::vector<std::pair<int64_t, int64_t>> collectives() const {
+    std::vector<std::pair<int64_t, int64_t>> k;
+    for (const auto& i : tape_)
+      if (i.kind == COLL) k.emplace_back(i.channel, i.op);
+    return k;
+  }
 
  private:
   void prepare_events() {
@@ -236,10 +271,12 @@ class StageRunner {
     int64_t slot = -1;
     int64_t stream = 0;  // GRAPH / COPY: issuing stream (0 = compute stream)
     int channel = 0;
+    int op = 0;
+    ncclDataType_t dtype = ncclFloat32;
     std::string label;
-    RcclP2P* engine = nullptr;
+    RcclEngine* engine = nullptr;
     py::object keep;  // keeps the engine alive
-    std::vector<RcclP2P::RawOp> sends, recvs;
+    std::vector<RcclEngine::RawOp> sends, recvs;
     py::function fn;
   };
 
@@ -277,6 +314,7 @@ void register_runner(py::module& m) {
            py::arg("stream") = 0)
       .def("add_sync", &StageRunner::add_sync, py::arg("waiter"), py::arg("signal"))
       .def("add_post", &StageRunner::add_post)
+      .def("add_coll", &StageRunner::add_coll)
       .def("add_wait", &StageRunner::add_wait)
       .def("add_call", &StageRunner::add_call)
       .def("run", &StageRunner::run)
@@ -284,6 +322,7 @@ void register_runner(py::module& m) {
       .def("timeline", &StageRunner::timeline)
       .def("kinds", &StageRunner::kinds)
       .def("channels", &StageRunner::channels)
+      .def("collectives", &StageRunner::collectives)
       .def_property_readonly("size", &StageRunner::size)
       .def_property_readonly("runs", &StageRunner::runs);
 }

@@ -6,8 +6,11 @@
 
 One process per GPU (``torchrun``), RCCL over xGMI between pipeline ranks and between
 DP replicas.  A training step = the lowered pipeline program (fwd/bwd of all
-microbatches, p2p, per-stage DP all-reduce at REDUCE_GRAD) + tied-embedding sync +
-global grad-norm clip + one fused AdamW launch per stage arena.
+microbatches, p2p, per-stage DP all-reduce at REDUCE_GRAD, the distributed head's
+gradient reduce-scatter at REDUCE_HEAD -- all on the native RCCL engines,
+parallel/collectives.py) + tied-embedding sync + global grad-norm clip + one fused AdamW
+launch per stage arena (the head: on this rank's shard only, then an all-gather of the
+bf16 weights -- ZeRO-1 for the replicated head).
 """
 from __future__ import annotations
 
@@ -22,6 +25,7 @@ from . import ops
 from .models.config import NativeConfig
 from .models.native import HeadShard, NativeModel, ParamArena, balanced_layer_ranges, stage_cost_model
 from .models.stage import NativeStage
+from .parallel.collectives import Collectives
 from .parallel.comm import P2P
 from .parallel.headsplit import HeadPlan, head_token_split, plan_head_schedule
 from .parallel.mesh import Mesh, build_mesh
@@ -38,8 +42,11 @@ class FlatAdamW:
 
     def __init__(self, arenas: List[ParamArena], lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, max_grad_norm: float = 1.0, pp_group=None, norm_skip=(),
-                 norm_exclude=None, grad_scale: float = 1.0):
+                 norm_exclude=None, grad_scale: float = 1.0, coll=None):
         self.arenas = arenas
+        # parallel/collectives.py: the clip-norm sum over the pipeline group and the
+        # all-gather of ZeRO-sharded arenas' updated bf16 weights
+        self.coll = coll
         # arenas replicated across the pipeline group (distributed head) count in the
         # global grad norm on one rank only
         self.norm_skip = set(norm_skip)
@@ -67,6 +74,9 @@ class FlatAdamW:
             for i, a in enumerate(self.arenas):
                 if i in self.norm_skip:
                     continue
+                if a.shard is not None:     # this rank's (reduced) range of a sharded arena
+                    ops.sumsq(a.opt_views()[1], self.sumsq)
+                    continue
                 lo = 0
                 for off, n in self.norm_exclude.get(i, ()):
                     if off > lo:
@@ -74,12 +84,20 @@ class FlatAdamW:
                     lo = max(lo, off + n)
                 if lo < a.grad.numel():
                     ops.sumsq(a.grad[lo:] if lo else a.grad, self.sumsq)
-            if self.pp_group is not None and dist.get_world_size(self.pp_group) > 1:
+            if self.coll is not None:
+                self.coll.all_reduce(self.sumsq, "pp").wait()
+            elif self.pp_group is not None and dist.get_world_size(self.pp_group) > 1:
                 dist.all_reduce(self.sumsq, group=self.pp_group)
         for a, m, v in zip(self.arenas, self.m, self.v):
-            ops.adamw_(a.master, a.grad, m, v, a.w16, a.n_decay, lr, self.betas[0], self.betas[1], self.eps, self.wd,
+            master, g, w16, n_decay = a.opt_views()
+            ops.adamw_(master, g, m, v, w16, n_decay, lr, self.betas[0], self.betas[1], self.eps, self.wd,
                        self.step_count, self.sumsq if use_clip else None, self.max_norm if use_clip else 0.0,
                        self.grad_scale, zero_grad=True)
+            if a.shard is not None:
+                lo, hi, _ = a.shard
+                a.grad[:lo].zero_()
+                a.grad[hi:].zero_()
+                self.coll.all_gather(a.w16, "pp").wait()
             a.refresh_transposes()
 
     def state_dict(self):
@@ -172,8 +190,11 @@ class PipelineTrainer:
         self.head: Optional[HeadShard] = None
         orders = head_plan = head_costs = stage_costs = None
         self.head_chunks = None
+        # ZeRO-1 for the replicated head: master / Adam moments sharded over the pipeline
+        # group (MIPIPE_HEAD_ZERO=0: fully replicated, gradient all-reduced)
+        self.head_zero = self.split_head and os.environ.get("MIPIPE_HEAD_ZERO", "1") != "0"
         if self.split_head:
-            self.head = HeadShard(cfg, self.device, seed=seed, dtype=dtype)
+            self.head = HeadShard(cfg, self.device, seed=seed, dtype=dtype, shards=pp if self.head_zero else 1)
             lc, head_units, ec = stage_cost_model(cfg, seq_len)
             stage_costs = [(r1 - r0) * lc + (ec if s == 0 else 0.0) + (0.1 if s == num_stages - 1 else 0.0)
                            for s, (r0, r1) in enumerate(layer_ranges)]
@@ -213,9 +234,14 @@ class PipelineTrainer:
             self.stages.append(NativeStage(model, mbs, seq_len, dp_group=self.mesh.dp_group, embed_group=egroup,
                                            seed=seed + 1000 * self.mesh.dp_rank, graphs=graphs))
         p2p = P2P(self.mesh.pp_group, self.mesh.pipe_ranks, self.device, ctrl_group=self.mesh.ctrl_group)
+        # every collective of the step (DP all-reduce, head reduction, clip norm, losses)
+        self.coll = Collectives(self.mesh, self.device, pipe_engine=p2p.engine)
+        for st in self.stages:
+            st.coll = self.coll
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
                                        scale_grads=True, style=style, profile=profile, orders=orders,
-                                       head=head_plan, head_costs=head_costs, stage_costs=stage_costs)
+                                       head=head_plan, head_costs=head_costs, stage_costs=stage_costs,
+                                       dp=self.mesh.dp, head_reduce_after_stage0=bool(cfg.tie_embeddings))
         # microbatch lanes (PipelineRuntime.set_lanes): MIPIPE_LANES=auto|1 (off)|n
         self.lanes = self.runtime.set_lanes(self._auto_lanes(pp, v, graphs, n_microbatches, mbs, seq_len)
                                             if os.environ.get("MIPIPE_LANES", "auto") == "auto"
@@ -231,19 +257,46 @@ class PipelineTrainer:
             g = a.g("tok_embeddings.weight")
             norm_exclude[i] = [(g.storage_offset() - a.grad.storage_offset(), g.numel())]
         if self.head is not None:
-            arenas.append(self.head.arena)
-            if self.mesh.pp_rank != 0:
-                norm_skip.append(len(arenas) - 1)
-            if dist.is_initialized() and dist.get_world_size() > 1:
-                # replicated head: gradient all-reduce (SUM) over every rank (pipeline x DP),
-                # issued asynchronously right after this rank's last head-arena write
-                hgrad = self.head.arena.grad
-                self.runtime.head_reduce = lambda: dist.all_reduce(hgrad, async_op=True)
-                self.runtime.head_reduce_after_stage0 = bool(cfg.tie_embeddings)
+            ha = self.head.arena
+            if self.head_zero and pp > 1:
+                # this pipeline rank owns block pp_rank of the head arena: its f32 master and
+                # Adam moments; the gradient is reduce-scattered into that block
+                n = ha.numel // pp
+                lo = self.mesh.pp_rank * n
+
+                def gather(shard, numel=ha.numel, lo=lo, n=n):
+                    full = torch.empty(numel, dtype=shard.dtype, device=shard.device)
+                    full[lo:lo + n].copy_(shard)
+                    self.coll.all_gather(full, "pp").wait()
+                    return full
+                ha.shard_master(lo, lo + n, gather)
+            elif self.mesh.pp_rank != 0:
+                norm_skip.append(len(arenas))
+            arenas.append(ha)
+            if self.mesh.world > 1:
+                self.runtime.head_reduce = self._head_reduce
         self.optimizer = FlatAdamW(arenas, lr=lr, eps=adam_eps, weight_decay=weight_decay, max_grad_norm=max_grad_norm,
                                    pp_group=self.mesh.pp_group if pp > 1 else None, norm_skip=norm_skip,
-                                   norm_exclude=norm_exclude, grad_scale=1.0 / self.mesh.dp)
+                                   norm_exclude=norm_exclude, grad_scale=1.0 / self.mesh.dp, coll=self.coll)
         self.last_losses: List[torch.Tensor] = []
+
+    def _head_reduce(self) -> list:
+        """REDUCE_HEAD: sum the replicated head's gradient over the pipeline x DP ranks --
+        ZeRO-1: reduce-scatter over the pipeline group (this rank's block is summed), then
+        all-reduce of that block over DP; replicated: all-reduce of the whole gradient over
+        the pipeline group, then over DP.  On the native engines both run on the one
+        collective stream (FIFO: the DP step follows the pipeline step without a stream
+        wait); through torch.distributed the second waits for the first."""
+        g = self.head.arena.grad
+        if self.head_zero and self.mesh.pp > 1:
+            w1, part = self.coll.reduce_scatter(g, "pp")
+        else:
+            w1, part = self.coll.all_reduce(g, "pp"), g
+        if self.mesh.dp == 1:
+            return [w1]
+        if not (self.coll.pp_kind == "native" and self.coll.dp_kind == "native"):
+            w1.wait()
+        return [w1, self.coll.all_reduce(part, "dp")]
 
     def _auto_lanes(self, pp: int, v: int, graphs: bool, m: int, mbs: int, seq_len: int) -> int:
         """Lanes at PP = 1 with HIP graphs: up to 4 for <= 4096-token microbatches, 2 above,
@@ -296,8 +349,7 @@ class PipelineTrainer:
             # (the head gradient all-reduce was issued and waited on inside the step)
             parts = torch.stack([self.runtime.head_losses.get(i, torch.zeros((), device=self.device))
                                  for i in range(self.m)]).float()
-            if self.mesh.pp_group is not None and dist.get_world_size(self.mesh.pp_group) > 1:
-                dist.all_reduce(parts, group=self.mesh.pp_group)
+            self.coll.all_reduce(parts, "pp").wait()
             losses = list(parts / (self.mbs * self.S))
         self.optimizer.step(lr)
         self.last_losses = losses

@@ -55,7 +55,7 @@ class ParamArena:
     flat buffer (one AdamW launch for the whole stage)."""
 
     def __init__(self, specs: Sequence[ParamSpec], device, dtype=torch.bfloat16, seed: int = 0,
-                 init: bool = True):
+                 init: bool = True, numel_multiple: int = 8):
         specs = sorted(specs, key=lambda s: (not s.decay,))
         self.specs = {s.name: s for s in specs}
         self.order = [s.name for s in specs]
@@ -67,7 +67,11 @@ class ParamArena:
             off = (off + 7) // 8 * 8
             self.offsets[s.name] = off
             off += n
-        self.numel = (off + 7) // 8 * 8
+        mult = max(8, int(numel_multiple))
+        self.numel = (off + mult - 1) // mult * mult
+        # ZeRO-1 (shard_master): this rank keeps only master[lo:hi] (and the optimizer
+        # moments of that range); ``unsharded()`` gathers the full master when needed
+        self.shard: Optional[Tuple[int, int, Callable]] = None
         self.n_decay = 0
         for s in specs:
             if s.decay:
@@ -107,6 +111,8 @@ class ParamArena:
         self.sync_w16()
 
     def sync_w16(self) -> None:
+        if self.shard is not None:
+            raise RuntimeError("sync_w16 on a sharded arena: use `with arena.unsharded(): arena.sync_w16()`")
         ops.cast_f32_bf16(self.master, self.w16)
         self.refresh_transposes()
 
@@ -159,20 +165,58 @@ class ParamArena:
         return name in self.specs
 
     def state_dict(self) -> Dict[str, torch.Tensor]:
-        return {n: self.master_view(n).detach().clone() for n in self.order}
+        with self.unsharded():
+            return {n: self.master_view(n).detach().clone() for n in self.order}
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor], strict: bool = True) -> None:
         missing = [n for n in self.order if n not in sd]
         if strict and missing:
             raise KeyError(f"missing keys: {missing[:5]}...")
-        for n in self.order:
-            if n in sd:
-                self.master_view(n).copy_(sd[n].to(self.device, torch.float32).reshape(self.specs[n].shape))
-        self.sync_w16()
+        with self.unsharded():
+            for n in self.order:
+                if n in sd:
+                    self.master_view(n).copy_(sd[n].to(self.device, torch.float32).reshape(self.specs[n].shape))
+            self.sync_w16()
 
     def zero_grad(self) -> None:
         for g in self.grad_lanes:
             g.zero_()
+
+    # ------------------------------------------------------------------ ZeRO-1
+    def shard_master(self, lo: int, hi: int, gather: Callable[[torch.Tensor], torch.Tensor]) -> None:
+        """Keep only ``master[lo:hi]`` on this rank (``gather(shard) -> full`` rebuilds the
+        whole f32 master: a collective).  bf16 weights and f32 gradients stay full-size
+        (every rank computes with the whole matrix and accumulates its whole gradient)."""
+        if self.shard is not None:
+            raise RuntimeError("arena already sharded")
+        self.master = self.master[lo:hi].clone()
+        self.shard = (int(lo), int(hi), gather)
+
+    @contextlib.contextmanager
+    def unsharded(self):
+        """Full f32 master inside the block (checkpoint save / load, state_dict); writes to
+        it are kept (this rank's range) when the block ends.  Collective when sharded."""
+        if self.shard is None:
+            yield self
+            return
+        lo, hi, gather = self.shard
+        shard = self.master
+        self.master = gather(shard)
+        self.shard = None
+        try:
+            yield self
+        finally:
+            shard.copy_(self.master[lo:hi])
+            self.master = shard
+            self.shard = (lo, hi, gather)
+
+    def opt_views(self):
+        """(master, grad, w16, n_decay) that the optimizer updates: the whole arena, or
+        this rank's range of a sharded one (n_decay relative to it)."""
+        if self.shard is None:
+            return self.master, self.grad, self.w16, self.n_decay
+        lo, hi, _ = self.shard
+        return self.master, self.grad[lo:hi], self.w16[lo:hi], max(0, min(self.n_decay, hi) - lo)
 
     def set_lanes(self, n: int) -> None:
         """Keep ``n`` gradient buffers: two microbatches of different lanes run their
@@ -749,10 +793,14 @@ class HeadShard:
     (accumulated locally, all-reduced once per step).  With tied embeddings the
     first stage's embedding reads/updates this same arena."""
 
-    def __init__(self, cfg: NativeConfig, device, seed: int = 0, dtype=torch.bfloat16, init: bool = True):
+    def __init__(self, cfg: NativeConfig, device, seed: int = 0, dtype=torch.bfloat16, init: bool = True,
+                 shards: int = 1):
         self.cfg = cfg
         self.device = torch.device(device)
-        self.arena = ParamArena(head_param_specs(cfg), self.device, dtype=dtype, seed=seed, init=init)
+        # numel divisible by 8 x shards: equal, 16-byte aligned blocks for the ZeRO-1
+        # reduce-scatter / all-gather over the pipeline group (engine.py)
+        self.arena = ParamArena(head_param_specs(cfg), self.device, dtype=dtype, seed=seed, init=init,
+                                numel_multiple=8 * max(1, shards))
         self.wname = "tok_embeddings.weight" if cfg.tie_embeddings else "output.weight"
 
     def weight(self):

@@ -159,11 +159,19 @@ class NativeStage(StageBase):
     def infer_output_specs(self, args):
         return self.output_specs
 
+    # REDUCE_GRAD issues through parallel/collectives.py, which records its own native
+    # COLL instruction (or CALL) on a recording step's tape
+    records_own_collectives = True
+    coll = None     # set by the trainer (engine.PipelineTrainer)
+
     def reduce_grad(self, n_microbatches, scaled_in_loss):
         if not scaled_in_loss:
             self.arena.grad.div_(n_microbatches)
         if self.dp_group is not None and dist.get_world_size(self.dp_group) > 1:
-            # SUM: the 1/dp average is folded into the AdamW kernel (engine.FlatAdamW)
+            # SUM: the 1/dp average is folded into the AdamW kernel (engine.FlatAdamW).  One
+            # call over the flat arena: RCCL pipelines a large all-reduce internally
+            if self.coll is not None:
+                return self.coll.all_reduce(self.arena.grad, "dp")
             return allreduce_flat(self.arena.grad, self.dp_group, average=False)
         return None
 

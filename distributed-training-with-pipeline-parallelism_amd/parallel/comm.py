@@ -1,8 +1,9 @@
 """Point-to-point transport between pipeline stages.
 
-On MI355X the transport is the native RCCL engine (csrc/comm/rccl_p2p.h) over the
+On MI355X the transport is the native RCCL engine (csrc/comm/rccl_engine.h) over the
 point-to-point xGMI links: one communicator and one high-priority HIP stream per
 traffic direction (activations down, gradients up), grouped ``ncclSend``/``ncclRecv``,
+plus a third communicator for the step's collectives (parallel/collectives.py),
 pre-flight pinged at construction with an in-process fallback to torch p2p if any
 pipeline rank fails.  On CPU it is gloo (reference plumbing config, helper:175).  The
 executor hands this module :class:`~.ir.CommGroup` s whose per-peer order is already
@@ -73,32 +74,37 @@ class _NativeWork:
 
 def load_native_rccl(ext) -> None:
     """Bind the engine to the librccl PyTorch loaded (one RCCL per process)."""
-    ext.RcclP2P.load(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
+    ext.RcclEngine.load(os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so"))
 
 
 # message kind -> engine channel: 0 = activations down the pipeline (F, and the last
-# stage's hidden rows to the head ranks, H), 1 = gradients back up (B, head grads D)
+# stage's hidden rows to the head ranks, H), 1 = gradients back up (B, head grads D);
+# channel 2 carries the pipeline group's collectives (parallel/collectives.py)
 CHANNEL_OF_KIND = {"F": 0, "H": 0, "B": 1, "D": 1}
+PIPE_CHANNEL_SLOTS = (0, 1, 2)   # channel c issues on comm stream slot c (rccl_engine.h)
 
 
 def make_native_engine(group, ranks: Sequence[int], my_pipe_rank: int, device: torch.device):
     """Collective over the pipeline group: pipeline rank 0 draws one RCCL unique id per
-    channel, the group broadcasts them, every rank joins both communicators
-    (csrc/comm/rccl_p2p.h)."""
+    channel, the group broadcasts them, every rank joins the three communicators
+    (csrc/comm/rccl_engine.h).  RCCL's communicator init blocks until every peer joined:
+    callers run it under a watchdog (bench.py) or a process-group timeout."""
     from ..ops.kernels import load_ext
     ext = load_ext()
-    if ext is None or not hasattr(ext, "RcclP2P"):
+    if ext is None or not hasattr(ext, "RcclEngine"):
         raise RuntimeError("the native RCCL engine needs the built extension (_C.so)")
     load_native_rccl(ext)
-    nb = int(ext.RcclP2P.id_bytes()) * 2
+    nch = len(PIPE_CHANNEL_SLOTS)
+    nb = int(ext.RcclEngine.id_bytes()) * nch
     buf = torch.zeros(nb, dtype=torch.uint8, device=device)
     if my_pipe_rank == 0:
-        uid = ext.RcclP2P.unique_id() + ext.RcclP2P.unique_id()
+        uid = b"".join(ext.RcclEngine.unique_id() for _ in range(nch))
         buf.copy_(torch.frombuffer(bytearray(uid), dtype=torch.uint8))
     if len(ranks) > 1:
         dist.broadcast(buf, src=ranks[0], group=group)
     uid = bytes(buf.cpu().tolist())
-    return ext.RcclP2P(uid, len(ranks), my_pipe_rank, device.index if device.index is not None else 0)
+    return ext.RcclEngine(uid, len(ranks), my_pipe_rank, device.index if device.index is not None else 0,
+                          list(PIPE_CHANNEL_SLOTS))
 
 
 def preflight(engine, peers: Sequence[int], me: int, device: torch.device, timeout_s: float) -> Tuple[bool, str]:
@@ -135,8 +141,9 @@ def preflight(engine, peers: Sequence[int], me: int, device: torch.device, timeo
 
 def agree(ok: bool, group, device: torch.device) -> bool:
     """True iff every rank of ``group`` reports ok (control plane: a gloo group when
-    available, so a wedged RCCL channel cannot block the vote)."""
-    if group is None or not dist.is_initialized():
+    available, so a wedged RCCL channel cannot block the vote).  ``group=None`` is the
+    world group (as everywhere in torch.distributed): every rank still votes."""
+    if not dist.is_initialized() or dist.get_world_size(group) <= 1:
         return ok
     backend = dist.get_backend(group)
     dev = torch.device("cpu") if backend == "gloo" else device
@@ -152,7 +159,7 @@ class P2P:
     ``MIPIPE_P2P``):
 
     * ``auto`` (default) / ``native`` -- on GPUs with the RCCL backend, the C++ engine
-      (csrc/comm/rccl_p2p.h): one communicator + stream per direction, grouped
+      (csrc/comm/rccl_engine.h): one communicator + stream per direction, grouped
       ncclSend/ncclRecv, posts replayed natively by the stage runner.  It is created and
       pinged (:func:`preflight`) at construction; if any rank of the pipeline fails, every
       rank agrees (:func:`agree`) to fall back to torch p2p in-process -- ``auto`` logs
@@ -191,7 +198,8 @@ class P2P:
             all_ok = agree(ok, ctrl_group if ctrl_group is not None else group, device)
             if all_ok:
                 self.engine = eng
-                self.channels = int(eng.channels)
+                # p2p directions; the engine's last channel is the collective channel
+                self.channels = min(2, int(eng.channels))
             else:
                 if eng is not None:
                     eng.abort()

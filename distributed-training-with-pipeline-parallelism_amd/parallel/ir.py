@@ -31,6 +31,10 @@ class Op(enum.Enum):
     SEND_B = "SEND_B"
     RECV_B = "RECV_B"
     REDUCE_GRAD = "REDUCE_GRAD"
+    # distributed LM head: ``rREDUCE_HEAD`` = rank r issues the reduction of the replicated
+    # head's gradient (reduce-scatter over the pipeline, then all-reduce of its shard over
+    # DP) -- a collective of the whole pipeline group, placed by :func:`.lower.add_head_reduce`
+    REDUCE_HEAD = "REDUCE_HEAD"
     # distributed LM head (see :mod:`.headsplit`): ``rH m`` = rank r's token chunk of
     # microbatch m through the head + loss (fwd and bwd fused); the last stage sends the
     # chunk's final hidden states (SEND_H) and receives its input gradient (RECV_D)
@@ -43,6 +47,10 @@ class Op(enum.Enum):
     @property
     def is_compute(self) -> bool:
         return self in (Op.F, Op.B, Op.I, Op.W, Op.H)
+
+    @property
+    def is_collective(self) -> bool:
+        return self in (Op.REDUCE_GRAD, Op.REDUCE_HEAD)
 
     @property
     def is_comm(self) -> bool:
@@ -61,7 +69,7 @@ class Op(enum.Enum):
 MSG_OPS = {"F": (Op.SEND_F, Op.RECV_F), "B": (Op.SEND_B, Op.RECV_B), "H": (Op.SEND_H, Op.RECV_H),
            "D": (Op.SEND_D, Op.RECV_D)}
 
-_ACTION_RE = re.compile(r"^(\d+)(SEND_F|RECV_F|SEND_B|RECV_B|SEND_H|RECV_H|SEND_D|RECV_D|REDUCE_GRAD|F|B|I|W|H)(\d*)$")
+_ACTION_RE = re.compile(r"^(\d+)(SEND_F|RECV_F|SEND_B|RECV_B|SEND_H|RECV_H|SEND_D|RECV_D|REDUCE_GRAD|REDUCE_HEAD|F|B|I|W|H)(\d*)$")
 
 
 @dataclass(frozen=True)

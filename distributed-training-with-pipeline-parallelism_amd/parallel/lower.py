@@ -136,14 +136,49 @@ def lower(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1, st
             # (its sends), in descending index order, so a blocking grad reduction can
             # never hold back the send its peer is waiting for
             for st, i in sorted(last_bwd.items(), key=lambda kv: -kv[1]):
-                j = i + 1
-                while j < len(program[r]) and isinstance(program[r][j], CommGroup) and \
-                        all(op.action.op.is_send for op in program[r][j].ops):
-                    j += 1
-                program[r].insert(j, Action(st, Op.REDUCE_GRAD))
+                program[r].insert(_after_sends(program[r], i), Action(st, Op.REDUCE_GRAD))
     if check:
         check_lowered(program, S)
     return program
+
+
+def _after_sends(prog: List[Entry], i: int) -> int:
+    """Index right after entry ``i`` and the send-only comm groups that directly follow it
+    (a collective placed there never holds back the send its peer waits for)."""
+    j = i + 1
+    while j < len(prog) and isinstance(prog[j], CommGroup) and all(op.action.op.is_send for op in prog[j].ops):
+        j += 1
+    return j
+
+
+def add_head_reduce(program: Dict[int, List[Entry]], after_stage0: bool = False) -> Dict[int, List[Entry]]:
+    """Insert ``rREDUCE_HEAD`` into every rank's program, right after the rank's last write
+    to the replicated head arena -- its last ``H`` (with tied embeddings also stage 0's last
+    backward, whose embedding gradient lands in the head arena) and the sends that follow
+    it -- so the head-gradient reduction overlaps the rest of the flush.  Every rank of the
+    pipeline issues exactly one (a collective of the whole group)."""
+    out = {}
+    for r, prog in program.items():
+        last = -1
+        for i, e in enumerate(prog):
+            if isinstance(e, Action) and (e.op == Op.H or (after_stage0 and e.stage == 0 and
+                                                            e.op in (Op.B, Op.I, Op.W))):
+                last = i
+        j = _after_sends(prog, last) if last >= 0 else len(prog)
+        out[r] = list(prog[:j]) + [Action(r, Op.REDUCE_HEAD)] + list(prog[j:])
+    return out
+
+
+def defer_collectives(program: Dict[int, List[Entry]]) -> Dict[int, List[Entry]]:
+    """Move every collective (``REDUCE_GRAD``, ``REDUCE_HEAD``) to the end of its rank's
+    program, keeping their relative order: all point-to-point traffic of the step is
+    issued before the first collective.  The safe placement when comm streams may share a
+    hardware queue with compute (see :func:`.simulate.check_lowered` ``serial``)."""
+    out = {}
+    for r, prog in program.items():
+        coll = [e for e in prog if isinstance(e, Action) and e.op.is_collective]
+        out[r] = [e for e in prog if not (isinstance(e, Action) and e.op.is_collective)] + coll
+    return out
 
 
 def format_program(program: Dict[int, List[Entry]]) -> str:

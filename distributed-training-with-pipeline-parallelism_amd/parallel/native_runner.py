@@ -9,9 +9,11 @@ a ``StageRunner`` (csrc/runtime/stage_runner.cpp) that replays the step with the
 released: no per-action Python, no allocator traffic, no host synchronisation.
 
 Transfers on the native RCCL engine (the default p2p transport on GPUs) become native
-POST/WAIT instructions (one per direction channel); transfers through ``torch.distributed`` (RCCL via ProcessGroupNCCL, or gloo)
-and DP all-reduces become CALL instructions that re-issue the same Python call on the same
-persistent tensors, so the runner is exact for every backend.  Anything that would break
+POST/WAIT instructions (one per direction channel), and the step's collectives on the native
+engines (parallel/collectives.py: DP gradient all-reduce, head-gradient reduce-scatter) native
+COLL/WAIT instructions.  Only transfers / collectives through ``torch.distributed`` (gloo on
+CPU, or the torch p2p fallback) become CALL instructions that re-issue the same Python call on
+the same persistent tensors, so the runner is exact for every backend.  Anything that would break
 replay (a graph captured during the recording step, a dependency tracker or profiler
 attached) invalidates the tape and the runtime stays on the Python path.
 
@@ -105,6 +107,17 @@ class TapeRecorder:
                 out.append((t.data_ptr(), t.numel(), code, int(peer)))
             return out
         return self.runner.add_post(engine, int(channel), ops(sends), ops(recvs))
+
+    def native_coll(self, engine, channel: int, op: int, send: torch.Tensor, recv: torch.Tensor,
+                    nranks: int) -> int:
+        """A collective on a native engine (op codes of csrc/comm/rccl_engine.h CollOp)."""
+        code = _DTYPE_CODE.get(send.dtype)
+        if code is None or not (send.is_contiguous() and recv.is_contiguous()):
+            self.invalidate(f"unsupported collective tensor {send.dtype}")
+            code = 6
+        count = send.numel() if op == 2 else recv.numel()   # ALL_GATHER counts the send block
+        return self.runner.add_coll(engine, int(channel), int(op), send.data_ptr(), recv.data_ptr(), int(count),
+                                    code)
 
     def native_wait(self, slot: int) -> None:
         self.runner.add_wait(slot)

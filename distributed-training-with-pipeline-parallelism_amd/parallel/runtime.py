@@ -39,7 +39,7 @@ from .comm import P2P
 from .debug import DepTracker, debug_level
 from .headsplit import HeadPlan
 from .ir import Action, CommGroup, Entry, Op, format_compute_grid
-from .lower import lower
+from .lower import add_head_reduce, defer_collectives, lower
 from .schedules import canonical_name, generate, stage_to_rank
 from .simulate import message_channel
 from .stage import StageBase, specs_of
@@ -114,7 +114,7 @@ class PipelineRuntime:
                  style: str = "loop", program: Optional[Dict[int, List[Entry]]] = None, profile: bool = False,
                  orders: Optional[Dict[int, List[Action]]] = None, head: Optional[HeadPlan] = None,
                  head_costs: Optional[Dict[int, float]] = None, stage_costs: Optional[Sequence[float]] = None,
-                 debug: Optional[int] = None):
+                 debug: Optional[int] = None, dp: int = 1, head_reduce_after_stage0: bool = False):
         self.stages: Dict[int, StageBase] = {s.stage_index: s for s in stages}
         self.schedule = canonical_name(schedule)
         self.m = n_microbatches
@@ -142,20 +142,15 @@ class PipelineRuntime:
             validate(orders, pp_size, self.v, n_microbatches, style)
             self.orders = orders
             program = lower(orders, pp_size, self.v, style, head_costs=head_costs, stage_costs=stage_costs)
+            if head is not None:
+                program = add_head_reduce(program, after_stage0=head_reduce_after_stage0)
         else:
             self.orders = {r: [e for e in es if isinstance(e, Action) and e.op.is_compute] for r, es in program.items()}
+        self.device = any_stage.device
+        self.dp = int(dp)
+        program = self._prove(program, p2p)
         self.program_all = program
         self.program = program[pp_rank]
-        # the native engine posts each group split by direction (one RCCL communicator +
-        # stream per channel): use that only if the split order is proven hang-free
-        if getattr(p2p, "channels", 1) > 1:
-            from .simulate import check_lowered
-            try:
-                check_lowered(program, self.num_stages, channels=p2p.channels)
-            except RuntimeError as e:
-                log.warning("two-channel p2p order not provably safe (%s): single channel", e)
-                p2p.use_single_channel()
-        self.device = any_stage.device
         self.profile = profile
         self.timer = _Timer(self.device)
         self.last_timeline: List[Tuple[str, float, float]] = []
@@ -176,13 +171,9 @@ class PipelineRuntime:
         self.native_enabled = os.environ.get("MIPIPE_NATIVE_RUNNER", "1") != "0"
         self.native_runner = None
         self.native_reason = "not recorded yet"
-        # distributed head: ``head_reduce()`` issues the async all-reduce of the replicated
-        # head gradient; it runs right after this rank's last action that writes the head
-        # arena (its last H; with tied embeddings also stage 0's last backward), so it
-        # overlaps the rest of the flush instead of following the step
-        self.head_reduce: Optional[Callable[[], object]] = None
-        self.head_reduce_after_stage0 = False
-        self._head_reduce_idx: Optional[int] = None
+        # distributed head: ``head_reduce()`` issues the reduction of the replicated head's
+        # gradient (returns work handles); the program's REDUCE_HEAD action says when
+        self.head_reduce: Optional[Callable[[], list]] = None
         # microbatch lanes (set_lanes): odd microbatches on a second HIP stream
         self.lanes = 1
         self.lane_streams: List[Optional[torch.cuda.Stream]] = [None]
@@ -190,6 +181,49 @@ class PipelineRuntime:
         self._in_bufs: Dict[int, Tuple[torch.Tensor, ...]] = {}
         self._tgt_bufs: Dict[int, torch.Tensor] = {}
         self._loss_bufs: Dict[tuple, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ hang-freedom
+    def _prove(self, program: Dict[int, List[Entry]], p2p) -> Dict[int, List[Entry]]:
+        """Choose where the step's collectives go and PROVE the resulting program cannot
+        hang under the queue model that holds on this machine (simulate.check_lowered).
+
+        Default: collectives deferred to the end of the step (after every p2p group), and the
+        program must pass the *serial* model -- one FIFO per rank, the worst case of any
+        stream -> hardware-queue mapping (GPU_MAX_HW_QUEUES per priority; RCCL's own
+        internal streams included), so nothing about the mapping needs to be known.
+        ``MIPIPE_COLL_OVERLAP=1`` keeps each collective where it was placed (DP all-reduce
+        right after the stage's last backward, head reduction after the rank's last head
+        chunk) to overlap the flush; that needs the *independent* model, so it is used only
+        if the hardware-queue probe (parallel/queues.py) finds every comm stream on a queue
+        of its own.  With two p2p channels the per-direction order is proven as well
+        (independent model), else the p2p falls back to one channel.  A program that no
+        model admits raises instead of running."""
+        from .simulate import check_lowered
+        S = self.num_stages
+        has_coll = any(isinstance(e, Action) and (e.op == Op.REDUCE_HEAD or (e.op == Op.REDUCE_GRAD and self.dp > 1))
+                       for es in program.values() for e in es)
+        self.coll_placement = "none"
+        self.queue_report = None
+        if has_coll:
+            overlap = os.environ.get("MIPIPE_COLL_OVERLAP", "0") == "1" and getattr(p2p, "kind", "") == "native"
+            if overlap and self.device.type == "cuda":
+                from .queues import comm_queues_independent
+                overlap, self.queue_report = comm_queues_independent(self.device)
+            if overlap:
+                check_lowered(program, S, channels=getattr(p2p, "channels", 1), dp=self.dp)
+                self.coll_placement = "overlapped (independent queues, probed)"
+            else:
+                program = defer_collectives(program)
+                self.coll_placement = "step end (serial-model proof)"
+        if getattr(p2p, "channels", 1) > 1:
+            try:
+                check_lowered(program, S, channels=p2p.channels, dp=self.dp)
+            except RuntimeError as e:
+                log.warning("two-channel p2p order not provably safe (%s): single channel", e)
+                p2p.use_single_channel()
+        if self.coll_placement != "overlapped (independent queues, probed)":
+            check_lowered(program, S, serial=True, dp=self.dp)
+        return program
 
     # ------------------------------------------------------------------ lanes
     def set_lanes(self, n: int) -> int:
@@ -554,15 +588,8 @@ class PipelineRuntime:
                 return contextlib.nullcontext()
             return _Range(f"PP:{a}")
 
-        hr_idx = self._head_reduce_index() if self.head_reduce is not None else None
         self._fork_lanes(rec)
         for idx, e in enumerate(self.program):
-            if hr_idx is not None and idx == hr_idx:
-                if rec is not None:
-                    from .native_runner import record_issue
-                    reduce_works.extend(record_issue(rec, lambda: [self.head_reduce()]))
-                else:
-                    reduce_works.append(self.head_reduce())
             try:
                 if isinstance(e, CommGroup):
                     sends, recvs, rkeys, sch, rch = [], [], [], [], []
@@ -588,12 +615,17 @@ class PipelineRuntime:
                         recv_works.setdefault(k, []).append(w)
                     continue
                 a = e
+                if a.op == Op.REDUCE_HEAD:
+                    if self.head_reduce is not None:
+                        reduce_works.extend(self.head_reduce())
+                    continue
                 st = self.stages.get(a.stage)
                 if a.op == Op.REDUCE_GRAD:
                     self._join_lanes(rec)
                     if rec is not None and not st.has_grad_reduction(self.scale_grads):
-                        continue    # nothing to issue (no DP, scale folded into the loss): no CALL
-                    if rec is not None:
+                        continue    # nothing to issue (no DP, scale folded into the loss)
+                    if rec is not None and not getattr(st, "records_own_collectives", False):
+                        # an autograd stage's torch.distributed reduction: a CALL on the tape
                         from .native_runner import record_issue
 
                         def _rg(st=st):
@@ -617,12 +649,6 @@ class PipelineRuntime:
                 self._report_failure(idx)
                 raise
         self._join_lanes(rec)
-        if hr_idx is not None and hr_idx >= len(self.program):
-            if rec is not None:
-                from .native_runner import record_issue
-                reduce_works.extend(record_issue(rec, lambda: [self.head_reduce()]))
-            else:
-                reduce_works.append(self.head_reduce())
         if deps is not None:
             deps.finish(send_tensors, handoff)
         for w in send_keep:
@@ -641,24 +667,6 @@ class PipelineRuntime:
         if self.stages.get(S - 1) is not None and return_outputs:
             return [outputs[i] for i in sorted(outputs)]
         return None
-
-    def _head_reduce_index(self) -> int:
-        """Program index right after this rank's last write to the head arena (and after
-        the sends that directly follow it, so the peer's transfers are not held back)."""
-        if self._head_reduce_idx is None:
-            last = -1
-            for i, e in enumerate(self.program):
-                if not isinstance(e, Action):
-                    continue
-                if e.op == Op.H or (self.head_reduce_after_stage0 and e.stage == 0 and
-                                    e.op in (Op.B, Op.I, Op.W)):
-                    last = i
-            j = last + 1
-            while j < len(self.program) and isinstance(self.program[j], CommGroup) and \
-                    all(op.action.op.is_send for op in self.program[j].ops):
-                j += 1
-            self._head_reduce_idx = j
-        return self._head_reduce_idx
 
     def _run_compute(self, a: Action, st, inputs, targets, return_outputs, loss_scale, handoff, outputs, mb_losses,
                      wait_recv, read_recv, produce) -> None:

@@ -168,87 +168,132 @@ def message_channel(key: tuple) -> int:
     return 0 if key[0] in ("F", "H") else 1
 
 
-def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: int = 1) -> None:
+def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: int = 1, serial: bool = False,
+                  dp: int = 1) -> None:
     """Raise RuntimeError if the lowered program can hang under RCCL semantics.
 
-    Model: per rank one in-order compute stream and ``channels`` in-order comm streams
-    (``channels=2``: each CommGroup is split by :func:`message_channel` and every part goes
-    to its direction's stream, as the native engine posts it).  A posted group starts
-    after the previous group of its stream completed and after every compute issued
-    before it; a message completes when both endpoint groups have started; a group
-    completes when all its messages have; a compute waits for the groups carrying its
-    inputs.  A fixpoint that does not finish means the program can hang."""
-    comp_orders = {r: [e for e in es if isinstance(e, Action)] for r, es in program.items()}
+    Queues of a rank (each a FIFO in host issue order = program order):
+
+    * independent model (``serial=False``, every stream on a hardware queue of its own):
+      one compute queue; ``channels`` p2p queues (``channels=2``: each CommGroup is split
+      by :func:`message_channel`, one part per direction stream, as the native engine posts
+      it); one collective queue (``REDUCE_GRAD`` with ``dp > 1`` -- the stage's DP
+      all-reduce -- and ``REDUCE_HEAD`` -- the pipeline-wide head reduction);
+    * serial model (``serial=True``): ONE queue holding every entry -- the worst case of
+      hardware-queue sharing (GPU_MAX_HW_QUEUES streams per priority, a blocked RCCL kernel
+      holds its queue).  Any real stream -> queue mapping only removes ordering edges from
+      this model, so a program proven here cannot hang whatever the mapping.
+
+    Rules: an entry starts when it is at the head of its queue and the previous entry of
+    the queue has COMPLETED; a comm group or collective also waits for every compute
+    issued before it (the engine orders its stream after the compute stream); a compute
+    waits for the groups carrying its inputs (stream-event waits).  A compute completes
+    when it starts; a p2p group when every message in it has both endpoint groups started;
+    a collective when every member has started it (``REDUCE_HEAD``: every rank of the
+    program; ``REDUCE_GRAD``: the same stage of the DP replicas, which run this program
+    symmetrically).  A fixpoint that does not drain every queue means a possible hang."""
+    comp_orders = {r: [e for e in es if isinstance(e, Action) and e.op.is_compute] for r, es in program.items()}
     split = uses_split_backward(comp_orders)
     head = head_ranks_of(comp_orders)
     ranks = sorted(program)
     chan = (lambda key: 0) if channels <= 1 else message_channel
-    # posted (sub)groups per rank: (channel, ops, index of the last compute issued before it)
-    posts: Dict[int, List[Tuple[int, List, int]]] = {}
-    comp_list: Dict[int, List[Action]] = {}
+    # items per rank: (queue, kind, payload, index of the last compute issued before it)
+    #   kind 'c': compute Action; 'g': list of CommOps; 'x': collective key
+    items: Dict[int, List[Tuple[object, str, object, int]]] = {}
     for r in ranks:
-        posts[r], comp_list[r] = [], []
+        lst = []
+        ncomp = 0
         for e in program[r]:
             if isinstance(e, CommGroup):
                 by_ch: Dict[int, List] = {}
                 for op in e.ops:
                     by_ch.setdefault(chan(op.key), []).append(op)
                 for ch in sorted(by_ch):
-                    posts[r].append((ch, by_ch[ch], len(comp_list[r]) - 1))
-            else:
-                comp_list[r].append(e)
-    msg_groups: Dict[tuple, List[Tuple[int, int]]] = {}
-    recv_group_of: Dict[tuple, Tuple[int, int]] = {}
-    queues: Dict[Tuple[int, int], List[int]] = {}       # (rank, channel) -> post indices in order
+                    lst.append((0 if serial else ("p", ch), "g", by_ch[ch], ncomp - 1))
+            elif e.op.is_compute:
+                lst.append((0 if serial else "c", "c", e, ncomp - 1))
+                ncomp += 1
+            elif e.op == Op.REDUCE_HEAD:
+                lst.append((0 if serial else "x", "x", ("RH",), ncomp - 1))
+            elif e.op == Op.REDUCE_GRAD and dp > 1:
+                lst.append((0 if serial else "x", "x", ("RG", e.stage, r), ncomp - 1))
+        items[r] = lst
+    # message -> the (rank, item) endpoints; collective key -> members
+    msg_items: Dict[tuple, List[Tuple[int, int]]] = {}
+    recv_item_of: Dict[tuple, Tuple[int, int]] = {}
+    coll_items: Dict[tuple, List[Tuple[int, int]]] = {}
+    comp_index: Dict[Tuple[int, int], int] = {}
     for r in ranks:
-        for gi, (ch, ops, _) in enumerate(posts[r]):
-            queues.setdefault((r, ch), []).append(gi)
-            for op in ops:
-                msg_groups.setdefault(op.key, []).append((r, gi))
-                if op.action.op.is_recv:
-                    recv_group_of[(r,) + op.key] = (r, gi)
-    for k, gs in msg_groups.items():
+        ci = 0
+        for ii, (q, kind, pl, _) in enumerate(items[r]):
+            if kind == "g":
+                for op in pl:
+                    msg_items.setdefault(op.key, []).append((r, ii))
+                    if op.action.op.is_recv:
+                        recv_item_of[(r,) + op.key] = (r, ii)
+            elif kind == "x":
+                coll_items.setdefault(pl, []).append((r, ii))
+            else:
+                comp_index[(r, ci)] = ii
+                ci += 1
+    for k, gs in msg_items.items():
         if len(gs) != 2:
             raise RuntimeError(f"message {k} has {len(gs)} endpoints (expected send+recv)")
-    comp_waits: Dict[Tuple[int, int], List[Tuple[int, int]]] = {}
+    n_rh = len(coll_items.get(("RH",), []))
+    if n_rh and n_rh != len(ranks):
+        raise RuntimeError(f"REDUCE_HEAD issued by {n_rh} of {len(ranks)} ranks")
+    waits: Dict[Tuple[int, int], List[Tuple[int, int]]] = {}
     for r in ranks:
-        for ci, a in enumerate(comp_list[r]):
-            comp_waits[(r, ci)] = [recv_group_of[(r,) + key] for _, key in in_messages(a, num_stages, split, head)
-                                   if key is not None and (r,) + key in recv_group_of]
-    comp_done: Dict[Tuple[int, int], bool] = {}
-    grp_started: Dict[Tuple[int, int], bool] = {}
-    grp_done: Dict[Tuple[int, int], bool] = {}
-    cptr = {r: 0 for r in ranks}
+        for ii, (q, kind, pl, _) in enumerate(items[r]):
+            if kind == "c":
+                waits[(r, ii)] = [recv_item_of[(r,) + key] for _, key in in_messages(pl, num_stages, split, head)
+                                  if key is not None and (r,) + key in recv_item_of]
+    queues: Dict[Tuple[int, object], List[int]] = {}
+    for r in ranks:
+        for ii, (q, _, _, _) in enumerate(items[r]):
+            queues.setdefault((r, q), []).append(ii)
+    started: Dict[Tuple[int, int], bool] = {}
+    done: Dict[Tuple[int, int], bool] = {}
     qptr = {q: 0 for q in queues}
-    ncomp = {r: len(comp_list[r]) for r in ranks}
     changed = True
     while changed:
         changed = False
-        for r in ranks:
-            while cptr[r] < ncomp[r] and all(grp_done.get(g, False) for g in comp_waits[(r, cptr[r])]):
-                comp_done[(r, cptr[r])] = True
-                cptr[r] += 1
-                changed = True
         for q, lst in queues.items():
             r = q[0]
-            # retire completed heads, then start the next group if its computes are done
-            while qptr[q] < len(lst) and grp_done.get((r, lst[qptr[q]]), False):
+            while qptr[q] < len(lst) and done.get((r, lst[qptr[q]]), False):
                 qptr[q] += 1
                 changed = True
-            if qptr[q] < len(lst):
-                gi = lst[qptr[q]]
-                if (r, gi) not in grp_started:
-                    last_c = posts[r][gi][2]
-                    if last_c < 0 or comp_done.get((r, last_c), False):
-                        grp_started[(r, gi)] = True
-                        changed = True
-        for (r, gi) in list(grp_started):
-            if grp_done.get((r, gi)):
+            if qptr[q] >= len(lst):
                 continue
-            if all(all(grp_started.get(x, False) for x in msg_groups[op.key]) for op in posts[r][gi][1]):
-                grp_done[(r, gi)] = True
+            ii = lst[qptr[q]]
+            if (r, ii) in started:
+                continue
+            _, kind, pl, last_c = items[r][ii]
+            if kind == "c":
+                ok = all(done.get(g, False) for g in waits[(r, ii)])
+            else:
+                ok = last_c < 0 or done.get((r, comp_index[(r, last_c)]), False)
+            if ok:
+                started[(r, ii)] = True
+                if kind == "c":
+                    done[(r, ii)] = True
                 changed = True
-    stuck = {r for r in ranks if cptr[r] < ncomp[r]} | {q[0] for q, lst in queues.items() if qptr[q] < len(lst)}
+        for (r, ii) in list(started):
+            if done.get((r, ii)):
+                continue
+            _, kind, pl, _ = items[r][ii]
+            if kind == "g":
+                fin = all(all(started.get(x, False) for x in msg_items[op.key]) for op in pl)
+            else:
+                fin = all(started.get(x, False) for x in coll_items[pl])
+            if fin:
+                done[(r, ii)] = True
+                changed = True
+    stuck = sorted({q[0] for q, lst in queues.items() if qptr[q] < len(lst)})
     if stuck:
-        detail = {r: (str(comp_list[r][cptr[r]]) if cptr[r] < ncomp[r] else "-") for r in sorted(stuck)}
-        raise RuntimeError(f"lowered schedule can deadlock ({channels} comm channel(s)); stuck computes: {detail}")
+        detail = {}
+        for r in stuck:
+            heads = [str(items[r][lst[qptr[q]]][2]) for q, lst in queues.items() if q[0] == r and qptr[q] < len(lst)]
+            detail[r] = heads
+        model = "serial (one queue per rank)" if serial else f"{channels} comm channel(s)"
+        raise RuntimeError(f"lowered schedule can deadlock ({model}); stuck queue heads: {detail}")

@@ -46,6 +46,11 @@ def _flat_view(flat: torch.Tensor, arena, name: str) -> torch.Tensor:
     return flat[o: o + int(math.prod(shape))].view(shape)
 
 
+def _full(arena, t: torch.Tensor) -> torch.Tensor:
+    """An optimizer moment of ``arena`` over the whole arena (gathered when ZeRO-sharded)."""
+    return t if arena.shard is None else arena.shard[2](t)
+
+
 def _barrier():
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
@@ -64,13 +69,15 @@ def save_checkpoint(trainer, path: str, step: Optional[int] = None, extra: Optio
         head_params, head_moments = {}, {}
         for arena, slot, tag in _arenas(trainer):
             is_head = tag == "head"
-            for name in arena.order:
-                p = arena.master_view(name).detach().float().cpu().contiguous()
-                m = _flat_view(opt.m[slot], arena, name).detach().float().cpu().contiguous()
-                v = _flat_view(opt.v[slot], arena, name).detach().float().cpu().contiguous()
-                (head_params if is_head else params)[name] = p
-                (head_moments if is_head else moments)[name + ".exp_avg"] = m
-                (head_moments if is_head else moments)[name + ".exp_avg_sq"] = v
+            fm, fv = _full(arena, opt.m[slot]), _full(arena, opt.v[slot])
+            with arena.unsharded():
+                for name in arena.order:
+                    p = arena.master_view(name).detach().float().cpu().contiguous()
+                    m = _flat_view(fm, arena, name).detach().float().cpu().contiguous()
+                    v = _flat_view(fv, arena, name).detach().float().cpu().contiguous()
+                    (head_params if is_head else params)[name] = p
+                    (head_moments if is_head else moments)[name + ".exp_avg"] = m
+                    (head_moments if is_head else moments)[name + ".exp_avg_sq"] = v
         r = mesh.pp_rank
         if params:
             save_file(params, os.path.join(path, f"stage-pp{r}.safetensors"), metadata={"format": FORMAT})
@@ -139,20 +146,29 @@ def load_checkpoint(trainer, path: str, load_optimizer: bool = True, strict: boo
 
     missing = []
     for arena, slot, _ in _arenas(trainer):
-        for name in arena.order:
-            t = get(name)
-            if t is None:
-                missing.append(name)
-                continue
-            arena.master_view(name).copy_(t.reshape(arena.specs[name].shape).to(arena.device, torch.float32))
-            if load_optimizer:
-                m, v = get(name + ".exp_avg"), get(name + ".exp_avg_sq")
-                if m is not None and v is not None:
-                    _flat_view(opt.m[slot], arena, name).copy_(m.reshape(arena.specs[name].shape))
-                    _flat_view(opt.v[slot], arena, name).copy_(v.reshape(arena.specs[name].shape))
-                elif strict:
-                    missing.append(name + ".exp_avg")
-        arena.sync_w16()
+        sharded = arena.shard is not None
+        # moments of a ZeRO-sharded arena: loaded full, this rank's range kept
+        fm = torch.zeros(arena.numel, device=arena.device) if sharded else opt.m[slot]
+        fv = torch.zeros(arena.numel, device=arena.device) if sharded else opt.v[slot]
+        lo_hi = arena.shard[:2] if sharded else None
+        with arena.unsharded():
+            for name in arena.order:
+                t = get(name)
+                if t is None:
+                    missing.append(name)
+                    continue
+                arena.master_view(name).copy_(t.reshape(arena.specs[name].shape).to(arena.device, torch.float32))
+                if load_optimizer:
+                    m, v = get(name + ".exp_avg"), get(name + ".exp_avg_sq")
+                    if m is not None and v is not None:
+                        _flat_view(fm, arena, name).copy_(m.reshape(arena.specs[name].shape))
+                        _flat_view(fv, arena, name).copy_(v.reshape(arena.specs[name].shape))
+                    elif strict:
+                        missing.append(name + ".exp_avg")
+            arena.sync_w16()
+        if sharded and load_optimizer:
+            opt.m[slot].copy_(fm[lo_hi[0]:lo_hi[1]])
+            opt.v[slot].copy_(fv[lo_hi[0]:lo_hi[1]])
     if strict and missing:
         raise KeyError(f"checkpoint {path} lacks {len(missing)} tensors, e.g. {missing[:4]}")
     if load_optimizer:
@@ -178,11 +194,12 @@ def reference_state_dict(arenas, cfg) -> Dict[str, torch.Tensor]:
     holds for the same stage."""
     out: Dict[str, torch.Tensor] = {}
     for arena in arenas:
-        for name in arena.order:
-            t = arena.master_view(name).detach().float().cpu()
-            if name in VOCAB_ROWS:
-                t = t[: cfg.vocab_size]
-            out[name] = t.clone().contiguous()
+        with arena.unsharded():
+            for name in arena.order:
+                t = arena.master_view(name).detach().float().cpu()
+                if name in VOCAB_ROWS:
+                    t = t[: cfg.vocab_size]
+                out[name] = t.clone().contiguous()
     return out
 
 
@@ -193,20 +210,21 @@ def load_reference_state_dict(arenas, cfg, state_dict: Dict[str, torch.Tensor], 
     ``strict`` every arena tensor must be present.  Returns the keys that were loaded."""
     loaded, missing = [], []
     for arena in arenas:
-        for name in arena.order:
-            src = state_dict.get(name)
-            if src is None:
-                missing.append(name)
-                continue
-            dst = arena.master_view(name)
-            src = src.detach().to(dst.device, torch.float32)
-            if name in VOCAB_ROWS and src.shape[0] != dst.shape[0]:
-                dst.zero_()
-                dst[: src.shape[0]].copy_(src)
-            else:
-                dst.copy_(src.reshape(dst.shape))
-            loaded.append(name)
-        arena.sync_w16()
+        with arena.unsharded():
+            for name in arena.order:
+                src = state_dict.get(name)
+                if src is None:
+                    missing.append(name)
+                    continue
+                dst = arena.master_view(name)
+                src = src.detach().to(dst.device, torch.float32)
+                if name in VOCAB_ROWS and src.shape[0] != dst.shape[0]:
+                    dst.zero_()
+                    dst[: src.shape[0]].copy_(src)
+                else:
+                    dst.copy_(src.reshape(dst.shape))
+                loaded.append(name)
+            arena.sync_w16()
     if strict and missing:
         raise KeyError(f"reference state_dict lacks {len(missing)} tensors, e.g. {missing[:4]}")
     return loaded

@@ -16,8 +16,9 @@ ARGS = ["--model", "gpt2-tiny", "--vocab", "256", "--mbs", "1", "--seq", "32", "
         "--step-timeout", "4"]
 
 
-def _bench(extra, stall, timeout=240):
+def _bench(extra, stall, timeout=240, **envx):
     env = dict(os.environ, MIPIPE_FAULT_STALL=stall, OMP_NUM_THREADS="1", MIPIPE_BENCH_ATTEMPT_S="90")
+    env.update(envx)
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
@@ -42,6 +43,34 @@ def test_supervisor_retries_a_stalled_attempt():
     assert out["attempt"] == 1 and out["n_gpus"] == 2 and out["value"] > 0
     assert out["config"]["parallelism"] == "pp2"
     assert "attempt 0" in r.stderr
+
+
+def test_default_budget_fits_the_driver_timeout():
+    """The attempt budgets of the defaults never add up past 560 s of the driver's 600 s,
+    however long each attempt hangs (each runs out its whole budget)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    t, n = 0.0, 0
+    while n < 10:
+        b = bench.attempt_budget(t)
+        if b <= 0:
+            break
+        t += b + 5.0        # the attempt hangs to its limit; killing it takes <= 5 s
+        n += 1
+    assert n >= 2 and t <= 560.0, (n, t)
+
+
+def test_two_stalled_attempts_end_nonzero_within_the_deadline():
+    """Every attempt stalls: the supervisor gives up non-zero inside its global deadline
+    (scaled down here to 80 s; the default is 540 s, test above)."""
+    import time
+    t0 = time.monotonic()
+    r = _bench([], "1:2", timeout=200, MIPIPE_BENCH_DEADLINE_S="80", MIPIPE_BENCH_ATTEMPT_S="40")
+    dt = time.monotonic() - t0
+    assert r.returncode != 0
+    assert dt < 80 + 25, dt
+    assert "attempt 0" in r.stderr and "attempt 1" in r.stderr and "giving up" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
 
 
 def test_bench_eight_ranks_gpt2_small_layout():

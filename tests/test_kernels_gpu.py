@@ -498,30 +498,61 @@ def test_norm_bwd_fused_colsums():
 
 
 def test_native_rccl_engine_self_transfer():
-    """csrc/comm/rccl_p2p.cpp: a one-rank communicator sends to itself (grouped send+recv on
-    the engine's comm stream, stream-ordered completion), and only one RCCL is loaded."""
+    """csrc/comm/rccl_engine.cpp: a one-rank engine sends to itself (grouped send+recv on
+    the p2p channels' comm streams, stream-ordered completion), runs its collectives on the
+    collective channel, reuses the process-wide comm streams, and only one RCCL is loaded."""
     from mipipe.ops import kernels as _k
     from mipipe.parallel.comm import load_native_rccl
     ext = _k.load_ext()
     load_native_rccl(ext)
-    eng = ext.RcclP2P(ext.RcclP2P.unique_id() + ext.RcclP2P.unique_id(), 1, 0, torch.cuda.current_device())
-    assert eng.channels == 2 and eng.stream_handle(0) != eng.stream_handle(1)
+    dev = torch.cuda.current_device()
+    uid = lambda k: b"".join(ext.RcclEngine.unique_id() for _ in range(k))
+    eng = ext.RcclEngine(uid(3), 1, 0, dev, [0, 1, 2])
+    assert eng.channels == 3 and len({eng.stream_handle(c) for c in range(3)}) == 3
+    assert [eng.stream_handle(c) for c in range(3)] == [ext.comm_stream(dev, c) for c in range(3)]
     src = torch.randn(1 << 20, device=DEV).to(torch.bfloat16)
     dst = torch.empty_like(src)
     src2 = torch.arange(1000, device=DEV, dtype=torch.int64)
     dst2 = torch.zeros_like(src2)
     h = eng.post(0, [(src, 0)], [(dst, 0)])          # channel 0 (activations)
     h2 = eng.post(1, [(src2, 0)], [(dst2, 0)])       # channel 1 (gradients)
-    eng.wait(h)
-    eng.wait(h2)
+    g = torch.randn(4096, device=DEV)
+    ref = g.clone()
+    h3 = eng.coll(2, 0, g, g)                        # all-reduce (1 rank: identity), in place
+    out = torch.empty(4096, device=DEV)
+    h4 = eng.coll(2, 2, g, out)                      # all-gather into another buffer
+    mx = torch.tensor([3.0], device=DEV)
+    h5 = eng.coll(2, 3, mx, mx)                      # all-reduce max
+    for x in (h, h2, h3, h4, h5):
+        eng.wait(x)
     torch.cuda.synchronize()
     assert torch.equal(dst, src) and torch.equal(dst2, src2)
+    assert torch.equal(g, ref) and torch.equal(out, ref) and float(mx) == 3.0
     assert eng.query(h) and eng.query(h2)
     assert eng.async_error() == ""
     eng.close()
+    # a second engine (e.g. the DP group's, one channel on the collective slot) reuses the
+    # process-wide streams: no stream per engine, no drift of the hardware-queue mapping
+    eng2 = ext.RcclEngine(uid(1), 1, 0, dev, [2])
+    assert eng2.stream_handle(0) == ext.comm_stream(dev, 2)
+    eng2.close()
     with open("/proc/self/maps") as f:
         libs = {line.split()[-1] for line in f if "librccl" in line}
     assert len(libs) == 1, libs
+
+
+def test_queue_probe_detects_shared_and_separate_queues():
+    """csrc/kernels/probe.hip: the bounded spinner sees the flag store of another stream
+    when the two streams run on separate hardware queues, and times out (never hangs) when
+    the store is queued behind it on the SAME stream (a queue shared by construction)."""
+    from mipipe.parallel.queues import check_comm_queues, shares_queue
+    dev = torch.device(DEV)
+    s1 = torch.cuda.Stream(priority=-1)
+    shared, us = shares_queue(s1.cuda_stream, s1.cuda_stream, dev, timeout_us=5000)
+    assert shared and us >= 4000, (shared, us)
+    rep = check_comm_queues(dev, timeout_us=20000)
+    assert set(rep["pairs"]) >= {"comm:fwd|comm:bwd", "comm:fwd|compute", "comm:coll|dw_side"}
+    print(rep)
 
 
 @pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 5])

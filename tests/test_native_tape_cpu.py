@@ -10,9 +10,14 @@ replayed from C++.  Multi-rank RCCL cannot run on a one-GPU box, so this test sw
   data over one gloo group per channel;
 * ``FakeRunner`` -- ``StageRunner``'s interface; ``run()`` replays the tape in Python.
 
-It checks that a recorded PP=4 step holds only GRAPH/COPY/POST/WAIT plus CALLs for the
-collectives (the distributed head's gradient all-reduce, DP all-reduces), that both
-channels carry POSTs, and that replaying the tape trains exactly like the Python executor.
+* ``FakeEngine.coll`` -- the engines' collectives (the pipeline engine's collective
+  channel, the DP engine), run on gloo.
+
+It checks that a recorded PP=4 step (x DP=2, distributed ZeRO-1 head) holds only
+GRAPH/COPY/POST/WAIT/COLL -- no Python CALL: the DP all-reduce of REDUCE_GRAD and the
+head's reduce-scatter + shard all-reduce of REDUCE_HEAD are native COLL instructions --
+that both p2p channels carry POSTs, and that replaying the tape trains exactly like the
+Python executor.
 """
 import types
 
@@ -29,7 +34,7 @@ from mipipe.parallel.runtime import PipelineRuntime
 
 from dist_utils import run_world
 
-GRAPH, COPY, POST, WAIT, CALL = range(5)
+GRAPH, COPY, POST, WAIT, CALL, SYNC, COLL = range(7)
 
 
 def _nested_copy(dst, src):
@@ -89,6 +94,7 @@ class FakeEngine:
         self.groups, self.ranks, self.channels = groups, ranks, len(groups)
         self.reg, self.pending, self.next = {}, {}, 1
         self.posts = [0] * len(groups)
+        self.colls = 0
 
     def post(self, ch, sends, recvs):
         ops = []
@@ -102,6 +108,25 @@ class FakeEngine:
         self.next += 1
         self.pending[h] = dist.batch_isend_irecv(ops) if ops else []
         self.posts[ch] += 1
+        return h
+
+    def coll(self, ch, op, send, recv):
+        """Collectives complete on issue (the real engine runs them in one stream FIFO, so a
+        later collective always sees an earlier one's result)."""
+        # (by object, not pointer: an in-place reduce-scatter's block 0 shares the pointer)
+        self.last_coll = (send, recv)
+        g = self.groups[ch]
+        if op in (0, 3):
+            dist.all_reduce(recv, op=dist.ReduceOp.SUM if op == 0 else dist.ReduceOp.MAX, group=g)
+        elif op == 1:     # reduce-scatter in place: recv is this rank's block of send
+            dist.all_reduce(send, group=g)
+        else:             # all-gather in place: send is this rank's block of recv
+            parts = [torch.empty_like(send) for _ in range(dist.get_world_size(g))]
+            dist.all_gather(parts, send.clone(), group=g)
+            recv.copy_(torch.cat(parts).view_as(recv))
+        self.colls += 1
+        h = self.next
+        self.next += 1
         return h
 
     def wait(self, h):
@@ -130,6 +155,16 @@ class FakeRunner:
         self.tape.append((POST, (engine, ch, res(sends), res(recvs), self.nslots)))
         self.nslots += 1
         return self.nslots - 1
+
+    def add_coll(self, engine, ch, op, send, recv, count, code):
+        snd, rcv = engine.last_coll    # recorded right after the live engine.coll call
+        assert (snd.data_ptr(), rcv.data_ptr()) == (send, recv)
+        self.tape.append((COLL, (engine, ch, op, snd, rcv, self.nslots)))
+        self.nslots += 1
+        return self.nslots - 1
+
+    def collectives(self):
+        return [(x[1], x[2]) for k, x in self.tape if k == COLL]
 
     def add_wait(self, slot):
         self.tape.append((WAIT, slot))
@@ -160,6 +195,9 @@ class FakeRunner:
             elif k == POST:
                 eng, ch, s_, r_, slot = x
                 handles[slot] = (eng, eng.post(ch, s_, r_))
+            elif k == COLL:
+                eng, ch, op, snd, rcv, slot = x
+                handles[slot] = (eng, eng.coll(ch, op, snd, rcv))
             elif k == WAIT:
                 eng, h = handles.pop(x)
                 eng.wait(h)
@@ -205,12 +243,20 @@ def _worker(rank, world, pp, dp, schedule, v, native, steps):
         groups = []
         for d in range(dp):      # every rank creates every group, in the same order
             rr = [d * pp + i for i in range(pp)]
-            gs = [dist.new_group(rr, backend="gloo") for _ in range(2)]
+            gs = [dist.new_group(rr, backend="gloo") for _ in range(3)]   # fwd, bwd, coll
             if d == tr.mesh.dp_rank:
                 groups = gs
+        dgroup = None
+        for i in range(pp):
+            g_ = dist.new_group([d * pp + i for d in range(dp)], backend="gloo") if dp > 1 else None
+            if i == tr.mesh.pp_rank:
+                dgroup = g_
         eng = FakeEngine(groups, ranks)
         tr.runtime.p2p.engine = eng
         tr.runtime.p2p.channels = 2
+        tr.coll.pipe_engine, tr.coll.pp_kind = eng, "native"
+        if dp > 1:
+            tr.coll.dp_engine, tr.coll.dp_kind = FakeEngine([dgroup], None), "native"
         for st in tr.stages:
             st.graphs = FakeGraphCache(str(st.stage_index))
         if tr.runtime.head is not None:
@@ -223,9 +269,9 @@ def _worker(rank, world, pp, dp, schedule, v, native, steps):
     r = tr.runtime.native_runner
     if native:
         out.update(recorded=r is not None, kinds=r.kinds() if r else [], channels=r.channels() if r else [],
-                   runs=r.runs if r else 0, reason=tr.runtime.native_reason,
-                   n_reduce_grad_calls=sum(1 for st in tr.stages if st.has_grad_reduction(True)),
-                   head=tr.runtime.head_reduce is not None)
+                   colls=r.collectives() if r else [], runs=r.runs if r else 0, reason=tr.runtime.native_reason,
+                   n_reduce_grad=sum(1 for st in tr.stages if st.has_grad_reduction(True)),
+                   head=tr.runtime.head_reduce is not None, placement=tr.runtime.coll_placement)
     return out
 
 
@@ -239,11 +285,15 @@ def test_pp4_tape_is_native_and_replays_exactly(schedule, v, dp):
         assert o["recorded"], o["reason"]
         assert o["runs"] == 2                   # steps 4 and 5 replayed from the tape
         kinds = o["kinds"]
-        assert set(kinds) <= {GRAPH, COPY, POST, WAIT, CALL}
+        assert set(kinds) <= {GRAPH, COPY, POST, WAIT, COLL, SYNC}, kinds    # no CALL
         assert kinds.count(POST) > 0 and kinds.count(GRAPH) > 0
-        # CALLs only for collectives (an issue + a stream-wait each): the head-gradient
-        # all-reduce and the per-stage DP all-reduces
-        assert kinds.count(CALL) == 2 * (int(o["head"]) + o["n_reduce_grad_calls"]), kinds
+        # collectives: REDUCE_HEAD = reduce-scatter over the pipeline (+ the shard's DP
+        # all-reduce), one DP all-reduce per stage at REDUCE_GRAD; deferred to the step end
+        head_colls = [(2, 1)] + ([(0, 0)] if dp > 1 else [])
+        assert sorted(o["colls"]) == sorted(head_colls + [(0, 0)] * o["n_reduce_grad"]), o["colls"]
+        last_post = max(i for i, k in enumerate(kinds) if k == POST)
+        assert all(i > last_post for i, k in enumerate(kinds) if k == COLL), "collectives after every p2p group"
+        assert o["placement"].startswith("step end")
         # both directions use their own channel
         assert set(o["channels"]) == {0, 1}
         assert o["losses"] == pytest.approx(ref[r]["losses"], rel=1e-6, abs=1e-6)

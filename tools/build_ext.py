@@ -70,7 +70,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, variant: st
     incs, tlib, abi = _torch_paths()
     # translation units that include torch: the pybind module, the native RCCL engine, the stage runner
     host_hdrs = glob.glob(os.path.join(CSRC, "comm", "*.h"))
-    for bsrc in (os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "comm", "rccl_p2p.cpp"),
+    for bsrc in (os.path.join(CSRC, "bindings.cpp"), os.path.join(CSRC, "comm", "rccl_engine.cpp"),
                  os.path.join(CSRC, "runtime", "stage_runner.cpp")):
         bobj = os.path.join(OBJ, os.path.basename(bsrc) + ".o")
         objs.append(bobj)

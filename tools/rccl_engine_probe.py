@@ -1,4 +1,4 @@
-"""Step-by-step probe of the native RCCL P2P engine (csrc/comm/rccl_p2p.cpp) on one GPU.
+"""Step-by-step probe of the native RCCL P2P engine (csrc/comm/rccl_engine.cpp) on one GPU.
 
 Prints a line before each stage so a failure points at the exact call.  GPU only: run it
 through gpurun.
@@ -31,9 +31,9 @@ say("loaded")
 torch.cuda.init()
 dev = torch.cuda.current_device()
 say("device", dev)
-uid = ext.RcclP2P.unique_id() + ext.RcclP2P.unique_id()
+uid = b"".join(ext.RcclEngine.unique_id() for _ in range(3))
 say("uid", len(uid))
-eng = ext.RcclP2P(uid, 1, 0, dev)
+eng = ext.RcclEngine(uid, 1, 0, dev, [0, 1, 2])
 say("comm up")
 src = torch.randn(1 << 20, device="cuda").to(torch.bfloat16)
 dst = torch.empty_like(src)
