@@ -22,7 +22,7 @@ int mp_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe,
 int mp_sumsq(const float* g, int64_t n, float* out, hipStream_t st);
 int mp_gemm_f32(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int64_t lda,
                 int a_kc, int64_t ldb, int b_nc, int64_t ldc, float alpha, int accumulate, hipStream_t st);
-int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, hipStream_t st);
+int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, float* sumsq, hipStream_t st);
 int mp_adamw(float* p, float* g, float* m, float* v, void* w16, int64_t n, int64_t n_decay, float lr, float b1,
              float b2, float eps, float wd, int step, const float* sumsq, float max_norm, float grad_scale,
              int zero_grad, hipStream_t st);
@@ -55,6 +55,7 @@ int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void
              int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, float* colsum, float p_drop,
              uint64_t seed, hipStream_t st);
 int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg, int* split_out);
+int mp_gemm2_has_probe_engines();
 int mp_gemm_tt_grouped(int n, const void* const* A, const void* const* B, float* const* C, const int* M, const int* N,
                        const int* K, const int64_t* lda, const int64_t* ldb, const int64_t* ldc, float alpha,
                        hipStream_t st);
@@ -163,8 +164,9 @@ void embed_bwd(torch::Tensor idx, torch::Tensor dout, torch::Tensor dwte, c10::o
         "embed_bwd");
 }
 
-// g0 += sum(lanes); lanes zeroed (1..3 extra f32 lane buffers of g0's size)
-void lane_merge(torch::Tensor g0, std::vector<torch::Tensor> lanes) {
+// g0 += sum(lanes); lanes zeroed (1..3 extra f32 lane buffers of g0's size); with
+// `sumsq` (f32 [1]) also *sumsq += |merged g0|^2 in the same pass
+void lane_merge(torch::Tensor g0, std::vector<torch::Tensor> lanes, c10::optional<torch::Tensor> sumsq) {
   TORCH_CHECK(lanes.size() >= 1 && lanes.size() <= 3, "lane_merge: 1..3 lane buffers");
   req(g0, torch::kFloat32, "g0");
   float* p[3] = {nullptr, nullptr, nullptr};
@@ -173,7 +175,10 @@ void lane_merge(torch::Tensor g0, std::vector<torch::Tensor> lanes) {
     TORCH_CHECK(lanes[i].numel() == g0.numel(), "lane_merge: size mismatch");
     p[i] = lanes[i].data_ptr<float>();
   }
-  check(mp_lane_merge(g0.data_ptr<float>(), p[0], p[1], p[2], g0.numel(), cur_stream()), "lane_merge");
+  if (sumsq.has_value()) req(*sumsq, torch::kFloat32, "sumsq");
+  check(mp_lane_merge(g0.data_ptr<float>(), p[0], p[1], p[2], g0.numel(),
+                      sumsq.has_value() ? sumsq->data_ptr<float>() : nullptr, cur_stream()),
+        "lane_merge");
 }
 
 void sumsq(torch::Tensor g, torch::Tensor out) {
@@ -502,7 +507,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
-  m.def("lane_merge", &lane_merge);
+  m.def("lane_merge", &lane_merge, pybind11::arg("g0"), pybind11::arg("lanes"), pybind11::arg("sumsq") = pybind11::none());
   m.def("gemm_tt_grouped", &gemm_tt_grouped, pybind11::arg("dy"), pybind11::arg("x"), pybind11::arg("C"),
         pybind11::arg("alpha") = 1.0);
   m.def("gemm2", &gemm2, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
@@ -517,4 +522,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("result"), pybind11::arg("waiter") = 0);
   m.def("probe_set", &probe_set, pybind11::arg("flag"), pybind11::arg("value"), pybind11::arg("setter") = 0);
   m.def("probe_clock_khz", []() { return mp_probe_clock_khz(); });
+  m.def("gemm2_has_probe_engines", []() { return mp_gemm2_has_probe_engines() != 0; });
 }

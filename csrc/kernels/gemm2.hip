@@ -901,6 +901,9 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   return (int)hipGetLastError();
 }
 
+// gemm4 / gemm5: probe engines with recorded null results (profiles/r2_probes.md), built only
+// into the A/B variant (tools/build_ext.py --variant probes -D MP_PROBE_ENGINES), not _C.so.
+#ifdef MP_PROBE_ENGINES
 // ---------------------------------------------------------------------------------------
 // gemm4: persistent 256x256 NT GEMM (gemm3's 16x16x32 phase schedule) whose C write is
 // deferred into the NEXT tile's main loop.
@@ -1364,6 +1367,7 @@ static int launch5(const void* A, const void* B, void* C, const void* bias, cons
 }
 
 
+#endif  // MP_PROBE_ENGINES
 // ---------------------------------------------------------------------------------------
 // gemms: small-tile NT engine for short-token problems (the reference model's 1024-token
 // microbatches: M = 1024, N = 768..2304).  A 256x256 grid there has 12-36 tiles for 256
@@ -1649,9 +1653,11 @@ static int dispatch(int cfg, const void* A, const void* B, void* C, const void* 
     if (cfg == 12) return launchs<32, 32, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+#ifdef MP_PROBE_ENGINES
     if constexpr (!ACC) {
       if (cfg == 8) return launch5<EPI>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
     }
+#endif
   }
   switch (cfg) {
     case 0: return launch<256, 256, 2, 4, TA, TB, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
@@ -1719,22 +1725,39 @@ static int launch_splitk_epi(const float* ws, void* C, int M, int N, int64_t ldc
 
 // tile config + split-K factor the engine will use for this problem (callers size the
 // split-K workspace from it: split * M * N f32)
+// 1 when the probe engines (gemm4 cfg 7 / 100+G, gemm5 cfg 8) are compiled in
+extern "C" int mp_gemm2_has_probe_engines() {
+#ifdef MP_PROBE_ENGINES
+  return 1;
+#else
+  return 0;
+#endif
+}
+
 extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg,
                              int* split_out) {
   int split = 1;
   // 7: the persistent deferred-store engine (gemm4); 100 + G: gemm4 on a grid of G
   // workgroups (tests drive several tiles per workgroup through small problems)
+#ifdef MP_PROBE_ENGINES
   if (force_cfg == 7 || force_cfg >= 100) {
     *split_out = 1;
     return 7;
   }
+#else
+  if (force_cfg == 7 || force_cfg == 8 || force_cfg >= 100) return -1;   // probe engines not built
+#endif
   // 8: the 4-wave / one-wave-per-SIMD 256x256 NT engine (gemm5 probe; MIPIPE_GEMM5=1 uses
   // it wherever gemm3's M16 build would run without split-K)
+#ifdef MP_PROBE_ENGINES
   static const bool use5 = [] { const char* e = getenv("MIPIPE_GEMM5"); return e && e[0] == '1'; }();
   if (force_cfg == 8) {
     *split_out = 1;
     return 8;
   }
+#else
+  constexpr bool use5 = false;
+#endif
   int cfg = choose(M, N, K, c_f32_accum != 0, transA || transB, &split);
   if (force_cfg >= 0 && force_cfg < 7) cfg = force_cfg;
   if (force_cfg >= 10) cfg = 0;   // placeholder; the small-engine branches below set it
@@ -1816,6 +1839,8 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   // (MIPIPE_GEMM4=1): correct, but 1.2-2x slower than gemm3 -- the 64-VGPR stash does not
   // fit beside gemm3's 222 VGPRs at 2 waves/SIMD, and the spill reloads in the MFMA loop
   // drain the DMA pipeline (profiles/r2_probes.md "gemm4")
+  if (cfg < 0) return -1;
+#ifdef MP_PROBE_ENGINES
   static const bool use4 = [] { const char* e = getenv("MIPIPE_GEMM4"); return e && e[0] == '1'; }();
   const bool g4_ok = split == 1 && colsum == nullptr && !c_f32_accum && !transA && !transB &&
                      (epilogue == EPI_NONE || epilogue == EPI_BIAS) && ldc % 4 == 0;
@@ -1825,6 +1850,7 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
     if (epilogue == EPI_NONE) return launch4<EPI_NONE>(A, B, C, nullptr, M, N, K, lda, ldb, ldc, alpha, grid, st);
     return launch4<EPI_BIAS>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, grid, st);
   }
+#endif
   if (cfg == 7) return -2;
   float* wsp = (split > 1 || colsum != nullptr) ? ws : nullptr;
   int rc = -2;

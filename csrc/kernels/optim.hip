@@ -57,10 +57,52 @@ __global__ void __launch_bounds__(256) lane_merge_kernel(float* __restrict__ g0,
   }
 }
 
-extern "C" int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, hipStream_t st) {
+// lane merge + the clipping norm's sum of squares in ONE pass (the optimizer then reads
+// the merged g0 once more): g0 = g0 + g1 (+ g2 + g3), lanes zeroed, *sumsq += |g0|^2.  The
+// separate sumsq pass re-read the merged buffer (98 us of the reference model's step,
+// profiles/r2_end_ref_L8H8_kernel_stats.csv).
+__global__ void __launch_bounds__(256) lane_merge_sumsq_kernel(float* __restrict__ g0, float* __restrict__ g1,
+                                                               float* __restrict__ g2, float* __restrict__ g3,
+                                                               int64_t n, float* __restrict__ sumsq) {
+  __shared__ float red[4];
+  const int64_t n4 = n / 4;
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 a = reinterpret_cast<float4*>(g0)[i];
+    float4 b = reinterpret_cast<float4*>(g1)[i];
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    reinterpret_cast<float4*>(g1)[i] = z;
+    if (g2 != nullptr) {
+      b = reinterpret_cast<float4*>(g2)[i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      reinterpret_cast<float4*>(g2)[i] = z;
+    }
+    if (g3 != nullptr) {
+      b = reinterpret_cast<float4*>(g3)[i];
+      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      reinterpret_cast<float4*>(g3)[i] = z;
+    }
+    reinterpret_cast<float4*>(g0)[i] = a;
+    acc += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+  }
+  for (int64_t i = n4 * 4 + blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float a = g0[i] + g1[i];
+    g1[i] = 0.f;
+    if (g2 != nullptr) { a += g2[i]; g2[i] = 0.f; }
+    if (g3 != nullptr) { a += g3[i]; g3[i] = 0.f; }
+    g0[i] = a;
+    acc += a * a;
+  }
+  acc = block_sum<256>(acc, red);
+  if (threadIdx.x == 0) atomicAdd(sumsq, acc);
+}
+
+extern "C" int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, float* sumsq, hipStream_t st) {
   if (n <= 0) return 0;
   const int blocks = (int)std::min<int64_t>((n / 4 + 255) / 256 + 1, 8192);
-  lane_merge_kernel<<<blocks, 256, 0, st>>>(g0, g1, g2, g3, n);
+  if (sumsq != nullptr) lane_merge_sumsq_kernel<<<blocks, 256, 0, st>>>(g0, g1, g2, g3, n, sumsq);
+  else lane_merge_kernel<<<blocks, 256, 0, st>>>(g0, g1, g2, g3, n);
   return (int)hipGetLastError();
 }
 

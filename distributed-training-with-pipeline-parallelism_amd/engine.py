@@ -77,6 +77,9 @@ class FlatAdamW:
                 if a.shard is not None:     # this rank's (reduced) range of a sharded arena
                     ops.sumsq(a.opt_views()[1], self.sumsq)
                     continue
+                if len(a.grad_lanes) > 1 and a.merged_sumsq is not None and i not in self.norm_exclude:
+                    self.sumsq.add_(a.merged_sumsq)     # computed by the fused lane merge
+                    continue
                 lo = 0
                 for off, n in self.norm_exclude.get(i, ()):
                     if off > lo:

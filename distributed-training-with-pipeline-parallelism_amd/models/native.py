@@ -83,6 +83,7 @@ class ParamArena:
         # per-lane gradient buffers (microbatch lanes, parallel/runtime.py): lane 0 is
         # ``grad`` itself; the others are summed into it at the end of the step
         self.grad_lanes: List[torch.Tensor] = [self.grad]
+        self.merged_sumsq: Optional[torch.Tensor] = None   # set by merge_lanes (GPU, lanes > 1)
         self.w16 = torch.zeros(self.numel, dtype=dtype, device=self.device)
         # transposed bf16 copies of the matrices used as B in dX = dY W (GPU only)
         self.t_offsets: Dict[str, int] = {}
@@ -241,10 +242,19 @@ class ParamArena:
 
     def merge_lanes(self) -> None:
         """grad += every other lane's gradient; those are zeroed for the next step (one
-        fused pass on GPU: optim.hip lane_merge_kernel)."""
+        fused pass on GPU: optim.hip lane_merge_sumsq_kernel, which also leaves the merged
+        gradient's sum of squares in ``merged_sumsq`` for the optimizer's clipping norm --
+        engine.FlatAdamW then skips its own pass over this arena)."""
         g0 = self.grad_lanes[0]
         rest = self.grad_lanes[1:]
         if g0.is_cuda:
+            if len(rest) <= 3:
+                if self.merged_sumsq is None:
+                    self.merged_sumsq = torch.zeros(1, dtype=torch.float32, device=g0.device)
+                self.merged_sumsq.zero_()
+                ops.load_ext().lane_merge(g0, rest, self.merged_sumsq)
+                return
+            self.merged_sumsq = None
             for i in range(0, len(rest), 3):
                 ops.load_ext().lane_merge(g0, rest[i:i + 3])
             return

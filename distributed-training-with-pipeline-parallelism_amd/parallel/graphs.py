@@ -14,7 +14,12 @@ pipelines.  Design rules:
 * inputs are captured by pointer; if a later call passes a tensor at another address
   (e.g. the user's token chunk) it is copied into the captured buffer first;
 * communication stays outside the graphs (RCCL work is posted by the runtime between
-  replays, and ordered by stream waits), as do optimizer steps whose scalars change.
+  replays, and ordered by stream waits), as do optimizer steps whose scalars change;
+* capture never synchronises the device: actions are captured lazily in the middle of a
+  pipeline step, when receives posted on the comm streams may still be waiting for a peer
+  that itself waits for this rank (``torch.cuda.graph`` would ``torch.cuda.synchronize()``
+  on entry -- a cross-rank deadlock on the first multi-GPU capture step).  The capture
+  runs on a private stream ordered after the compute stream, in thread-local mode.
 
 Graphs are off on CPU.  Dropout is graph-safe: the per-site seeds are static kernel
 arguments, and every dropout kernel mixes in a device-side training-step counter
@@ -39,6 +44,29 @@ def _tensors(obj, out: List[torch.Tensor]) -> List[torch.Tensor]:
             _tensors(v, out)
     elif hasattr(obj, "__dict__") and not callable(obj):
         _tensors(vars(obj), out)
+    return out
+
+
+_CAPTURE_STREAMS: Dict[int, torch.cuda.Stream] = {}
+
+
+def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any]) -> Any:
+    """Capture ``fn()`` into ``g`` without a device-wide synchronisation (module docstring):
+    on a per-device capture stream that first waits for the current stream, thread-local
+    capture mode, a private memory pool."""
+    cur = torch.cuda.current_stream()
+    idx = cur.device.index if cur.device.index is not None else torch.cuda.current_device()
+    cs = _CAPTURE_STREAMS.get(idx)
+    if cs is None:
+        cs = _CAPTURE_STREAMS[idx] = torch.cuda.Stream(device=idx)
+    cs.wait_stream(cur)
+    with torch.cuda.stream(cs):
+        g.capture_begin(capture_error_mode="thread_local")
+        try:
+            out = fn()
+        finally:
+            g.capture_end()
+    cur.wait_stream(cs)
     return out
 
 
@@ -70,10 +98,7 @@ class GraphCache:
             if rec is not None:
                 rec.invalidate(f"graph {key!r} captured during the recording step")
             g = torch.cuda.CUDAGraph()
-            torch.cuda.synchronize()
-            # thread-local capture: the RCCL watchdog thread may query events meanwhile
-            with torch.cuda.graph(g, capture_error_mode="thread_local"):
-                out = fn(inputs)
+            out = capture(g, lambda: fn(inputs))
             kept = _tensors(keep(), []) if keep is not None else []
             entry = (g, list(inputs), out, kept)
             self.graphs[key] = entry

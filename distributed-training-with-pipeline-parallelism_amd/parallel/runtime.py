@@ -240,7 +240,6 @@ class PipelineRuntime:
         n = max(1, int(n))
         if n > 1 and (self.pp != 1 or len(self.stages) != 1 or self.device.type != "cuda" or self.m < 2):
             n = 1
-        self.lanes = n
         self.lane_streams = [None]
         idx = (self.device.index if self.device.index is not None else torch.cuda.current_device()) if n > 1 else 0
         # one set of lane streams per device and process: HIP maps each stream onto one of
@@ -251,10 +250,22 @@ class PipelineRuntime:
         # process); the first ones taken are reused instead
         cache = _LANE_STREAMS.setdefault(idx, [])
         main_s = torch.cuda.current_stream(idx).cuda_stream if n > 1 else None
-        while len(cache) < n - 1:
+        # ... and a lane must not land on the compute stream's hardware queue or another
+        # lane's: the spin/flag probe (parallel/queues.py, profiles/r3_queue_probe.json)
+        # found torch's second pool stream on the compute stream's queue -- the 3-lane
+        # anomaly of round 2 (456K tok/s vs 495K with 2 lanes, 594K with 4).  Candidates are
+        # drawn from the pool until one has a queue of its own (at most 4 per priority).
+        tried = 0
+        while len(cache) < n - 1 and tried < 64:
+            tried += 1
             ls = torch.cuda.Stream(device=idx)
-            if ls.cuda_stream != main_s and all(ls.cuda_stream != c.cuda_stream for c in cache):
-                cache.append(ls)
+            if ls.cuda_stream == main_s or any(ls.cuda_stream == c.cuda_stream for c in cache):
+                continue
+            if not self._own_queue(ls, [main_s] + [c.cuda_stream for c in cache]):
+                continue
+            cache.append(ls)
+        n = min(n, len(cache) + 1)
+        self.lanes = n
         self.lane_streams += cache[: n - 1]
         for st in self.stages.values():
             st.arena.set_lanes(n)
@@ -262,6 +273,18 @@ class PipelineRuntime:
                 st.model.wgrad_side = n == 1
         self.native_runner = None   # a recorded tape does not know about lanes
         return n
+
+    def _own_queue(self, s: torch.cuda.Stream, others) -> bool:
+        """True if stream ``s`` shares a hardware queue with none of ``others`` (probe; true
+        without the extension or with MIPIPE_LANE_PROBE=0)."""
+        if os.environ.get("MIPIPE_LANE_PROBE", "1") == "0":
+            return True
+        try:
+            from .queues import shares_queue
+            return not any(shares_queue(int(s.cuda_stream), int(o), self.device, timeout_us=5000)[0]
+                           for o in others)
+        except RuntimeError:
+            return True
 
     def _lane_ctx(self, a: Action, st):
         """Stream + gradient-lane context of one compute action."""

@@ -119,6 +119,13 @@ class PipelineStage(StageBase):
         # reference's 1024-token microbatches: hundreds of small ATen kernels) replay each
         # direction as one graph.  Captured lazily on the first forward of each slot.
         self.graphs = bool(graphs)
+        # make_graphed_callables synchronises the whole device while it captures, lazily, in
+        # the middle of a step: with RCCL receives pending on the comm streams that is a
+        # cross-rank wait.  Autograd-stage graphs stay for one process / gloo-staged runs;
+        # NativeStage graphs (parallel/graphs.py capture) never synchronise
+        import torch.distributed as dist
+        if self.graphs and dist.is_initialized() and dist.get_world_size() > 1 and dist.get_backend() == "nccl":
+            self.graphs = False
         self._graph_fns: Dict[int, Callable] = {}
         # f32 modules on GPU: every linear / attention projection on the f32 MFMA GEMM
         # (ops.f32_linears); off: ATen (hipBLASLt)
