@@ -6,22 +6,25 @@
 #include <hip/hip_runtime.h>
 
 extern "C" {
-int mp_norm_fwd(int rms, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
+int mp_norm_fwd(int f32, int rms, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
                 float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed, hipStream_t st);
-int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
+int mp_norm_bwd(int f32, int rms, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
                 const void* dres, void* ds, void* dbranch, float* dw, float* dbias, float* cs_res, float* cs_ds,
                 int rows, int D, float p, uint64_t seed, float* part, hipStream_t st);
 int64_t mp_norm_bwd_part_elems(int rows, int D);
 int64_t mp_colsum_part_elems(int rows, int cols);
 int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss, int T, int V, int Vp, float grad_scale,
-                    int64_t ignore_index, int write_grad, hipStream_t st);
+                    int64_t ignore_index, int write_grad, int f32, hipStream_t st);
 int mp_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int T, int S, int D, int pos_offset,
-                 hipStream_t st);
+                 int f32, hipStream_t st);
 int mp_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int T, int S, int D, int pos_offset,
-                 hipStream_t st);
+                 int f32, hipStream_t st);
 int mp_sumsq(const float* g, int64_t n, float* out, hipStream_t st);
 int mp_gemm_f32(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int64_t lda,
                 int a_kc, int64_t ldb, int b_nc, int64_t ldc, float alpha, int accumulate, hipStream_t st);
+int mp_gemm_f32_ex(const float* A, const float* B, float* C, const float* bias, const float* R, float* X, int M, int N,
+                   int K, int64_t lda, int a_kc, int64_t ldb, int b_kc, int64_t ldc, int64_t ldr, int64_t ldx, int epi,
+                   float alpha, int accumulate, float p_drop, uint64_t seed, int force_ks, hipStream_t st);
 int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, float* sumsq, hipStream_t st);
 int mp_adamw(float* p, float* g, float* m, float* v, void* w16, int64_t n, int64_t n_decay, float lr, float b1,
              float b2, float eps, float wd, int step, const float* sumsq, float max_norm, float grad_scale,
@@ -30,7 +33,7 @@ int mp_cast_f32_bf16(const float* src, void* dst, int64_t n, hipStream_t st);
 int mp_act_fwd(const void* a, void* g, int64_t n, int act, float p, uint64_t seed, hipStream_t st);
 int mp_act_bwd(const void* dg, const void* a, void* da, float* dbias, int rows, int cols, int act, float p,
                uint64_t seed, float* part, hipStream_t st);
-int mp_colsum(const void* x, float* dbias, int rows, int cols, float* part, hipStream_t st);
+int mp_colsum(const void* x, float* dbias, int rows, int cols, float* part, int f32, hipStream_t st);
 int mp_swiglu_fwd(const void* gu, void* y, int T, int F, hipStream_t st);
 int mp_swiglu_bwd(const void* gu, const void* dy, void* dgu, int T, int F, hipStream_t st);
 int mp_rope(void* qkv, const float* cs, const float* sn, int T, int S, int H, int Hkv, int Dh, int pos_offset,
@@ -43,6 +46,15 @@ int mp_attn_bwd(const void* q, const void* k, const void* v, const void* o, cons
                 int64_t q_stride, int64_t k_stride, int64_t v_stride, int64_t o_stride, int64_t dq_stride,
                 int64_t dk_stride, int64_t dv_stride, int causal, float scale, float p_drop, uint64_t seed,
                 float* csq, float* csk, float* csv, hipStream_t st);
+int mp_attn_f32_fwd(const float* q, const float* k, const float* v, float* o, float* lse, int B, int Sq, int Sk, int H,
+                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int causal, float scale,
+                    float p_drop, uint64_t seed, hipStream_t st);
+int mp_attn_f32_bwd(const float* q, const float* k, const float* v, const float* o, const float* dout,
+                    const float* lse, float* delta, float* dq, float* dk, float* dv, int B, int Sq, int Sk, int H,
+                    int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs, int64_t dks,
+                    int64_t dvs, int causal, float scale, float p_drop, uint64_t seed, hipStream_t st);
+int mp_set_drop_step_attn_f32(uint64_t v, hipStream_t st);
+int mp_set_drop_step_gemm_f32(uint64_t v, hipStream_t st);
 int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st);
 int mp_transpose_batched(const void* src, void* dst, const int64_t* desc, const int* tile0, int n, int total_tiles,
                          hipStream_t st);
@@ -74,6 +86,14 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 void check(int rc, const char* what) { TORCH_CHECK(rc == 0, "mipipe kernel ", what, " failed with code ", rc); }
 
 const void* ptr_or_null(const c10::optional<torch::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+// storage dtype of the normalisation / loss / embedding kernels: bf16, or f32 (the
+// reference-precision path); returns 1 for f32
+int storage(const torch::Tensor& t, const char* name) {
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32, name,
+              " must be bf16 or f32, got ", t.scalar_type());
+  return t.scalar_type() == torch::kFloat32 ? 1 : 0;
+}
 void* mptr_or_null(const c10::optional<torch::Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
 
 void req(const torch::Tensor& t, torch::ScalarType dt, const char* name) {
@@ -85,15 +105,21 @@ void req(const torch::Tensor& t, torch::ScalarType dt, const char* name) {
 void norm_fwd(bool rms, torch::Tensor a, c10::optional<torch::Tensor> b, torch::Tensor w,
               c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> s_out, torch::Tensor y,
               c10::optional<torch::Tensor> mean, torch::Tensor rstd, double eps, double p, int64_t seed) {
-  req(a, torch::kBFloat16, "a");
-  req(y, torch::kBFloat16, "y");
+  const int f32 = storage(a, "a");
+  const auto dt = a.scalar_type();
+  req(a, dt, "a");
+  req(y, dt, "y");
+  req(w, dt, "w");
+  if (b.has_value()) req(*b, dt, "b");
+  if (bias.has_value()) req(*bias, dt, "bias");
+  if (s_out.has_value()) req(*s_out, dt, "s_out");
   req(rstd, torch::kFloat32, "rstd");
   const int D = a.size(-1);
   const int rows = a.numel() / D;
   TORCH_CHECK(!b.has_value() || (s_out.has_value() && b->numel() == a.numel()), "b needs s_out");
   TORCH_CHECK(rms || mean.has_value(), "LayerNorm needs mean");
   TORCH_CHECK(rstd.numel() >= rows && w.numel() == D, "bad norm shapes");
-  check(mp_norm_fwd(rms, a.data_ptr(), ptr_or_null(b), w.data_ptr(), ptr_or_null(bias), mptr_or_null(s_out),
+  check(mp_norm_fwd(f32, rms, a.data_ptr(), ptr_or_null(b), w.data_ptr(), ptr_or_null(bias), mptr_or_null(s_out),
                     y.data_ptr(), mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(), rows,
                     D, (float)eps, (float)p, (uint64_t)seed, cur_stream()),
         "norm_fwd");
@@ -105,9 +131,14 @@ int64_t norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c
               torch::Tensor rstd, c10::optional<torch::Tensor> dres, torch::Tensor ds,
               c10::optional<torch::Tensor> dbranch, torch::Tensor dw, c10::optional<torch::Tensor> dbias, double p,
               int64_t seed, c10::optional<torch::Tensor> cs_res, c10::optional<torch::Tensor> cs_ds) {
-  req(dy, torch::kBFloat16, "dy");
-  req(s, torch::kBFloat16, "s");
-  req(ds, torch::kBFloat16, "ds");
+  const int f32 = storage(dy, "dy");
+  const auto dt = dy.scalar_type();
+  req(dy, dt, "dy");
+  req(s, dt, "s");
+  req(ds, dt, "ds");
+  req(w, dt, "w");
+  if (dres.has_value()) req(*dres, dt, "dres");
+  if (dbranch.has_value()) req(*dbranch, dt, "dbranch");
   req(dw, torch::kFloat32, "dw");
   const int D = dy.size(-1);
   const int rows = dy.numel() / D;
@@ -116,7 +147,7 @@ int64_t norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c
   const int64_t pe = mp_norm_bwd_part_elems(rows, D);
   torch::Tensor part;
   if (pe > 0) part = torch::empty({pe}, dy.options().dtype(torch::kFloat32));
-  const int rc = mp_norm_bwd(rms, dy.data_ptr(), s.data_ptr(), w.data_ptr(),
+  const int rc = mp_norm_bwd(f32, rms, dy.data_ptr(), s.data_ptr(), w.data_ptr(),
                              mean.has_value() ? mean->data_ptr<float>() : nullptr, rstd.data_ptr<float>(),
                              ptr_or_null(dres), ds.data_ptr(), mptr_or_null(dbranch), dw.data_ptr<float>(),
                              dbias.has_value() ? dbias->data_ptr<float>() : nullptr,
@@ -130,26 +161,30 @@ int64_t norm_bwd(bool rms, torch::Tensor dy, torch::Tensor s, torch::Tensor w, c
 
 void xent(torch::Tensor logits, torch::Tensor target, torch::Tensor loss, int64_t V, double grad_scale,
           int64_t ignore_index, bool write_grad) {
-  req(logits, torch::kBFloat16, "logits");
+  const int f32 = storage(logits, "logits");
+  req(logits, logits.scalar_type(), "logits");
   req(target, torch::kInt64, "target");
   req(loss, torch::kFloat32, "loss");
   const int Vp = logits.size(-1);
   const int T = logits.numel() / Vp;
   TORCH_CHECK(target.numel() == T && loss.numel() == T, "bad xent shapes");
   check(mp_xent_fwd_bwd(logits.data_ptr(), target.data_ptr<int64_t>(), loss.data_ptr<float>(), T, V, Vp,
-                        (float)grad_scale, ignore_index, write_grad, cur_stream()),
+                        (float)grad_scale, ignore_index, write_grad, f32, cur_stream()),
         "xent");
 }
 
 void embed_fwd(torch::Tensor idx, torch::Tensor wte, c10::optional<torch::Tensor> wpe, torch::Tensor out, int64_t S,
                int64_t pos_offset) {
   req(idx, torch::kInt64, "idx");
-  req(out, torch::kBFloat16, "out");
+  const int f32 = storage(out, "out");
+  req(out, out.scalar_type(), "out");
+  req(wte, out.scalar_type(), "wte");
+  if (wpe.has_value()) req(*wpe, out.scalar_type(), "wpe");
   const int D = wte.size(1);
   const int T = idx.numel();
   TORCH_CHECK(out.numel() == (int64_t)T * D, "bad embed shapes");
   check(mp_embed_fwd(idx.data_ptr<int64_t>(), wte.data_ptr(), ptr_or_null(wpe), out.data_ptr(), T, S, D, pos_offset,
-                     cur_stream()),
+                     f32, cur_stream()),
         "embed_fwd");
 }
 
@@ -157,10 +192,13 @@ void embed_bwd(torch::Tensor idx, torch::Tensor dout, torch::Tensor dwte, c10::o
                int64_t S, int64_t pos_offset) {
   req(idx, torch::kInt64, "idx");
   req(dwte, torch::kFloat32, "dwte");
+  const int f32 = storage(dout, "dout");
+  req(dout, dout.scalar_type(), "dout");
   const int D = dwte.size(-1);
   const int T = idx.numel();
+  TORCH_CHECK(dout.numel() == (int64_t)T * D, "bad embed_bwd shapes");
   check(mp_embed_bwd(idx.data_ptr<int64_t>(), dout.data_ptr(), dwte.data_ptr<float>(),
-                     dwpe.has_value() ? dwpe->data_ptr<float>() : nullptr, T, S, D, pos_offset, cur_stream()),
+                     dwpe.has_value() ? dwpe->data_ptr<float>() : nullptr, T, S, D, pos_offset, f32, cur_stream()),
         "embed_bwd");
 }
 
@@ -224,7 +262,8 @@ void act_bwd(torch::Tensor dg, torch::Tensor a, torch::Tensor da, c10::optional<
 }
 
 void colsum(torch::Tensor x, torch::Tensor dbias) {
-  req(x, torch::kBFloat16, "x");
+  const int f32 = storage(x, "x");
+  req(x, x.scalar_type(), "x");
   req(dbias, torch::kFloat32, "dbias");
   const int cols = x.size(-1);
   const int rows = x.numel() / cols;
@@ -232,7 +271,7 @@ void colsum(torch::Tensor x, torch::Tensor dbias) {
   torch::Tensor part;
   if (pe > 0) part = torch::empty({pe}, x.options().dtype(torch::kFloat32));
   check(mp_colsum(x.data_ptr(), dbias.data_ptr<float>(), rows, cols, part.defined() ? part.data_ptr<float>() : nullptr,
-                  cur_stream()),
+                  f32, cur_stream()),
         "colsum");
 }
 
@@ -259,8 +298,19 @@ void attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o
               int64_t Sq, int64_t Sk, int64_t H, int64_t Hkv, int64_t D, bool causal, double scale, double p,
               int64_t seed) {
   req(lse, torch::kFloat32, "lse");
-  TORCH_CHECK(q.scalar_type() == torch::kBFloat16 && o.scalar_type() == torch::kBFloat16, "attn bf16 only");
   TORCH_CHECK(lse.numel() >= B * H * Sq, "lse too small");
+  TORCH_CHECK(q.stride(1) == 1 && k.stride(1) == 1 && v.stride(1) == 1 && o.stride(1) == 1, "attn: token-major rows");
+  if (q.scalar_type() == torch::kFloat32) {
+    // f32 flash attention (attention_f32.hip): the reference-precision path
+    TORCH_CHECK(k.scalar_type() == torch::kFloat32 && v.scalar_type() == torch::kFloat32 &&
+                    o.scalar_type() == torch::kFloat32, "attn f32: q/k/v/o all f32");
+    check(mp_attn_f32_fwd(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), o.data_ptr<float>(),
+                          lse.data_ptr<float>(), B, Sq, Sk, H, Hkv, D, q.stride(0), k.stride(0), v.stride(0),
+                          o.stride(0), causal, (float)scale, (float)p, (uint64_t)seed, cur_stream()),
+          "attn_f32_fwd");
+    return;
+  }
+  TORCH_CHECK(q.scalar_type() == torch::kBFloat16 && o.scalar_type() == torch::kBFloat16, "attn: bf16 or f32");
   check(mp_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), o.data_ptr(), lse.data_ptr<float>(), B, Sq, Sk, H, Hkv,
                     D, q.stride(0), k.stride(0), v.stride(0), o.stride(0), causal, (float)scale, (float)p,
                     (uint64_t)seed, cur_stream()),
@@ -272,6 +322,18 @@ void attn_bwd(torch::Tensor q, torch::Tensor k, torch::Tensor v, torch::Tensor o
               int64_t B, int64_t Sq, int64_t Sk, int64_t H, int64_t Hkv, int64_t D, bool causal,
               double scale, double p, int64_t seed, c10::optional<torch::Tensor> dbias) {
   TORCH_CHECK(o.stride(0) == dout.stride(0), "o and dout must share a row stride");
+  if (q.scalar_type() == torch::kFloat32) {
+    TORCH_CHECK(!dbias.has_value(), "attn_bwd f32: no fused bias sums");
+    for (const torch::Tensor* t : {&k, &v, &o, &dout, &dq, &dk, &dv})
+      TORCH_CHECK(t->scalar_type() == torch::kFloat32 && t->stride(1) == 1, "attn_bwd f32: f32 token-major rows");
+    check(mp_attn_f32_bwd(q.data_ptr<float>(), k.data_ptr<float>(), v.data_ptr<float>(), o.data_ptr<float>(),
+                          dout.data_ptr<float>(), lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr<float>(),
+                          dk.data_ptr<float>(), dv.data_ptr<float>(), B, Sq, Sk, H, Hkv, D, q.stride(0), k.stride(0),
+                          v.stride(0), o.stride(0), dq.stride(0), dk.stride(0), dv.stride(0), causal, (float)scale,
+                          (float)p, (uint64_t)seed, cur_stream()),
+          "attn_f32_bwd");
+    return;
+  }
   // dbias: f32 [(H + 2 Hkv) D] QKV bias gradient, accumulated by the kernels (q | k | v)
   float* cs = nullptr;
   if (dbias.has_value()) {
@@ -425,6 +487,8 @@ int64_t create_stream(int64_t device, int64_t priority) {
 void set_dropout_step(int64_t step) {
   const uint64_t v = (uint64_t)step;
   check(mp_set_drop_step_attn(v, cur_stream()), "set_drop_step");
+  check(mp_set_drop_step_attn_f32(v, cur_stream()), "set_drop_step");
+  check(mp_set_drop_step_gemm_f32(v, cur_stream()), "set_drop_step");
   check(mp_set_drop_step_elem(v, cur_stream()), "set_drop_step");
   check(mp_set_drop_step_norm(v, cur_stream()), "set_drop_step");
   check(mp_set_drop_step_gemm(v, cur_stream()), "set_drop_step");
@@ -485,6 +549,52 @@ int64_t gemm_f32(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optiona
   return 1;
 }
 
+// f32 GEMM with fused epilogues (gemm_f32.hip mp_gemm_f32_ex): C = epi(alpha * A @ B (+ C)).
+// A [M,K], B [K,N] 2-D views with either inner stride 1 (a transposed view of an [N,K]
+// weight is the K-contiguous B); C row-major.  epi: 0 none, 1 bias, 2 bias+ReLU(+dropout,
+// pre-activation -> X), 3 residual R, 4 bias+residual, 5 dReLU(R = pre-activation) x mask.
+// Returns 1 if done, 0 if the layout is not supported.
+int64_t gemm_f32_ex(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> bias,
+                    c10::optional<torch::Tensor> R, c10::optional<torch::Tensor> X, int64_t epi, double alpha,
+                    bool accumulate, double p_drop, int64_t seed, int64_t force_ks) {
+  TORCH_CHECK(A.scalar_type() == torch::kFloat32 && B.scalar_type() == torch::kFloat32 &&
+                  C.scalar_type() == torch::kFloat32, "gemm_f32_ex: f32 tensors");
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm_f32_ex: GPU tensors");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm_f32_ex: 2-D");
+  const int M = A.size(0), K = A.size(1), N = B.size(1);
+  TORCH_CHECK(B.size(0) == K && C.size(0) == M && C.size(1) == N, "gemm_f32_ex: shape mismatch");
+  if (C.stride(1) != 1) return 0;
+  int a_kc, b_kc;
+  int64_t lda, ldb;
+  if (A.stride(1) == 1) { a_kc = 1; lda = A.stride(0); }
+  else if (A.stride(0) == 1) { a_kc = 0; lda = A.stride(1); }
+  else return 0;
+  if (B.stride(0) == 1) { b_kc = 1; ldb = B.stride(1); }
+  else if (B.stride(1) == 1) { b_kc = 0; ldb = B.stride(0); }
+  else return 0;
+  const bool need_bias = epi == 1 || epi == 2 || epi == 4, need_r = epi >= 3, need_x = epi == 2;
+  TORCH_CHECK(!need_bias || (bias.has_value() && bias->is_contiguous() && bias->numel() == N), "gemm_f32_ex: bias [N]");
+  int64_t ldr = 0, ldx = 0;
+  if (need_r) {
+    TORCH_CHECK(R.has_value() && R->scalar_type() == torch::kFloat32 && R->dim() == 2 && R->stride(1) == 1 &&
+                    R->size(0) == M && R->size(1) == N, "gemm_f32_ex: R [M,N] f32 rows");
+    ldr = R->stride(0);
+  }
+  if (need_x) {
+    TORCH_CHECK(X.has_value() && X->scalar_type() == torch::kFloat32 && X->dim() == 2 && X->stride(1) == 1 &&
+                    X->size(0) == M && X->size(1) == N, "gemm_f32_ex: X [M,N] f32 rows");
+    ldx = X->stride(0);
+  }
+  const int rc = mp_gemm_f32_ex(A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(),
+                                need_bias ? bias->data_ptr<float>() : nullptr, need_r ? R->data_ptr<float>() : nullptr,
+                                need_x ? X->data_ptr<float>() : nullptr, M, N, K, lda, a_kc, ldb, b_kc, C.stride(0), ldr,
+                                ldx, (int)epi, (float)alpha, accumulate ? 1 : 0, (float)p_drop, (uint64_t)seed,
+                                (int)force_ks, cur_stream());
+  if (rc == -1) return 0;
+  check(rc, "gemm_f32_ex");
+  return 1;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   mipipe_comm::register_rccl(m);
   mipipe_runtime::register_runner(m);
@@ -496,6 +606,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_bwd", &embed_bwd);
   m.def("sumsq", &sumsq);
   m.def("gemm_f32", &gemm_f32);
+  m.def("gemm_f32_ex", &gemm_f32_ex, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
+        pybind11::arg("R"), pybind11::arg("X"), pybind11::arg("epi") = 0, pybind11::arg("alpha") = 1.0,
+        pybind11::arg("accumulate") = false, pybind11::arg("p_drop") = 0.0, pybind11::arg("seed") = 0,
+        pybind11::arg("force_ks") = 0);
   m.def("adamw", &adamw);
   m.def("cast_f32_bf16", &cast_f32_bf16);
   m.def("act_fwd", &act_fwd);

@@ -30,6 +30,61 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return __builtin_bit_cast(bf16_t, b);
 }
 
+// 8-element vector I/O for kernels templated on the storage type (bf16 or f32): the
+// reference-precision (f32) path runs the same normalisation / loss / embedding kernels as
+// the bf16 one.  Raw = the packed registers (16 B of bf16, 32 B of f32).
+template <typename T>
+struct IO8;
+template <>
+struct IO8<bf16_t> {
+  typedef u16x8 Raw;
+  static __device__ __forceinline__ Raw load(const bf16_t* p) { return *reinterpret_cast<const u16x8*>(p); }
+  static __device__ __forceinline__ void store(bf16_t* p, const Raw& r) { *reinterpret_cast<u16x8*>(p) = r; }
+  static __device__ __forceinline__ float get(const Raw& r, int e) { return __uint_as_float(((uint32_t)r[e]) << 16); }
+  static __device__ __forceinline__ void set(Raw& r, int e, float v) {
+    __bf16 b = (__bf16)v;
+    r[e] = __builtin_bit_cast(uint16_t, b);
+  }
+  static __device__ __forceinline__ float round(float v) { return get_round(v); }
+  static __device__ __forceinline__ float get_round(float v) {
+    __bf16 b = (__bf16)v;
+    return __uint_as_float(((uint32_t)__builtin_bit_cast(uint16_t, b)) << 16);
+  }
+  static __device__ __forceinline__ float load1(const bf16_t* p) { return __uint_as_float(((uint32_t)*p) << 16); }
+  static __device__ __forceinline__ void store1(bf16_t* p, float v) {
+    __bf16 b = (__bf16)v;
+    *p = __builtin_bit_cast(uint16_t, b);
+  }
+};
+struct f32x8_raw {
+  float4 a, b;
+  __device__ __forceinline__ float operator[](int e) const {
+    return e < 4 ? (e == 0 ? a.x : e == 1 ? a.y : e == 2 ? a.z : a.w) : (e == 4 ? b.x : e == 5 ? b.y : e == 6 ? b.z : b.w);
+  }
+};
+template <>
+struct IO8<float> {
+  typedef f32x8_raw Raw;
+  static __device__ __forceinline__ Raw load(const float* p) {
+    Raw r;
+    r.a = reinterpret_cast<const float4*>(p)[0];
+    r.b = reinterpret_cast<const float4*>(p)[1];
+    return r;
+  }
+  static __device__ __forceinline__ void store(float* p, const Raw& r) {
+    reinterpret_cast<float4*>(p)[0] = r.a;
+    reinterpret_cast<float4*>(p)[1] = r.b;
+  }
+  static __device__ __forceinline__ float get(const Raw& r, int e) { return r[e]; }
+  static __device__ __forceinline__ void set(Raw& r, int e, float v) {
+    float* f = e < 4 ? &r.a.x : &r.b.x;
+    f[e & 3] = v;
+  }
+  static __device__ __forceinline__ float round(float v) { return v; }
+  static __device__ __forceinline__ float load1(const float* p) { return *p; }
+  static __device__ __forceinline__ void store1(float* p, float v) { *p = v; }
+};
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -45,8 +45,8 @@ __global__ void __launch_bounds__(256) act_fwd_kernel(const bf16_t* __restrict__
 }
 
 // MODE 0: colsum(x) -> dbias ; MODE 1: da = dg*act'(a)*mask (written), dbias += colsum(da)
-template <int MODE>
-__global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ a,
+template <int MODE, typename T = bf16_t>
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, const bf16_t* __restrict__ a,
                                                      bf16_t* __restrict__ da, float* __restrict__ dbias, int rows,
                                                      int cols, int rows_per_block, int act, float p, uint64_t seed,
                                                      float* __restrict__ part) {
@@ -62,11 +62,12 @@ __global__ void __launch_bounds__(256) colsum_kernel(const bf16_t* __restrict__ 
   if (active) {
     for (int r = r0 + wv; r < r1; r += 4) {
       const size_t off = (size_t)r * cols + chunk * 8;
-      u16x8 xv = *reinterpret_cast<const u16x8*>(x + off);
-      if (MODE == 0) {
+      if constexpr (MODE == 0) {
+        const typename IO8<T>::Raw xv = IO8<T>::load(x + off);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) acc[e] += bf2f(xv[e]);
+        for (int e = 0; e < 8; ++e) acc[e] += IO8<T>::get(xv, e);
       } else {
+        u16x8 xv = *reinterpret_cast<const u16x8*>(x + off);
         u16x8 av = *reinterpret_cast<const u16x8*>(a + off);
         u16x8 o;
 #pragma unroll
@@ -327,13 +328,17 @@ extern "C" int mp_act_bwd(const void* dg, const void* a, void* da, float* dbias,
   return (int)hipGetLastError();
 }
 
-extern "C" int mp_colsum(const void* x, float* dbias, int rows, int cols, float* part, hipStream_t st) {
+extern "C" int mp_colsum(const void* x, float* dbias, int rows, int cols, float* part, int f32, hipStream_t st) {
   if (cols % 8) return -1;
   dim3 grid;
   int rpb;
   colsum_grid(rows, cols, grid, rpb);
   if (grid.x < kColpartMinBlocks) part = nullptr;
-  colsum_kernel<0><<<grid, 256, 0, st>>>((const bf16_t*)x, nullptr, nullptr, dbias, rows, cols, rpb, 0, 0.f, 0, part);
+  if (f32)
+    colsum_kernel<0, float><<<grid, 256, 0, st>>>((const float*)x, nullptr, nullptr, dbias, rows, cols, rpb, 0, 0.f, 0,
+                                                  part);
+  else
+    colsum_kernel<0><<<grid, 256, 0, st>>>((const bf16_t*)x, nullptr, nullptr, dbias, rows, cols, rpb, 0, 0.f, 0, part);
   if (part != nullptr) return mp_colpart_reduce(part, grid.x, 1, cols, dbias, nullptr, nullptr, nullptr, st);
   return (int)hipGetLastError();
 }

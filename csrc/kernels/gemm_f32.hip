@@ -1,191 +1,208 @@
 // f32 GEMM on the f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 products, f32
 // accumulate, 64 FLOP/clk/SIMD -- gfx950 has no xf32/TF32 fast path; cdna guide §3
-// "FP32-input MFMA").  SURVEY §7.1 gemm_f32.hip: the reference's own workload runs in
-// f32 (helper:36-46, no autocast), and this is the matmul of the reference-precision
-// path (ops.linear_f32 / ops.f32_linears(): every nn.Linear / MultiheadAttention
-// projection of an f32 module, forward and both backward GEMMs).
+// "FP32-input MFMA").  The matmul of the reference-precision path: the reference trains
+// its model in f32 (helper:36-46, no autocast), and NativeModel(dtype=float32) runs every
+// linear of it here, forward (bias / bias+ReLU+dropout / residual epilogues), dX (dReLU x
+// dropout-mask epilogue) and dW (f32 accumulate into the gradient arena).
 //
-//   C[M][N] (f32, row stride ldc) = alpha * A B (+ bias[N]) (+ C if accumulate)
+//   C[M][N] (f32, row stride ldc) = epi(alpha * A B (+ C if accumulate))
 //   A(m, k) = A[m * lda + k] (A_KC: K-contiguous) or A[k * lda + m] (M-contiguous)
-//   B(k, n) = B[k * ldb + n] (B_NC: N-contiguous) or B[n * ldb + k] (K-contiguous)
+//   B(k, n) = B[n * ldb + k] (B_KC: K-contiguous) or B[k * ldb + n] (N-contiguous)
 //
-// 128x128 (or, for grids of few tiles, 64x64) tiles, BK = 32, 256 threads (2 x 2 waves).  Both
-// operands are staged k-major in LDS ([k][m], [k][n], padded rows), so a 32x32x2 fragment
-// read (lane l: row/col base + l % 32, k = kk + l / 32) is one conflict-free ds_read_b32
-// per operand.  Global -> register prefetch of K-tile t+1 overlaps the MFMAs of tile t;
-// two LDS buffers, one barrier per K-tile.  Grids of few tiles split K (f32 atomics into C).
+// Design (f32 MFMA is 16x slower than bf16 per clock, so the operand traffic per MFMA is
+// tiny and the kernel is issue-bound on the matrix pipe):
+//  * no LDS staging: each lane loads its own fragments straight from L2 into registers.
+//    The k index an MFMA lane supplies is free to permute as long as A and B agree, so
+//    for 4 consecutive 32x32x2 MFMAs lane half hl supplies k = 8g + 4 hl + j (j = 0..3):
+//    a K-contiguous operand is ONE float4 load per lane per 4 MFMAs, an outer-contiguous
+//    one four dword loads, each coalesced over 32 lanes;
+//  * a 4-deep register ring of those fragments keeps ~1000 cycles of loads in flight;
+//  * one wave = one 32x32 output block; a 4-wave workgroup covers 4/KS blocks side by side
+//    and splits K over KS waves, reducing the partial sums through LDS -- deterministic
+//    split-K without slabs or atomics.  KS is chosen so the grid fills every SIMD
+//    (the reference's 1024-token GEMMs have 768-2304 blocks for 1024 SIMDs).
 #include "mp_common.h"
 
 using namespace mp;
 
 namespace gf32 {
 
-constexpr int BK = 32, NTH = 256, PAD = 4;
+enum Epi { E_NONE = 0, E_BIAS = 1, E_BIAS_RELU = 2, E_RES = 3, E_BIAS_RES = 4, E_DRELU = 5 };
 
-// T = 128: 2 x 2 waves of 64x64 (2 x 2 MFMA blocks each); T = 64: 2 x 2 waves of 32x32 (one
-// block each) -- 4x the workgroups for the short-token shapes without split-K atomics
-template <int T, bool A_KC, bool B_NC>
-__global__ void __launch_bounds__(NTH, 2) gemm_f32_kernel(const float* __restrict__ A, const float* __restrict__ B,
-                                                          float* __restrict__ C, const float* __restrict__ bias,
-                                                          int M, int N, int K, int64_t lda, int64_t ldb,
-                                                          int64_t ldc, float alpha, int accumulate) {
-  constexpr int BM = T, BN = T, LDA_S = BM + PAD, LDB_S = BN + PAD;
-  constexpr int WT = T / 2, NB = WT / 32;      // wave tile, 32x32 blocks per wave side
-  constexpr int U = BM * BK / 4 / NTH;          // float4 per thread per operand tile
-  constexpr int CPR = BK / 4;                   // float4 per k-row of a K-contiguous operand row
-  constexpr int RPR = BM / 4;                   // float4 per k-row of an outer-contiguous operand
-  __shared__ __attribute__((aligned(16))) float As[2][BK][LDA_S];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK][LDB_S];
-  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hl = lane >> 5;
-  const int wave = tid >> 6, wm = (wave >> 1) * WT, wn = (wave & 1) * WT;
-  const int gn = (N + BN - 1) / BN;
-  const int m0 = (blockIdx.x / gn) * BM, n0 = (blockIdx.x % gn) * BN;
-  // split-K (blockIdx.y of gridDim.y): K-tiles [kt0, kt0 + nk); partial sums are added to C
-  // with f32 atomics (C zeroed by the host unless accumulating), the bias by split 0
-  const int ktiles = (K + BK - 1) / BK;
-  const int nsplit = gridDim.y;
-  const int kt0 = (int)blockIdx.y * ktiles / nsplit;
-  const int nk = ((int)blockIdx.y + 1) * ktiles / nsplit - kt0;
+constexpr int NTH = 256, RING = 4;
 
-  float4 ra[U], rb[U];
-  auto load = [&](int kt) {
-    const int k0 = (kt0 + kt) * BK;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int idx = tid + NTH * u;
-      // A
-      if constexpr (A_KC) {         // rows m, CPR float4 along k
-        const int r = idx / CPR, k = k0 + (idx % CPR) * 4;
-        const int m = m0 + r;
-        ra[u] = (m < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)m * lda + k) : float4{0, 0, 0, 0};
-      } else {                      // k-rows, RPR float4 along m
-        const int kr = idx / RPR, m = m0 + (idx % RPR) * 4;
-        const int k = k0 + kr;
-        ra[u] = (m < M && k < K) ? *reinterpret_cast<const float4*>(A + (int64_t)k * lda + m) : float4{0, 0, 0, 0};
-      }
-      // B
-      if constexpr (B_NC) {         // k-rows, RPR float4 along n
-        const int kr = idx / RPR, n = n0 + (idx % RPR) * 4;
-        const int k = k0 + kr;
-        rb[u] = (n < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)k * ldb + n) : float4{0, 0, 0, 0};
-      } else {                      // rows n, CPR float4 along k
-        const int r = idx / CPR, k = k0 + (idx % CPR) * 4;
-        const int n = n0 + r;
-        rb[u] = (n < N && k < K) ? *reinterpret_cast<const float4*>(B + (int64_t)n * ldb + k) : float4{0, 0, 0, 0};
-      }
-    }
-  };
-  auto store = [&](int buf) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int idx = tid + NTH * u;
-      if constexpr (A_KC) {
-        const int r = idx / CPR, kq = (idx % CPR) * 4;
-        As[buf][kq + 0][r] = ra[u].x;
-        As[buf][kq + 1][r] = ra[u].y;
-        As[buf][kq + 2][r] = ra[u].z;
-        As[buf][kq + 3][r] = ra[u].w;
-      } else {
-        *reinterpret_cast<float4*>(&As[buf][idx / RPR][(idx % RPR) * 4]) = ra[u];
-      }
-      if constexpr (B_NC) {
-        *reinterpret_cast<float4*>(&Bs[buf][idx / RPR][(idx % RPR) * 4]) = rb[u];
-      } else {
-        const int r = idx / CPR, kq = (idx % CPR) * 4;
-        Bs[buf][kq + 0][r] = rb[u].x;
-        Bs[buf][kq + 1][r] = rb[u].y;
-        Bs[buf][kq + 2][r] = rb[u].z;
-        Bs[buf][kq + 3][r] = rb[u].w;
-      }
-    }
-  };
-
-  f32x16 acc[NB][NB];
-#pragma unroll
-  for (int i = 0; i < NB; ++i)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
-
-  load(0);
-  store(0);
-  __syncthreads();
-#pragma unroll 1
-  for (int t = 0; t < nk; ++t) {
-    const int buf = t & 1;
-    if (t + 1 < nk) load(t + 1);           // in flight during this tile's MFMAs
-#pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      float a[NB], b[NB];
-#pragma unroll
-      for (int i = 0; i < NB; ++i) a[i] = As[buf][kk + hl][wm + 32 * i + l32];
-#pragma unroll
-      for (int j = 0; j < NB; ++j) b[j] = Bs[buf][kk + hl][wn + 32 * j + l32];
-#pragma unroll
-      for (int i = 0; i < NB; ++i)
-#pragma unroll
-        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
-    }
-    if (t + 1 < nk) store(buf ^ 1);        // the other buffer: last read one barrier ago
-    __syncthreads();
+template <bool KC>
+__device__ __forceinline__ float4 frag(const float* __restrict__ P, int64_t ld, int outer, int k, int n_outer, int K) {
+  // 4 consecutive k (k, k+1, k+2, k+3) of row / column `outer`
+  if (outer >= n_outer || k >= K) return float4{0.f, 0.f, 0.f, 0.f};
+  if constexpr (KC) {
+    return *reinterpret_cast<const float4*>(P + (int64_t)outer * ld + k);
+  } else {
+    const float* p = P + (int64_t)k * ld + outer;
+    return float4{p[0], p[ld], p[2 * ld], p[3 * ld]};
   }
-  // acc[i][j] element r -> row wm + 32 i + (r & 3) + 8 (r >> 2) + 4 hl, column wn + 32 j + l32
+}
+
+template <int KS, bool A_KC, bool B_KC, int EPI>
+__global__ void __launch_bounds__(NTH) gemm_f32_kernel(const float* __restrict__ A, const float* __restrict__ B,
+                                                          float* __restrict__ C, const float* __restrict__ bias,
+                                                          const float* __restrict__ R, float* __restrict__ X, int M,
+                                                          int N, int K, int64_t lda, int64_t ldb, int64_t ldc,
+                                                          int64_t ldr, int64_t ldx, float alpha, int accumulate,
+                                                          float p_drop, uint64_t seed) {
+  constexpr int NBW = 4 / KS;                  // 32x32 blocks per workgroup (along n)
+  __shared__ float red[KS > 1 ? (KS - 1) * 16 * 64 : 1];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hl = lane >> 5;
+  const int wave = tid >> 6;
+  const int blk = wave % NBW, kp = wave / NBW;
+  const int gn = (N + 32 * NBW - 1) / (32 * NBW);
+  const int m0 = (blockIdx.x / gn) * 32, n0 = (blockIdx.x % gn) * 32 * NBW + 32 * blk;
+  // this wave's share of the 8-deep k groups
+  const int ng = (K + 7) / 8;
+  const int g0 = kp * ng / KS, g1 = (kp + 1) * ng / KS;
+  const int arow = m0 + l32, bcol = n0 + l32;
+
+  f32x16 acc = f32x16{};
+  float4 ra[RING], rb[RING];
 #pragma unroll
-  for (int i = 0; i < NB; ++i)
+  for (int u = 0; u < RING; ++u) {
+    const int k = (g0 + u) * 8 + 4 * hl;
+    if (g0 + u < g1) {
+      ra[u] = frag<A_KC>(A, lda, arow, k, M, K);
+      rb[u] = frag<B_KC>(B, ldb, bcol, k, N, K);
+    }
+  }
+  for (int g = g0; g < g1; g += RING) {
 #pragma unroll
-    for (int j = 0; j < NB; ++j) {
-      const int col = n0 + wn + 32 * j + l32;
-      if (col >= N) continue;
-      const float bv = (bias != nullptr && blockIdx.y == 0) ? bias[col] : 0.f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
-        if (row < M) {
-          float* cp = C + (int64_t)row * ldc + col;
-          const float v = alpha * acc[i][j][r] + bv;
-          if (nsplit > 1) atomicAdd(cp, v);
-          else *cp = accumulate ? *cp + v : v;
+    for (int u = 0; u < RING; ++u) {
+      if (g + u < g1) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].x, rb[u].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].y, rb[u].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].z, rb[u].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ra[u].w, rb[u].w, acc, 0, 0, 0);
+        const int gn_ = g + u + RING;
+        if (gn_ < g1) {
+          const int k = gn_ * 8 + 4 * hl;
+          ra[u] = frag<A_KC>(A, lda, arow, k, M, K);
+          rb[u] = frag<B_KC>(B, ldb, bcol, k, N, K);
         }
       }
     }
+  }
+  if constexpr (KS > 1) {
+    // partial sums of waves kp > 0 -> LDS; the kp == 0 wave of each block adds them
+    if (kp > 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(((kp - 1) * NBW + blk) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (kp > 0) return;
+#pragma unroll
+    for (int q = 1; q < KS; ++q)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += red[(((q - 1) * NBW + blk) * 16 + r) * 64 + lane];
+  }
+  // acc element r -> row m0 + (r & 3) + 8 (r >> 2) + 4 hl, column n0 + l32
+  const int col = n0 + l32;
+  if (col >= N) return;
+  float bv = 0.f;
+  if constexpr (EPI == E_BIAS || EPI == E_BIAS_RELU || EPI == E_BIAS_RES) bv = bias[col];
+  const float thr_p = p_drop;
+  uint32_t thr = 0;
+  float inv = 1.f;
+  if ((EPI == E_BIAS_RELU || EPI == E_DRELU) && thr_p > 0.f) {
+    seed = step_seed(seed);
+    thr = drop_thr(thr_p);
+    inv = 1.f / (1.f - thr_p);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int row = m0 + (r & 3) + 8 * (r >> 2) + 4 * hl;
+    if (row >= M) continue;
+    float* cp = C + (int64_t)row * ldc + col;
+    float v = alpha * acc[r];
+    if (accumulate) v += *cp;
+    if constexpr (EPI == E_BIAS || EPI == E_BIAS_RELU || EPI == E_BIAS_RES) v += bv;
+    if constexpr (EPI == E_BIAS_RELU) {
+      X[(int64_t)row * ldx + col] = v;            // pre-activation, for the backward
+      v = fmaxf(v, 0.f);
+      if (thr_p > 0.f) v *= hash_u32(seed, (uint64_t)row * N + col) >= thr ? inv : 0.f;
+    }
+    if constexpr (EPI == E_DRELU) {
+      const float pre = R[(int64_t)row * ldr + col];
+      v = pre > 0.f ? v : 0.f;
+      if (thr_p > 0.f) v *= hash_u32(seed, (uint64_t)row * N + col) >= thr ? inv : 0.f;
+    }
+    if constexpr (EPI == E_RES || EPI == E_BIAS_RES) v += R[(int64_t)row * ldr + col];
+    *cp = v;
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+static int launch(int ks, const float* A, const float* B, float* C, const float* bias, const float* R, float* X, int M,
+                  int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
+                  int accumulate, float p_drop, uint64_t seed, hipStream_t st) {
+  const int nbw = 4 / ks;
+  const int grid = ((M + 31) / 32) * ((N + 32 * nbw - 1) / (32 * nbw));
+#define MP_L(KS_)                                                                                             \
+  gemm_f32_kernel<KS_, A_KC, B_KC, EPI><<<grid, NTH, 0, st>>>(A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, \
+                                                              ldx, alpha, accumulate, p_drop, seed)
+  if (ks == 4) MP_L(4);
+  else if (ks == 2) MP_L(2);
+  else MP_L(1);
+#undef MP_L
+  return (int)hipGetLastError();
+}
+
+// K split per workgroup: enough waves for ~3 per SIMD (256 CUs x 4 SIMDs), while every
+// wave keeps at least 16 k-groups of work
+static int pick_ks(int M, int N, int K) {
+  const int64_t blocks = (int64_t)((M + 31) / 32) * ((N + 31) / 32);
+  const int ng = (K + 7) / 8;
+  int ks = 1;
+  while (ks < 4 && blocks * ks < 3072 && ng / (ks * 2) >= 16) ks *= 2;
+  return ks;
 }
 
 }  // namespace gf32
 
-// returns -1 if the operand layouts do not fit (inner stride != 1 / float4 alignment)
+// epi: 0 none, 1 bias, 2 bias+ReLU (+dropout p_drop; pre-activation -> X), 3 residual,
+// 4 bias+residual, 5 dReLU (pre-activation in R) x dropout mask.  Dropout element index =
+// row * N + col (identical in the forward and the backward).  Returns -1 if the operand
+// layouts do not fit (A/B inner stride != 1 / float4 alignment of a K-contiguous operand).
+extern "C" int mp_gemm_f32_ex(const float* A, const float* B, float* C, const float* bias, const float* R, float* X,
+                              int M, int N, int K, int64_t lda, int a_kc, int64_t ldb, int b_kc, int64_t ldc,
+                              int64_t ldr, int64_t ldx, int epi, float alpha, int accumulate, float p_drop,
+                              uint64_t seed, int force_ks, hipStream_t st) {
+  using namespace gf32;
+  if (M <= 0 || N <= 0) return 0;
+  if (K % 4) return -1;
+  if (a_kc && (lda % 4 || (reinterpret_cast<uintptr_t>(A) & 15))) return -1;
+  if (b_kc && (ldb % 4 || (reinterpret_cast<uintptr_t>(B) & 15))) return -1;
+  const int ks = force_ks > 0 ? force_ks : pick_ks(M, N, K);
+#define MP_E(E)                                                                                                   \
+  case E:                                                                                                         \
+    if (a_kc && b_kc) return launch<true, true, E>(ks, A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx,     \
+                                                   alpha, accumulate, p_drop, seed, st);                          \
+    if (a_kc) return launch<true, false, E>(ks, A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha,     \
+                                            accumulate, p_drop, seed, st);                                        \
+    if (b_kc) return launch<false, true, E>(ks, A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha,     \
+                                            accumulate, p_drop, seed, st);                                        \
+    return launch<false, false, E>(ks, A, B, C, bias, R, X, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, accumulate,  \
+                                   p_drop, seed, st);
+  switch (epi) {
+    MP_E(E_NONE) MP_E(E_BIAS) MP_E(E_BIAS_RELU) MP_E(E_RES) MP_E(E_BIAS_RES) MP_E(E_DRELU)
+    default: return -2;
+  }
+#undef MP_E
+}
+
+// the round-2 interface (ops.linear_f32 / f32_linears): B_NC = N-contiguous B
 extern "C" int mp_gemm_f32(const float* A, const float* B, float* C, const float* bias, int M, int N, int K,
                            int64_t lda, int a_kc, int64_t ldb, int b_nc, int64_t ldc, float alpha, int accumulate,
                            hipStream_t st) {
-  using namespace gf32;
-  if (M <= 0 || N <= 0) return 0;
-  if (K % 4 || M % 4 || N % 4 || lda % 4 || ldb % 4) return -1;
-  if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
-  // 128x128 tiles when they fill the chip four times over; else 64x64 tiles; split-K (f32
-  // atomics) while the grid is under 1.5 workgroups per CU and each split keeps >= 4 K-tiles
-  const int g128 = ((M + 127) / 128) * ((N + 127) / 128);
-  const bool big = g128 >= 1024;
-  const int T = big ? 128 : 64;
-  const int grid = ((M + T - 1) / T) * ((N + T - 1) / T);
-  const int ktiles = (K + BK - 1) / BK;
-  int split = 1;
-  while (split < 8 && grid * split < 384 && ktiles / (split * 2) >= 4) split *= 2;
-  if (split > 1 && !accumulate) {
-    const hipError_t e = hipMemset2DAsync(C, (size_t)ldc * sizeof(float), 0, (size_t)N * sizeof(float), M, st);
-    if (e != hipSuccess) return (int)e;
-  }
-#define MP_F32(TT, AK, BNC)                                                                                   \
-  gemm_f32_kernel<TT, AK, BNC><<<dim3(grid, split), NTH, 0, st>>>(A, B, C, bias, M, N, K, lda, ldb, ldc, alpha, \
-                                                                  accumulate)
-  if (big) {
-    if (a_kc && b_nc) MP_F32(128, true, true);
-    else if (a_kc) MP_F32(128, true, false);
-    else if (b_nc) MP_F32(128, false, true);
-    else MP_F32(128, false, false);
-  } else {
-    if (a_kc && b_nc) MP_F32(64, true, true);
-    else if (a_kc) MP_F32(64, true, false);
-    else if (b_nc) MP_F32(64, false, true);
-    else MP_F32(64, false, false);
-  }
-#undef MP_F32
-  return (int)hipGetLastError();
+  return mp_gemm_f32_ex(A, B, C, bias, nullptr, nullptr, M, N, K, lda, a_kc, ldb, b_nc ? 0 : 1, ldc, 0, 0,
+                        bias != nullptr ? gf32::E_BIAS : gf32::E_NONE, alpha, accumulate, 0.f, 0, 0, st);
 }
+
+MP_DROP_STEP_SETTER(mp_set_drop_step_gemm_f32)

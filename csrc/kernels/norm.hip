@@ -1,6 +1,8 @@
 // Fused residual-add (+dropout) + LayerNorm / RMSNorm, forward and backward.
 //
-// Forward (one wave per row, 16-byte bf16 vectors, row kept in registers):
+// Storage type T = bf16 (16-byte vectors) or f32 (the reference-precision path, 32-byte
+// vectors); statistics and accumulation always f32.
+// Forward (one wave per row, 8-element vectors, row kept in registers):
 //     s = a + dropout(b)        (optional; written out as the new residual stream)
 //     y = norm(s) * w (+ bias)  (LayerNorm or RMSNorm)
 //     mean / rstd saved in f32 for the backward
@@ -18,11 +20,13 @@
 
 using namespace mp;
 
-template <int MAXJ, bool RMS, bool HAS_B, bool HAS_BIAS>
+template <typename T, int MAXJ, bool RMS, bool HAS_B, bool HAS_BIAS>
 __global__ void __launch_bounds__(256) norm_fwd_kernel(
-    const bf16_t* __restrict__ a, const bf16_t* __restrict__ b, const bf16_t* __restrict__ w,
-    const bf16_t* __restrict__ bias, bf16_t* __restrict__ s_out, bf16_t* __restrict__ y, float* __restrict__ mean_out,
+    const T* __restrict__ a, const T* __restrict__ b, const T* __restrict__ w,
+    const T* __restrict__ bias, T* __restrict__ s_out, T* __restrict__ y, float* __restrict__ mean_out,
     float* __restrict__ rstd_out, int rows, int D, float eps, float p_drop, uint64_t seed) {
+  using IO = IO8<T>;
+  using Raw = typename IO::Raw;
   if (p_drop > 0.f) seed = step_seed(seed);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -35,25 +39,25 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(
   for (int j = 0; j < MAXJ; ++j) {
     const int c = lane + 64 * j;
     if (c < nchunk) {
-      u16x8 av = *reinterpret_cast<const u16x8*>(a + base + c * 8);
-      u16x8 bv;
-      if (HAS_B) bv = *reinterpret_cast<const u16x8*>(b + base + c * 8);
+      Raw av = IO::load(a + base + c * 8);
+      Raw bv;
+      if (HAS_B) bv = IO::load(b + base + c * 8);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float x = bf2f(av[e]);
+        float x = IO::get(av, e);
         if (HAS_B) {
-          float bb = bf2f(bv[e]);
+          float bb = IO::get(bv, e);
           if (p_drop > 0.f) bb *= dropout_scale(seed, base + c * 8 + e, p_drop);
-          x = bf2f(f2bf(x + bb));  // residual stream is stored in bf16: normalise what is stored
+          x = IO::round(x + bb);  // residual stream is stored in T: normalise what is stored
         }
         v[j][e] = x;
         sum += x;
       }
       if (HAS_B) {
-        u16x8 sv;
+        Raw sv;
 #pragma unroll
-        for (int e = 0; e < 8; ++e) sv[e] = f2bf(v[j][e]);
-        *reinterpret_cast<u16x8*>(s_out + base + c * 8) = sv;
+        for (int e = 0; e < 8; ++e) IO::set(sv, e, v[j][e]);
+        IO::store(s_out + base + c * 8, sv);
       }
     }
   }
@@ -80,17 +84,17 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(
   for (int j = 0; j < MAXJ; ++j) {
     const int c = lane + 64 * j;
     if (c < nchunk) {
-      u16x8 wv = *reinterpret_cast<const u16x8*>(w + c * 8);
-      u16x8 bv;
-      if (HAS_BIAS) bv = *reinterpret_cast<const u16x8*>(bias + c * 8);
-      u16x8 out;
+      Raw wv = IO::load(w + c * 8);
+      Raw bv;
+      if (HAS_BIAS) bv = IO::load(bias + c * 8);
+      Raw out;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        float o = (v[j][e] - mean) * rstd * bf2f(wv[e]);
-        if (HAS_BIAS) o += bf2f(bv[e]);
-        out[e] = f2bf(o);
+        float o = (v[j][e] - mean) * rstd * IO::get(wv, e);
+        if (HAS_BIAS) o += IO::get(bv, e);
+        IO::set(out, e, o);
       }
-      *reinterpret_cast<u16x8*>(y + base + c * 8) = out;
+      IO::store(y + base + c * 8, out);
     }
   }
 }
@@ -99,13 +103,15 @@ __global__ void __launch_bounds__(256) norm_fwd_kernel(
 // COLS: also accumulate column sums of dres and of ds -- or, with a dropped branch, of the
 // branch gradient (the bias grads of the projections that feed / consume this residual
 // point: GPT-2's FFN-out and attn-out biases, the reference block's out_proj / linear2)
-template <int MAXJ, bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BRANCH_GRAD, bool COLS>
+template <typename T, int MAXJ, bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BRANCH_GRAD, bool COLS>
 __global__ void __launch_bounds__(256) norm_bwd_kernel(
-    const bf16_t* __restrict__ dy, const bf16_t* __restrict__ s, const bf16_t* __restrict__ w,
-    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const bf16_t* __restrict__ dres,
-    bf16_t* __restrict__ ds_out, bf16_t* __restrict__ dbranch, float* __restrict__ dw, float* __restrict__ dbias,
+    const T* __restrict__ dy, const T* __restrict__ s, const T* __restrict__ w,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const T* __restrict__ dres,
+    T* __restrict__ ds_out, T* __restrict__ dbranch, float* __restrict__ dw, float* __restrict__ dbias,
     float* __restrict__ cs_res, float* __restrict__ cs_ds, int rows, int D, int rows_per_block, float p_drop,
     uint64_t seed, float* __restrict__ part) {
+  using IO = IO8<T>;
+  using Raw = typename IO::Raw;
   if (p_drop > 0.f) seed = step_seed(seed);
   __shared__ float red[4][2][MAXJ * 64 * 8 > 1024 ? 1024 : MAXJ * 64 * 8];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -129,25 +135,25 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
       wreg[j][e] = 0.f;
     }
     if (c < nchunk) {
-      u16x8 wvv = *reinterpret_cast<const u16x8*>(w + c * 8);
+      Raw wvv = IO::load(w + c * 8);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) wreg[j][e] = bf2f(wvv[e]);
+      for (int e = 0; e < 8; ++e) wreg[j][e] = IO::get(wvv, e);
     }
   }
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   // software pipeline over this wave's rows: row i+1's dy / s / dres loads are in flight
   // while row i is reduced and written (one row at a time exposed the load latency)
-  u16x8 pdv[MAXJ], psv[MAXJ], prv[HAS_DRES ? MAXJ : 1];
+  Raw pdv[MAXJ], psv[MAXJ], prv[HAS_DRES ? MAXJ : 1];
   auto fetch = [&](int row) {
     const size_t b = (size_t)row * D;
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
       const int c = lane + 64 * j;
       if (c < nchunk) {
-        pdv[j] = *reinterpret_cast<const u16x8*>(dy + b + c * 8);
-        psv[j] = *reinterpret_cast<const u16x8*>(s + b + c * 8);
-        if constexpr (HAS_DRES) prv[j] = *reinterpret_cast<const u16x8*>(dres + b + c * 8);
+        pdv[j] = IO::load(dy + b + c * 8);
+        psv[j] = IO::load(s + b + c * 8);
+        if constexpr (HAS_DRES) prv[j] = IO::load(dres + b + c * 8);
       }
     }
   };
@@ -156,7 +162,7 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
     const size_t base = (size_t)row * D;
     const float mean = RMS ? 0.f : mean_in[row];
     const float rstd = rstd_in[row];
-    u16x8 cdv[MAXJ], csv[MAXJ], crv[HAS_DRES ? MAXJ : 1];
+    Raw cdv[MAXJ], csv[MAXJ], crv[HAS_DRES ? MAXJ : 1];
 #pragma unroll
     for (int j = 0; j < MAXJ; ++j) {
       cdv[j] = pdv[j];
@@ -170,12 +176,12 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
     for (int j = 0; j < MAXJ; ++j) {
       const int c = lane + 64 * j;
       if (c < nchunk) {
-        u16x8 dv = cdv[j];
-        u16x8 sv = csv[j];
+        Raw dv = cdv[j];
+        Raw sv = csv[j];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float d = bf2f(dv[e]);
-          float x = (bf2f(sv[e]) - mean) * rstd;
+          float d = IO::get(dv, e);
+          float x = (IO::get(sv, e) - mean) * rstd;
           xh[j][e] = x;
           float gg = d * wreg[j][e];
           g[j][e] = gg;
@@ -192,23 +198,23 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
     for (int j = 0; j < MAXJ; ++j) {
       const int c = lane + 64 * j;
       if (c < nchunk) {
-        u16x8 rv;
+        Raw rv;
         if constexpr (HAS_DRES) rv = crv[j];
-        u16x8 out, bout;
+        Raw out, bout;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           float v = rstd * (g[j][e] - s1 - xh[j][e] * s2);
-          if (HAS_DRES) v += bf2f(rv[e]);
-          out[e] = f2bf(v);
-          if (BRANCH_GRAD) bout[e] = f2bf(v * dropout_scale(seed, base + c * 8 + e, p_drop));
+          if (HAS_DRES) v += IO::get(rv, e);
+          IO::set(out, e, v);
+          if (BRANCH_GRAD) IO::set(bout, e, v * dropout_scale(seed, base + c * 8 + e, p_drop));
           if constexpr (COLS) {
-            if constexpr (HAS_DRES) acc_r[j][e] += bf2f(rv[e]);
+            if constexpr (HAS_DRES) acc_r[j][e] += IO::get(rv, e);
             // with a dropped branch: the branch gradient's column sums (its projection's bias grad)
-            acc_s[j][e] += BRANCH_GRAD ? bf2f(bout[e]) : bf2f(out[e]);
+            acc_s[j][e] += BRANCH_GRAD ? IO::get(bout, e) : IO::get(out, e);
           }
         }
-        *reinterpret_cast<u16x8*>(ds_out + base + c * 8) = out;
-        if (BRANCH_GRAD) *reinterpret_cast<u16x8*>(dbranch + base + c * 8) = bout;
+        IO::store(ds_out + base + c * 8, out);
+        if (BRANCH_GRAD) IO::store(dbranch + base + c * 8, bout);
       }
     }
   }
@@ -260,15 +266,14 @@ __global__ void __launch_bounds__(256) norm_bwd_kernel(
 }
 
 // ------------------------------------------------------------------ launchers
-template <bool RMS, bool HAS_B, bool HAS_BIAS>
+template <typename T, bool RMS, bool HAS_B, bool HAS_BIAS>
 static void launch_fwd(int maxj, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
                        float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed, hipStream_t st) {
   dim3 grid((rows + 3) / 4), block(256);
 #define MP_FWD(J)                                                                                                  \
   case J:                                                                                                          \
-    norm_fwd_kernel<J, RMS, HAS_B, HAS_BIAS><<<grid, block, 0, st>>>(                                             \
-        (const bf16_t*)a, (const bf16_t*)b, (const bf16_t*)w, (const bf16_t*)bias, (bf16_t*)s_out, (bf16_t*)y, mean, \
-        rstd, rows, D, eps, p, seed);                                                                              \
+    norm_fwd_kernel<T, J, RMS, HAS_B, HAS_BIAS><<<grid, block, 0, st>>>(                                          \
+        (const T*)a, (const T*)b, (const T*)w, (const T*)bias, (T*)s_out, (T*)y, mean, rstd, rows, D, eps, p, seed); \
     break;
   switch (maxj) { MP_FWD(1) MP_FWD(2) MP_FWD(4) MP_FWD(8) MP_FWD(10) MP_FWD(16) }
 #undef MP_FWD
@@ -284,24 +289,32 @@ static int pick_j(int D) {
   return 16;
 }
 
-extern "C" int mp_norm_fwd(int rms, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
-                           float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed,
-                           hipStream_t st) {
+template <typename T>
+static int norm_fwd_t(int rms, const void* a, const void* b, const void* w, const void* bias, void* s_out, void* y,
+                      float* mean, float* rstd, int rows, int D, float eps, float p, uint64_t seed, hipStream_t st) {
   if (D % 8 != 0 || D > 16 * 512) return -1;
   const int J = pick_j(D);
   const bool hb = b != nullptr, hbias = bias != nullptr;
   if (rms) {
-    if (hb) hbias ? launch_fwd<true, true, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
-            : launch_fwd<true, true, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
-    else hbias ? launch_fwd<true, false, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
-               : launch_fwd<true, false, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+    if (hb) hbias ? launch_fwd<T, true, true, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+            : launch_fwd<T, true, true, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+    else hbias ? launch_fwd<T, true, false, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+               : launch_fwd<T, true, false, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
   } else {
-    if (hb) hbias ? launch_fwd<false, true, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
-            : launch_fwd<false, true, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
-    else hbias ? launch_fwd<false, false, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
-               : launch_fwd<false, false, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+    if (hb) hbias ? launch_fwd<T, false, true, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+            : launch_fwd<T, false, true, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+    else hbias ? launch_fwd<T, false, false, true>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st)
+               : launch_fwd<T, false, false, false>(J, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
   }
   return (int)hipGetLastError();
+}
+
+// f32 != 0: every tensor but mean / rstd in f32 (the reference-precision path), else bf16
+extern "C" int mp_norm_fwd(int f32, int rms, const void* a, const void* b, const void* w, const void* bias,
+                           void* s_out, void* y, float* mean, float* rstd, int rows, int D, float eps, float p,
+                           uint64_t seed, hipStream_t st) {
+  if (f32) return norm_fwd_t<float>(rms, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
+  return norm_fwd_t<bf16_t>(rms, a, b, w, bias, s_out, y, mean, rstd, rows, D, eps, p, seed, st);
 }
 
 extern "C" int mp_colpart_reduce(const float* part, int nblk, int nslot, int D, float* o0, float* o1, float* o2,
@@ -332,7 +345,7 @@ extern "C" int64_t mp_norm_bwd_part_elems(int rows, int D) {
   return g >= 256 ? (int64_t)g * 4 * D : 0;  // as kColpartMinBlocks (elementwise.hip)
 }
 
-template <bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG, bool COLS>
+template <typename T, bool RMS, bool HAS_DRES, bool HAS_BIAS, bool BG, bool COLS>
 static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, const float* mean, const float* rstd,
                        const void* dres, void* ds, void* dbr, float* dw, float* db, float* csr, float* css, int rows,
                        int D, float p, uint64_t seed, float* part, hipStream_t st) {
@@ -342,16 +355,17 @@ static void launch_bwd(int maxj, const void* dy, const void* s, const void* w, c
   if (grid.x < 256) part = nullptr;
 #define MP_BWD(J)                                                                                                   \
   case J:                                                                                                           \
-    norm_bwd_kernel<J, RMS, HAS_DRES, HAS_BIAS, BG, COLS><<<grid, block, 0, st>>>(                                  \
-        (const bf16_t*)dy, (const bf16_t*)s, (const bf16_t*)w, mean, rstd, (const bf16_t*)dres, (bf16_t*)ds,        \
-        (bf16_t*)dbr, dw, db, csr, css, rows, D, rpb, p, seed, part);                                               \
+    norm_bwd_kernel<T, J, RMS, HAS_DRES, HAS_BIAS, BG, COLS><<<grid, block, 0, st>>>(                               \
+        (const T*)dy, (const T*)s, (const T*)w, mean, rstd, (const T*)dres, (T*)ds, (T*)dbr, dw, db, csr, css, rows, \
+        D, rpb, p, seed, part);                                                                                     \
     break;
   switch (maxj) { MP_BWD(1) MP_BWD(2) MP_BWD(4) MP_BWD(8) MP_BWD(10) MP_BWD(16) }
 #undef MP_BWD
   if (part != nullptr) mp_colpart_reduce(part, grid.x, 4, D, dw, db, csr, css, st);
 }
 
-extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w, const float* mean,
+template <typename T>
+static int norm_bwd_t(int rms, const void* dy, const void* s, const void* w, const float* mean,
                            const float* rstd, const void* dres, void* ds, void* dbranch, float* dw, float* dbias,
                            float* cs_res, float* cs_ds, int rows, int D, float p, uint64_t seed, float* part,
                            hipStream_t st) {
@@ -364,7 +378,7 @@ extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w
     if (rms || J > 4 || (cs_res != nullptr && !hd)) return -3;
 #define MP_C(HD, HB, BG_)                                                                                        \
     if (hd == HD && hb == HB && bg == BG_) {                                                                       \
-      launch_bwd<false, HD, HB, BG_, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res, cs_ds,   \
+      launch_bwd<T, false, HD, HB, BG_, true>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res, cs_ds,   \
                                            rows, D, p, seed, part, st);                                            \
       return (int)hipGetLastError();                                                                               \
     }
@@ -374,7 +388,7 @@ extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w
   }
 #define MP_B(R, HD, HB, BG_)                                                                                   \
   if (rms == R && hd == HD && hb == HB && bg == BG_) {                                                          \
-    launch_bwd<R, HD, HB, BG_, false>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, nullptr, nullptr, \
+    launch_bwd<T, R, HD, HB, BG_, false>(J, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, nullptr, nullptr, \
                                       rows, D, p, seed, part, st);                                             \
     return (int)hipGetLastError();                                                                            \
   }
@@ -383,6 +397,17 @@ extern "C" int mp_norm_bwd(int rms, const void* dy, const void* s, const void* w
   MP_B(1, 0, 0, 0) MP_B(1, 0, 0, 1) MP_B(1, 1, 0, 0) MP_B(1, 1, 0, 1)
 #undef MP_B
   return -2;
+}
+
+extern "C" int mp_norm_bwd(int f32, int rms, const void* dy, const void* s, const void* w, const float* mean,
+                           const float* rstd, const void* dres, void* ds, void* dbranch, float* dw, float* dbias,
+                           float* cs_res, float* cs_ds, int rows, int D, float p, uint64_t seed, float* part,
+                           hipStream_t st) {
+  if (f32)
+    return norm_bwd_t<float>(rms, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res, cs_ds, rows, D, p, seed,
+                             part, st);
+  return norm_bwd_t<bf16_t>(rms, dy, s, w, mean, rstd, dres, ds, dbranch, dw, dbias, cs_res, cs_ds, rows, D, p, seed,
+                            part, st);
 }
 
 MP_DROP_STEP_SETTER(mp_set_drop_step_norm)

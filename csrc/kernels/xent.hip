@@ -12,23 +12,24 @@
 
 using namespace mp;
 
-template <bool WRITE_GRAD>
-__global__ void __launch_bounds__(256) xent_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ target,
+template <bool WRITE_GRAD, typename LT = bf16_t>
+__global__ void __launch_bounds__(256) xent_kernel(LT* __restrict__ logits, const int64_t* __restrict__ target,
                                                    float* __restrict__ loss, int T, int V, int Vp, float grad_scale,
                                                    int64_t ignore_index) {
+  using IO = IO8<LT>;
   __shared__ float red[8];
   const int row = blockIdx.x;
-  bf16_t* x = logits + (size_t)row * Vp;
+  LT* x = logits + (size_t)row * Vp;
   const int64_t tgt = target[row];
   const int nvec = V >> 3;  // full 8-wide chunks inside the real vocab
   float m = -INFINITY, s = 0.f;
   for (int c = threadIdx.x; c < nvec; c += 256) {
-    u16x8 v = *reinterpret_cast<const u16x8*>(x + c * 8);
+    const typename IO::Raw v = IO::load(x + c * 8);
     float f[8];
     float lm = m;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      f[e] = bf2f(v[e]);
+      f[e] = IO::get(v, e);
       lm = fmaxf(lm, f[e]);
     }
     s *= __expf(m - lm);
@@ -37,7 +38,7 @@ __global__ void __launch_bounds__(256) xent_kernel(bf16_t* __restrict__ logits, 
     m = lm;
   }
   for (int j = nvec * 8 + threadIdx.x; j < V; j += 256) {
-    float f = bf2f(x[j]);
+    float f = IO::load1(x + j);
     float lm = fmaxf(m, f);
     s = s * __expf(m - lm) + __expf(f - lm);
     m = lm;
@@ -48,22 +49,22 @@ __global__ void __launch_bounds__(256) xent_kernel(bf16_t* __restrict__ logits, 
   const float gs = block_sum<256>(s, red);
   const float lse = gm + __logf(gs);
   const bool valid = tgt != ignore_index && tgt >= 0 && tgt < V;
-  if (threadIdx.x == 0) loss[row] = valid ? lse - bf2f(x[tgt]) : 0.f;
+  if (threadIdx.x == 0) loss[row] = valid ? lse - IO::load1(x + tgt) : 0.f;
   if (!WRITE_GRAD) return;
   __syncthreads();  // everyone has read x[tgt] before it is overwritten
   const float sc = valid ? grad_scale : 0.f;
   const int nvec_p = Vp >> 3;
   for (int c = threadIdx.x; c < nvec_p; c += 256) {
-    u16x8 v = *reinterpret_cast<const u16x8*>(x + c * 8);
-    u16x8 o;
+    const typename IO::Raw v = IO::load(x + c * 8);
+    typename IO::Raw o;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int j = c * 8 + e;
       float g = 0.f;
-      if (j < V) g = (__expf(bf2f(v[e]) - lse) - (j == tgt ? 1.f : 0.f)) * sc;
-      o[e] = f2bf(g);
+      if (j < V) g = (__expf(IO::get(v, e) - lse) - (j == tgt ? 1.f : 0.f)) * sc;
+      IO::set(o, e, g);
     }
-    *reinterpret_cast<u16x8*>(x + c * 8) = o;
+    IO::store(x + c * 8, o);
   }
 }
 
@@ -163,8 +164,15 @@ __global__ void __launch_bounds__(NTH) xent_reg_kernel(bf16_t* __restrict__ logi
 }
 
 extern "C" int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss, int T, int V, int Vp,
-                               float grad_scale, int64_t ignore_index, int write_grad, hipStream_t st) {
+                               float grad_scale, int64_t ignore_index, int write_grad, int f32, hipStream_t st) {
   if (Vp % 8 != 0 || V > Vp) return -1;
+  if (f32) {   // f32 logits (reference-precision path): the streaming two-pass kernel
+    if (write_grad)
+      xent_kernel<true, float><<<T, 256, 0, st>>>((float*)logits, target, loss, T, V, Vp, grad_scale, ignore_index);
+    else
+      xent_kernel<false, float><<<T, 256, 0, st>>>((float*)logits, target, loss, T, V, Vp, grad_scale, ignore_index);
+    return (int)hipGetLastError();
+  }
   const int nchunk = Vp / 8;
 #define MP_XR(CPT)                                                                                               \
   if (nchunk <= 512 * CPT) {                                                                                     \

@@ -195,7 +195,8 @@ class PipelineTrainer:
         self.head_chunks = None
         # ZeRO-1 for the replicated head: master / Adam moments sharded over the pipeline
         # group (MIPIPE_HEAD_ZERO=0: fully replicated, gradient all-reduced)
-        self.head_zero = self.split_head and os.environ.get("MIPIPE_HEAD_ZERO", "1") != "0"
+        self.head_zero = (self.split_head and os.environ.get("MIPIPE_HEAD_ZERO", "1") != "0"
+                          and dtype != torch.float32)   # f32 arenas compute on their master
         if self.split_head:
             self.head = HeadShard(cfg, self.device, seed=seed, dtype=dtype, shards=pp if self.head_zero else 1)
             lc, head_units, ec = stage_cost_model(cfg, seq_len)

@@ -84,11 +84,15 @@ class ParamArena:
         # ``grad`` itself; the others are summed into it at the end of the step
         self.grad_lanes: List[torch.Tensor] = [self.grad]
         self.merged_sumsq: Optional[torch.Tensor] = None   # set by merge_lanes (GPU, lanes > 1)
-        self.w16 = torch.zeros(self.numel, dtype=dtype, device=self.device)
-        # transposed bf16 copies of the matrices used as B in dX = dY W (GPU only)
+        # the kernels' working copy of the weights: bf16, or -- f32 arenas (the reference-
+        # precision path) -- the f32 master itself (AdamW then writes no second copy)
+        self.w_is_master = dtype == torch.float32
+        self.w16 = self.master if self.w_is_master else torch.zeros(self.numel, dtype=dtype, device=self.device)
+        # transposed bf16 copies of the matrices used as B in dX = dY W (GPU bf16 only: the f32
+        # GEMM reads either operand layout)
         self.t_offsets: Dict[str, int] = {}
         toff = 0
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and dtype == torch.bfloat16:
             for s in specs:
                 if s.transpose and len(s.shape) == 2:
                     self.t_offsets[s.name] = toff
@@ -114,6 +118,9 @@ class ParamArena:
     def sync_w16(self) -> None:
         if self.shard is not None:
             raise RuntimeError("sync_w16 on a sharded arena: use `with arena.unsharded(): arena.sync_w16()`")
+        if self.w_is_master:
+            self.w16 = self.master       # (re-bound: load paths may have swapped the master tensor)
+            return
         ops.cast_f32_bf16(self.master, self.w16)
         self.refresh_transposes()
 
@@ -190,6 +197,8 @@ class ParamArena:
         (every rank computes with the whole matrix and accumulates its whole gradient)."""
         if self.shard is not None:
             raise RuntimeError("arena already sharded")
+        if self.w_is_master:
+            raise RuntimeError("ZeRO sharding of an f32 arena (its master is the working copy): not supported")
         self.master = self.master[lo:hi].clone()
         self.shard = (int(lo), int(hi), gather)
 
@@ -215,7 +224,7 @@ class ParamArena:
         """(master, grad, w16, n_decay) that the optimizer updates: the whole arena, or
         this rank's range of a sharded one (n_decay relative to it)."""
         if self.shard is None:
-            return self.master, self.grad, self.w16, self.n_decay
+            return self.master, self.grad, (None if self.w_is_master else self.w16), self.n_decay
         lo, hi, _ = self.shard
         return self.master, self.grad[lo:hi], self.w16[lo:hi], max(0, min(self.n_decay, hi) - lo)
 

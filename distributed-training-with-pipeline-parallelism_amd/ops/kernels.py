@@ -299,6 +299,19 @@ def _gemm(A, B, C, bias=None, residual=None, aux=None, transA=False, transB=Fals
     return C
 
 
+# f32 GEMM epilogues (csrc/kernels/gemm_f32.hip mp_gemm_f32_ex)
+F32_NONE, F32_BIAS, F32_BIAS_RELU, F32_RES, F32_BIAS_RES, F32_DRELU = range(6)
+
+
+def _gemm_f32(A, B, C, bias=None, R=None, X=None, epi=F32_NONE, alpha=1.0, accumulate=False, p_drop=0.0, seed=0):
+    """C = epi(alpha * A @ B (+ C)) on the f32 MFMA engine; A [M,K], B [K,N] views with a unit
+    stride in either dimension.  Raises if the layout is not supported (the f32 GPU path has
+    no ATen fallback: the reference-precision numbers must come from our kernels)."""
+    if not _ext().gemm_f32_ex(A, B, C, bias, R, X, int(epi), float(alpha), bool(accumulate), float(p_drop), int(seed), 0):
+        raise RuntimeError(f"gemm_f32_ex: unsupported layout A{tuple(A.shape)}/{A.stride()} B{tuple(B.shape)}/{B.stride()}")
+    return C
+
+
 def transpose(x: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """out = x^T for a 2-D bf16 matrix (row-contiguous views allowed)."""
     if out is None:
@@ -324,6 +337,19 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         out = torch.empty(T, N, device=x.device, dtype=x.dtype)
     if act != "none" and aux is None:
         aux = torch.empty(T, N, device=x.device, dtype=x.dtype)
+    if _gpu(x) and x.dtype == torch.float32:
+        # the reference-precision path: f32 MFMA GEMM with the same fused epilogues
+        if act not in ("none", "relu"):
+            raise ValueError("f32 GEMM epilogues: ReLU only")
+        if act == "relu":
+            if bias is None or residual is not None:
+                raise ValueError("activation epilogue needs a bias and no residual")
+            _gemm_f32(x, w.t(), out, bias=bias, X=aux, epi=F32_BIAS_RELU, p_drop=p_drop, seed=seed)
+        elif residual is not None:
+            _gemm_f32(x, w.t(), out, bias=bias, R=residual, epi=F32_BIAS_RES if bias is not None else F32_RES)
+        else:
+            _gemm_f32(x, w.t(), out, bias=bias, epi=F32_BIAS if bias is not None else F32_NONE)
+        return out, aux
     if _gpu(x):
         if act != "none":
             if bias is None or residual is not None:
@@ -396,6 +422,20 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
     K = w.shape[1]
     if out is None:
         out = torch.empty(T, K, device=dy.device, dtype=dy.dtype)
+    if _gpu(dy) and dy.dtype == torch.float32:
+        if act not in ("none", "relu"):
+            raise ValueError("f32 GEMM epilogues: dReLU only")
+        if act == "relu":
+            if residual is not None:
+                raise ValueError("dReLU epilogue takes no residual")
+            _gemm_f32(dy, w, out, R=act_input, epi=F32_DRELU, p_drop=p_drop, seed=seed)
+        elif residual is not None:
+            _gemm_f32(dy, w, out, R=residual, epi=F32_RES)
+        else:
+            _gemm_f32(dy, w, out)
+        if colsum is not None:
+            _ext().colsum(out, colsum)
+        return out
     if (_gpu(dy) and wt is not None and act == "none" and residual is None and colsum is None and
             _plain_pick(("dx", T, K, N), lambda: _plain_dx_hip(dy, wt, out), lambda: torch.mm(dy, w, out=out)) == "blas"):
         torch.mm(dy, w, out=out)
@@ -444,6 +484,8 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
 
 def linear_dw(dy: torch.Tensor, x: torch.Tensor, dw: torch.Tensor, alpha: float = 1.0):
     """dw (f32 [N,K]) += alpha * dy^T @ x   (dy [T,N], x [T,K])."""
+    if _gpu(dy) and dy.dtype == torch.float32:
+        return _gemm_f32(dy.t(), x, dw, alpha=alpha, accumulate=True)
     if _gpu(dy):
         if GEMM_BACKEND == "blas":
             dw.add_(torch.mm(dy.t(), x, out_dtype=torch.float32), alpha=alpha)
