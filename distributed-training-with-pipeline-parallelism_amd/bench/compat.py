@@ -17,10 +17,14 @@
   (SURVEY §2.8 item 11).
 
 ``engine='native'`` (the default whenever a GPU is present) runs the same reference
-architecture on the MI355X HIP path (explicit backward, hand-written kernels) and its
-last rank's ``step()`` returns the merged ``[B, S, vocab]`` logits like the reference's;
-``engine='torch'`` is the nn.Module / autograd path the reference uses (the CPU default).
-Every metrics dict also carries the measured and analytic pipeline bubble.
+architecture on the MI355X HIP path (explicit backward, hand-written kernels) at the
+reference's own precision (``precision='fp32'``: the f32 MFMA GEMM / f32 flash attention /
+f32 norm, CE and embedding kernels; ``'bf16'`` is the fast path), with per-microbatch HIP
+graphs, the native step tape and -- one process -- microbatch lanes; its last rank's
+``step()`` returns the merged ``[B, S, vocab]`` logits like the reference's (persistent
+graph outputs, so the tape replays that step too).  ``engine='torch'`` is the nn.Module /
+autograd path the reference uses (the CPU default).  Every metrics dict also carries the
+measured and analytic pipeline bubble, the precision and the execution path.
 """
 from __future__ import annotations
 
@@ -73,6 +77,14 @@ def run_train_iterations(schedule, x: torch.Tensor, y: torch.Tensor, rank: int, 
     elapsed = time.time() - start_t
     out = {"elapsed_time": elapsed, "throughput": total_toks / elapsed, "tokens_processed": total_toks}
     rt = getattr(schedule, "runtime", None)
+    if rt is not None:
+        st0 = next(iter(rt.stages.values()))
+        arena = getattr(st0, "arena", None)
+        out["precision"] = ("fp32" if arena.dtype == torch.float32 else "bf16") if arena is not None else \
+            str(next(st0.submod.parameters()).dtype).replace("torch.", "")
+        out["native_runner"] = rt.native_runner is not None
+        out["native_reason"] = rt.native_reason
+        out["lanes"] = rt.lanes
     if measure_bubble and rt is not None:
         from ..parallel.schedules import analytic_bubble
         if dist.is_initialized() and world_size > 1:
@@ -103,7 +115,8 @@ def stages_per_worker(schedule_type: str, n_layers: int, world_size: int) -> int
 
 def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_size, seq_length, num_iterations,
                    results_queue, num_microbatches: int = 4, device: Optional[str] = None, port: int = 29500,
-                   engine: str = "auto", dropout: float = 0.1, seed: Optional[int] = None):
+                   engine: str = "auto", dropout: float = 0.1, seed: Optional[int] = None, precision: str = "fp32",
+                   lanes: Optional[int] = None):
     """Reference worker (helper:150-235).  ``engine='auto'`` (default): the MI355X HIP path
     (``native``: hand-written kernels, explicit backward) when a GPU is present, the
     reference's nn.Module / autograd path (``torch``) on CPU.  ``MIPIPE_DIST_BACKEND=gloo``
@@ -142,7 +155,8 @@ def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_siz
             stage_idx = rank + world_size * i
             if engine == "native":
                 from ..models.stage import build_reference_stage
-                stages.append(build_reference_stage(args, stage_idx, num_stages, dev,
+                dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
+                stages.append(build_reference_stage(args, stage_idx, num_stages, dev, dtype=dt,
                                                     mbs=batch_size // num_microbatches, seq_len=seq_length))
             else:
                 model = Transformer(args)
@@ -152,6 +166,14 @@ def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_siz
         cls = get_schedule_class(schedule_type)
         schedule = cls(stages if spw > 1 or schedule_type == "Interleaved1F1B" else stages[0],
                        n_microbatches=num_microbatches, loss_fn=loss_fn)
+        if engine == "native" and use_gpu:
+            # one process: microbatch lanes as PipelineTrainer picks them (engine.auto_lanes)
+            from ..engine import auto_lanes
+            st = stages[0]
+            n = lanes if lanes is not None else auto_lanes(
+                st.cfg, world_size, spw, True, dev, num_microbatches, st.mbs * st.S, st.arena.numel,
+                st.model.layer_range[1] - st.model.layer_range[0])
+            schedule.runtime.set_lanes(n)
         metrics = run_train_iterations(schedule, x, y, rank, world_size, num_iterations, device=dev)
         if rank == world_size - 1:
             results_queue.put(metrics)

@@ -155,6 +155,26 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
                 recompute=bool(full > budget_frac * total))
 
 
+def auto_lanes(cfg: NativeConfig, pp: int, v: int, graphs: bool, device, m: int, tokens: int, params: int,
+               layers: int, recompute: bool = False) -> int:
+    """Microbatch lanes (PipelineRuntime.set_lanes) at PP = 1 with HIP graphs: up to 4 for
+    <= 4096-token microbatches, 2 above, if the extra per lane (an f32 gradient buffer + one
+    more microbatch's activation stash in flight) stays within 20 % of HBM.  Measured on one
+    MI355X (profiles/r2_lanes_ab.txt): reference model L8H8 (1024-token microbatches,
+    m = 4) 311K tok/s with 1 lane, 495K with 2, 456K with 3 (a lane on the compute
+    stream's hardware queue: fixed by the queue probe, parallel/runtime.py), 594K with 4;
+    GPT-2 small (16K-token microbatches, m = 2) 850K -> 888K with 2."""
+    device = torch.device(device)
+    if not (pp == 1 and v == 1 and graphs and device.type == "cuda" and m >= 2):
+        return 1
+    lanes = min(m, 4 if tokens <= 4096 else 2)
+    per_lane = 4.0 * params + layers * cfg.stash_bytes_per_layer(tokens, recompute=recompute)
+    hbm = torch.cuda.get_device_properties(device).total_memory
+    while lanes > 1 and (lanes - 1) * per_lane > 0.2 * hbm:
+        lanes -= 1
+    return lanes
+
+
 class PipelineTrainer:
     def __init__(self, cfg: NativeConfig, pp: int = 1, dp: int = 1, schedule: str = "1F1B",
                  n_microbatches: int = 8, mbs: int = 8, seq_len: int = 1024, v: Optional[int] = None,
@@ -303,23 +323,9 @@ class PipelineTrainer:
         return [w1, self.coll.all_reduce(part, "dp")]
 
     def _auto_lanes(self, pp: int, v: int, graphs: bool, m: int, mbs: int, seq_len: int) -> int:
-        """Lanes at PP = 1 with HIP graphs: up to 4 for <= 4096-token microbatches, 2 above,
-        if the extra per lane (an f32 gradient buffer + one more microbatch's activation
-        stash in flight) stays within 20 % of HBM.  Measured on one MI355X (profiles/
-        r2_lanes_ab.txt): reference model L8H8 (1024-token microbatches, m = 4) 311K tok/s
-        with 1 lane, 495K with 2, 456K with 3, 594K with 4; GPT-2 small (16K-token
-        microbatches, m = 2) 850K -> 888K with 2."""
-        if not (pp == 1 and v == 1 and graphs and self.device.type == "cuda" and m >= 2):
-            return 1
-        T = mbs * seq_len
-        lanes = min(m, 4 if T <= 4096 else 2)
-        params = sum(st.arena.numel for st in self.stages)
         layers = sum(r1 - r0 for r0, r1 in self.layer_ranges)
-        per_lane = 4.0 * params + layers * self.cfg.stash_bytes_per_layer(T, recompute=self.recompute)
-        hbm = torch.cuda.get_device_properties(self.device).total_memory
-        while lanes > 1 and (lanes - 1) * per_lane > 0.2 * hbm:
-            lanes -= 1
-        return lanes
+        return auto_lanes(self.cfg, pp, v, graphs, self.device, m, mbs * seq_len,
+                          sum(st.arena.numel for st in self.stages), layers, self.recompute)
 
     @property
     def is_first(self) -> bool:

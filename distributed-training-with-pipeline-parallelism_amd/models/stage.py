@@ -74,8 +74,8 @@ class NativeStage(StageBase):
     def forward_mb(self, mb, args, target, loss_fn, loss_scale):
         # compat step(return_outputs=True) on the last stage: also hand back the logits
         want_logits = self.is_last and not self.split_head and self.want_outputs and target is not None
-        if self._graphed() and not want_logits:
-            return self._forward_graphed(mb, args, target, loss_scale)
+        if self._graphed():
+            return self._forward_graphed(mb, args, target, loss_scale, want_logits)
         # on the GPU the step enters through the device counter (set_dropout_step), so
         # eager and graph-replayed steps draw identical masks; the CPU ops see the seed only
         ctx = MBContext(mb, _seed(self.seed, 0 if self.model.device.type == "cuda" else self.step_id, mb))
@@ -126,18 +126,26 @@ class NativeStage(StageBase):
         self.model.backward_weight(mb)
 
     # ------------------------------------------------------------------ HIP graphs
-    def _forward_graphed(self, mb, args, target, loss_scale):
+    def _forward_graphed(self, mb, args, target, loss_scale, want_logits=False):
         last_loss = self.is_last and not self.split_head and target is not None
         ins = (args[0],) + ((target,) if last_loss else ())
 
         def fn(ins):
             ctx = MBContext(mb, _seed(self.seed, 0, mb))
             out = self.model.forward(ins[0], ctx, self.mbs, self.S, target=ins[1] if last_loss else None,
-                                     loss_scale=loss_scale)
+                                     loss_scale=loss_scale, keep_logits=want_logits)
             self._gctx[mb] = ctx
+            if want_logits:
+                # the logits copy is a graph output: persistent, refreshed by every replay
+                return out, self._logits_view(ctx.misc.pop("logits_out"))
             return out
 
-        out = self.graphs.run(("F", mb), ins, fn, keep=lambda: self._gctx[mb])
+        # the logits-returning forward (compat step(return_outputs=True)) is its own graph
+        key = ("FL", mb) if want_logits else ("F", mb)
+        out = self.graphs.run(key, ins, fn, keep=lambda: self._gctx[mb])
+        if want_logits:
+            loss, logits = out
+            return (logits,), loss
         if self.is_last and not self.split_head:
             if not last_loss:
                 return (out,), None
@@ -184,16 +192,19 @@ class NativeStage(StageBase):
 
 
 def build_reference_stage(args, stage_index: int, num_stages: int, device, mbs: int = 8, seq_len: int = 128,
-                          seed: int = 0, dtype=None) -> NativeStage:
+                          seed: int = 0, dtype=torch.float32, graphs: Optional[bool] = None) -> NativeStage:
     """Reference architecture (helper:23-55) on the HIP path with the reference split rule.
-    ``dtype`` default: bf16 on GPUs (the HIP kernels), f32 on CPU (the reference's own
-    precision, so CPU runs are numerically the reference module)."""
-    if dtype is None:
-        dtype = torch.bfloat16 if torch.device(device).type == "cuda" else torch.float32
+    ``dtype``: the reference's own f32 by default -- on GPUs every op then runs on the f32
+    kernels (gemm_f32.hip, attention_f32.hip, the f32 norm / CE / embedding builds); bf16
+    is the fast path.  ``graphs`` (default: on with a GPU): per-microbatch HIP graphs, so
+    the schedule replays its steps from the native tape (parallel/native_runner.py),
+    including the last rank's merged-logits ``step()``."""
     cfg = NativeConfig.reference(n_layers=args.n_layers, n_heads=args.n_heads, dim=args.dim,
                                  vocab_size=args.vocab_size, dropout=getattr(args, "dropout", 0.1),
                                  dim_feedforward=getattr(args, "dim_feedforward", 2048))
     from .native import balanced_layer_ranges
     rng = balanced_layer_ranges(cfg, num_stages, reference_rule=True)[stage_index]
     model = NativeModel(cfg, stage_index, num_stages, device, layer_range=rng, seed=seed, dtype=dtype)
-    return NativeStage(model, mbs, seq_len)
+    if graphs is None:
+        graphs = torch.device(device).type == "cuda"
+    return NativeStage(model, mbs, seq_len, graphs=graphs)

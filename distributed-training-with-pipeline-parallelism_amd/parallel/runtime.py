@@ -171,6 +171,9 @@ class PipelineRuntime:
         self.native_enabled = os.environ.get("MIPIPE_NATIVE_RUNNER", "1") != "0"
         self.native_runner = None
         self.native_reason = "not recorded yet"
+        self._tapes: Dict[bool, tuple] = {}
+        self._tape_mode = False
+        self._native_outputs = None
         # distributed head: ``head_reduce()`` issues the reduction of the replicated head's
         # gradient (returns work handles); the program's REDUCE_HEAD action says when
         self.head_reduce: Optional[Callable[[], list]] = None
@@ -272,6 +275,7 @@ class PipelineRuntime:
             if hasattr(st, "model"):
                 st.model.wgrad_side = n == 1
         self.native_runner = None   # a recorded tape does not know about lanes
+        self._tapes.clear()
         return n
 
     def _own_queue(self, s: torch.cuda.Stream, others) -> bool:
@@ -464,8 +468,10 @@ class PipelineRuntime:
 
     # ------------------------------------------------------------------ native replay
     def _native_possible(self, return_outputs: bool) -> bool:
-        if not self.native_enabled or return_outputs or self.device.type != "cuda":
+        if not self.native_enabled or self.device.type != "cuda":
             return False
+        if return_outputs and not all(getattr(st, "records_own_collectives", False) for st in self.stages.values()):
+            return False     # autograd stages' outputs are not persistent graph buffers
         if self.deps is not None or self.ranges:
             return False
         if any(getattr(st, "graphs", None) is None for st in self.stages.values()):
@@ -508,7 +514,7 @@ class PipelineRuntime:
             targets = out
         return inputs, targets
 
-    def _step_native(self, inputs, targets, losses):
+    def _step_native(self, inputs, targets, losses, mode: bool = False):
         for st in self.stages.values():
             st.clear_runtime_states()
         self._steps += 1
@@ -533,7 +539,8 @@ class PipelineRuntime:
         if losses is not None and mb_losses:
             losses.extend(mb_losses[i] for i in sorted(mb_losses))
         self._last_losses = mb_losses
-        return None
+        # the last stage's per-microbatch outputs: graph buffers the replay just rewrote
+        return self._native_outputs if mode else None
 
     # ------------------------------------------------------------------ step
     def step(self, inputs: Optional[Sequence[Tuple[torch.Tensor, ...]]] = None,
@@ -541,9 +548,16 @@ class PipelineRuntime:
              return_outputs: bool = True) -> Optional[List[Tuple[torch.Tensor, ...]]]:
         if not self._initialized:
             self._initialize(inputs[0] if inputs is not None else None)
+        # one recorded tape per output mode: the compat last rank's step(return_outputs=True)
+        # replays a tape whose graphs also write the logits (persistent graph outputs)
+        mode = bool(return_outputs) and self.stages.get(self.num_stages - 1) is not None
+        if self._tape_mode != mode:
+            self._tapes[self._tape_mode] = (self.native_runner, self._native_outputs)
+            self.native_runner, self._native_outputs = self._tapes.get(mode, (None, None))
+            self._tape_mode = mode
         possible = self._native_possible(return_outputs)
         if possible and self.native_runner is not None:
-            return self._step_native(inputs, targets, losses)
+            return self._step_native(inputs, targets, losses, mode)
         rec = None
         if possible and self.profile:
             possible = False    # the recording step itself is not the profiled path
@@ -556,7 +570,12 @@ class PipelineRuntime:
         if rec is not None:
             if rec.valid:
                 self.native_runner = rec.runner
+                self._native_outputs = list(out) if (mode and out is not None) else None
                 self.native_reason = f"recorded {rec.runner.size} instructions"
+            elif "captured during the recording step" in rec.reason:
+                # a graph this step needed for the first time (e.g. the logits-returning
+                # forward of a new output mode): record again on the next step
+                self.native_reason = "re-recording: " + rec.reason
             else:
                 self.native_enabled = False
                 self.native_reason = "disabled: " + rec.reason

@@ -270,3 +270,18 @@ def test_trainer_f32_gpu_graphs_learns():
     assert all(math.isfinite(l) for l in losses)
     assert losses[-1] < losses[0]
     assert tr.runtime.native_runner is not None, tr.runtime.native_reason
+
+
+def test_compat_reference_api_runs_native_tape_fp32():
+    """The reference-compatible API (helper:98-235 signatures) on one GPU: build_reference_stage
+    in f32 with HIP graphs, Schedule1F1B, the last rank's step(target=y, losses=...) returning
+    merged logits -- and still replayed from the native tape."""
+    import multiprocessing as _mp
+    from mipipe.bench.compat import worker_process
+    q = _mp.get_context("spawn").Queue()
+    from mipipe.bench.compat import _free_port
+    worker_process(0, 1, 4, 8, "1F1B", 32, 128, 3, q, port=_free_port())
+    m = q.get(timeout=10)
+    assert "error" not in m, m
+    assert m["precision"] == "fp32" and m["native_runner"], m
+    assert m["throughput"] > 0 and m["lanes"] >= 1
