@@ -24,7 +24,9 @@ int mp_gemm_f32(const float* A, const float* B, float* C, const float* bias, int
                 int a_kc, int64_t ldb, int b_nc, int64_t ldc, float alpha, int accumulate, hipStream_t st);
 int mp_gemm_f32_ex(const float* A, const float* B, float* C, const float* bias, const float* R, float* X, int M, int N,
                    int K, int64_t lda, int a_kc, int64_t ldb, int b_kc, int64_t ldc, int64_t ldr, int64_t ldx, int epi,
-                   float alpha, int accumulate, float p_drop, uint64_t seed, int force_ks, hipStream_t st);
+                   float alpha, int accumulate, float p_drop, uint64_t seed, int force_split, float* ws,
+                   hipStream_t st);
+int64_t mp_gemm_f32_ws_elems(int M, int N, int K, int force_split);
 int mp_lane_merge(float* g0, float* g1, float* g2, float* g3, int64_t n, float* sumsq, hipStream_t st);
 int mp_adamw(float* p, float* g, float* m, float* v, void* w16, int64_t n, int64_t n_decay, float lr, float b1,
              float b2, float eps, float wd, int step, const float* sumsq, float max_norm, float grad_scale,
@@ -585,11 +587,15 @@ int64_t gemm_f32_ex(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::opti
                     X->size(0) == M && X->size(1) == N, "gemm_f32_ex: X [M,N] f32 rows");
     ldx = X->stride(0);
   }
+  // split-K slabs from the caching allocator (inside a graph capture: the graph's pool)
+  const int64_t ws_n = mp_gemm_f32_ws_elems(M, N, K, (int)force_ks);
+  torch::Tensor ws;
+  if (ws_n > 0) ws = torch::empty({ws_n}, A.options());
   const int rc = mp_gemm_f32_ex(A.data_ptr<float>(), B.data_ptr<float>(), C.data_ptr<float>(),
                                 need_bias ? bias->data_ptr<float>() : nullptr, need_r ? R->data_ptr<float>() : nullptr,
                                 need_x ? X->data_ptr<float>() : nullptr, M, N, K, lda, a_kc, ldb, b_kc, C.stride(0), ldr,
                                 ldx, (int)epi, (float)alpha, accumulate ? 1 : 0, (float)p_drop, (uint64_t)seed,
-                                (int)force_ks, cur_stream());
+                                (int)force_ks, ws_n > 0 ? ws.data_ptr<float>() : nullptr, cur_stream());
   if (rc == -1) return 0;
   check(rc, "gemm_f32_ex");
   return 1;

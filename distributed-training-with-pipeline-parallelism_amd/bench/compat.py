@@ -113,6 +113,33 @@ def stages_per_worker(schedule_type: str, n_layers: int, world_size: int) -> int
     return 2 if schedule_type == "Interleaved1F1B" and n_layers % (world_size * 2) == 0 else 1
 
 
+def native_reference_schedule(args: ModelArgs, schedule_type: str, rank: int, world_size: int, batch_size: int,
+                              seq_length: int, num_microbatches: int, device, precision: str = "fp32",
+                              lanes: Optional[int] = None):
+    """The reference's per-rank setup (helper:180-220: interleave rule, loop placement
+    ``stage = rank + world*i``, schedule factory) on the native path: build_reference_stage
+    per local stage (f32 or bf16 kernels, HIP graphs on GPUs), the schedule class, and --
+    with one process on a GPU -- microbatch lanes as PipelineTrainer picks them."""
+    from ..models.stage import build_reference_stage
+    dev = torch.device(device)
+    spw = stages_per_worker(schedule_type, args.n_layers, world_size)
+    num_stages = world_size * spw
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
+    stages = [build_reference_stage(args, rank + world_size * i, num_stages, dev, dtype=dt,
+                                    mbs=batch_size // num_microbatches, seq_len=seq_length) for i in range(spw)]
+    cls = get_schedule_class(schedule_type)
+    schedule = cls(stages if spw > 1 or schedule_type == "Interleaved1F1B" else stages[0],
+                   n_microbatches=num_microbatches, loss_fn=tokenwise_loss_fn(args.vocab_size))
+    if dev.type == "cuda":
+        from ..engine import auto_lanes
+        st = stages[0]
+        n = lanes if lanes is not None else auto_lanes(
+            st.cfg, world_size, spw, True, dev, num_microbatches, st.mbs * st.S, st.arena.numel,
+            st.model.layer_range[1] - st.model.layer_range[0])
+        schedule.runtime.set_lanes(n)
+    return schedule
+
+
 def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_size, seq_length, num_iterations,
                    results_queue, num_microbatches: int = 4, device: Optional[str] = None, port: int = 29500,
                    engine: str = "auto", dropout: float = 0.1, seed: Optional[int] = None, precision: str = "fp32",
@@ -149,31 +176,19 @@ def worker_process(rank, world_size, n_layers, n_heads, schedule_type, batch_siz
         args = ModelArgs(n_layers=n_layers, n_heads=n_heads, dropout=dropout)
         x = torch.randint(0, args.vocab_size, (batch_size, seq_length), dtype=torch.long, device=dev)
         y = torch.randint(0, args.vocab_size, (batch_size, seq_length), dtype=torch.long, device=dev)
-        loss_fn = tokenwise_loss_fn(args.vocab_size)
-        stages = []
-        for i in range(spw):
-            stage_idx = rank + world_size * i
-            if engine == "native":
-                from ..models.stage import build_reference_stage
-                dt = {"fp32": torch.float32, "bf16": torch.bfloat16}[precision]
-                stages.append(build_reference_stage(args, stage_idx, num_stages, dev, dtype=dt,
-                                                    mbs=batch_size // num_microbatches, seq_len=seq_length))
-            else:
+        if engine == "native":
+            schedule = native_reference_schedule(args, schedule_type, rank, world_size, batch_size, seq_length,
+                                                 num_microbatches, dev, precision=precision, lanes=lanes)
+        else:
+            stages = []
+            for i in range(spw):
                 model = Transformer(args)
-                st = manual_model_split(model, stage_idx, num_stages, dev)
+                st = manual_model_split(model, rank + world_size * i, num_stages, dev)
                 st.graphs = use_gpu   # the user module's fwd/bwd replayed as HIP graphs per microbatch slot
                 stages.append(st)
-        cls = get_schedule_class(schedule_type)
-        schedule = cls(stages if spw > 1 or schedule_type == "Interleaved1F1B" else stages[0],
-                       n_microbatches=num_microbatches, loss_fn=loss_fn)
-        if engine == "native" and use_gpu:
-            # one process: microbatch lanes as PipelineTrainer picks them (engine.auto_lanes)
-            from ..engine import auto_lanes
-            st = stages[0]
-            n = lanes if lanes is not None else auto_lanes(
-                st.cfg, world_size, spw, True, dev, num_microbatches, st.mbs * st.S, st.arena.numel,
-                st.model.layer_range[1] - st.model.layer_range[0])
-            schedule.runtime.set_lanes(n)
+            cls = get_schedule_class(schedule_type)
+            schedule = cls(stages if spw > 1 or schedule_type == "Interleaved1F1B" else stages[0],
+                           n_microbatches=num_microbatches, loss_fn=tokenwise_loss_fn(args.vocab_size))
         metrics = run_train_iterations(schedule, x, y, rank, world_size, num_iterations, device=dev)
         if rank == world_size - 1:
             results_queue.put(metrics)

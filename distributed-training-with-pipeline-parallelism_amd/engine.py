@@ -60,8 +60,9 @@ class FlatAdamW:
         self.max_norm = max_grad_norm
         self.pp_group = pp_group
         self.step_count = 0
-        self.m = [torch.zeros_like(a.master) for a in arenas]
-        self.v = [torch.zeros_like(a.master) for a in arenas]
+        # moments over what the optimizer updates (this rank's range of a sharded arena)
+        self.m = [torch.zeros_like(a.opt_views()[0]) for a in arenas]
+        self.v = [torch.zeros_like(a.opt_views()[0]) for a in arenas]
         dev = arenas[0].device if arenas else torch.device("cpu")
         self.sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
 
@@ -215,8 +216,7 @@ class PipelineTrainer:
         self.head_chunks = None
         # ZeRO-1 for the replicated head: master / Adam moments sharded over the pipeline
         # group (MIPIPE_HEAD_ZERO=0: fully replicated, gradient all-reduced)
-        self.head_zero = (self.split_head and os.environ.get("MIPIPE_HEAD_ZERO", "1") != "0"
-                          and dtype != torch.float32)   # f32 arenas compute on their master
+        self.head_zero = self.split_head and os.environ.get("MIPIPE_HEAD_ZERO", "1") != "0"
         if self.split_head:
             self.head = HeadShard(cfg, self.device, seed=seed, dtype=dtype, shards=pp if self.head_zero else 1)
             lc, head_units, ec = stage_cost_model(cfg, seq_len)

@@ -197,9 +197,11 @@ class ParamArena:
         (every rank computes with the whole matrix and accumulates its whole gradient)."""
         if self.shard is not None:
             raise RuntimeError("arena already sharded")
-        if self.w_is_master:
-            raise RuntimeError("ZeRO sharding of an f32 arena (its master is the working copy): not supported")
-        self.master = self.master[lo:hi].clone()
+        if not self.w_is_master:
+            self.master = self.master[lo:hi].clone()
+        # f32 arenas: the master is the working copy, so it stays full-size; the optimizer
+        # updates master[lo:hi] (opt_views) and the step's all-gather of w16 (= master)
+        # refreshes the rest -- only the Adam moments are sharded
         self.shard = (int(lo), int(hi), gather)
 
     @contextlib.contextmanager
@@ -210,6 +212,13 @@ class ParamArena:
             yield self
             return
         lo, hi, gather = self.shard
+        if self.w_is_master:      # full and current on every rank already
+            self.shard = None
+            try:
+                yield self
+            finally:
+                self.shard = (lo, hi, gather)
+            return
         shard = self.master
         self.master = gather(shard)
         self.shard = None
@@ -226,7 +235,10 @@ class ParamArena:
         if self.shard is None:
             return self.master, self.grad, (None if self.w_is_master else self.w16), self.n_decay
         lo, hi, _ = self.shard
-        return self.master, self.grad[lo:hi], self.w16[lo:hi], max(0, min(self.n_decay, hi) - lo)
+        nd = max(0, min(self.n_decay, hi) - lo)
+        if self.w_is_master:
+            return self.master[lo:hi], self.grad[lo:hi], None, nd
+        return self.master, self.grad[lo:hi], self.w16[lo:hi], nd
 
     def set_lanes(self, n: int) -> None:
         """Keep ``n`` gradient buffers: two microbatches of different lanes run their

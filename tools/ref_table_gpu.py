@@ -3,17 +3,19 @@
 BASELINE.md Table 1 times `Transformer(ModelArgs(dim=768, n_layers=L, n_heads=H,
 vocab_size=10000))` (post-LN decoder layers with cross-attention over h, ReLU FFN 2048,
 dropout 0.1) at batch 32 x seq 128, 4 microbatches, 2 warmup + 5 timed iterations, on a
-10-core CPU with gloo (helper:98-143, nb:679-732).  This runs the same model family
-(native explicit-backward twin, `NativeConfig.reference`) and the same batch / microbatch
-/ iteration counts through `PipelineTrainer` at PP=1 on one GPU, bf16, dropout on, and
-prints one JSON line per (L, H) next to the reference's best published run for that
-(L, H) (any P, any schedule) and its GPipe P=2 run.
+10-core CPU with gloo (helper:98-143, nb:679-732).  By default (--engine native) this runs the same
+model family (native explicit-backward twin, `NativeConfig.reference`) through the
+reference-compatible API -- Schedule1F1B.step, the reference's run_train_iterations loop,
+fwd+bwd only -- at the reference's precision (f32, on this framework's f32 kernels) at
+PP=1 on one GPU, dropout on, and prints one JSON line per (L, H) next to the reference's
+best published run for that (L, H) (any P, any schedule) and its GPipe P=2 run.
+--engine aten runs the reference's own nn.Module model through the same API (ATen f32);
+--engine trainer runs PipelineTrainer (bf16, AdamW included).
 
 Differences, stated: one GPU instead of P CPU processes (the multi-GPU rows need the
-8-GPU node the driver owns); each timed step here also runs the AdamW update (the
-reference times fwd+bwd only, §2.8-1); timing brackets all work with a device sync.
+8-GPU node the driver owns); timing brackets all work with a device sync.
 
-    python tools/ref_table_gpu.py [--json out.json]
+    python tools/ref_table_gpu.py [--precision fp32|bf16] [--engine native|aten|trainer] [--json out.json]
 """
 import argparse
 import json
@@ -48,12 +50,16 @@ def main():
     ap.add_argument("--f32-kernels", action="store_true",
                     help="fp32: the linears / attention projections on this framework's f32 MFMA GEMM (gemm_f32.hip) "
                          "instead of ATen (hipBLASLt); 2.3x slower today (profiles/r2_probes.md)")
-    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"],
-                    help="bf16: the native HIP path (PipelineTrainer, AdamW included); fp32: the reference's own "
-                         "nn.Module model in f32 on the GPU through the reference-compatible schedule API "
-                         "(fwd+bwd only, exactly the reference's timed loop)")
+    ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"])
+    ap.add_argument("--engine", default="native", choices=["native", "aten", "trainer"],
+                    help="native: the reference-compatible API (Schedule1F1B over build_reference_stage: this "
+                         "framework's kernels at --precision, HIP graphs + native tape + lanes), fwd+bwd only -- "
+                         "exactly the reference's timed loop; aten: the reference's own nn.Module model through the "
+                         "same API (ATen f32 compute); trainer: PipelineTrainer with the AdamW step (bf16)")
     a = ap.parse_args()
-    if a.precision == "fp32":
+    if a.engine == "native":
+        return main_native(a)
+    if a.engine == "aten":
         return main_fp32(a)
     import torch
     import mipipe  # noqa: F401
@@ -96,6 +102,51 @@ def main():
     summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
                          "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, bf16, AdamW step included, "
                          + ("eager" if a.no_graphs else "HIP graphs") + ", microbatch lanes (MIPIPE_LANES)",
+               "rows": out}
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(summary, f, indent=1)
+
+
+def main_native(a):
+    """The reference's workload through the reference-compatible API on this framework's
+    kernels: ``native_reference_schedule`` (build_reference_stage at --precision, HIP graphs,
+    lanes) + ``run_train_iterations`` (warmup + timed fwd+bwd steps, no optimizer: the
+    reference's own loop, helper:98-143) at PP = 1 on one GPU."""
+    import torch
+    import mipipe  # noqa: F401
+    from mipipe.bench.compat import native_reference_schedule, run_train_iterations
+    from mipipe.models.ref_transformer import ModelArgs
+
+    ref = reference_rows()
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    B, S, m = 32, 128, 4
+    out = []
+    for L in (4, 8, 12):
+        for H in (4, 8, 12):
+            torch.manual_seed(L * 100 + H)
+            args = ModelArgs(n_layers=L, n_heads=H)
+            sched = native_reference_schedule(args, "1F1B", 0, 1, B, S, m, dev, precision=a.precision)
+            x = torch.randint(0, args.vocab_size, (B, S), device=dev)
+            y = torch.randint(0, args.vocab_size, (B, S), device=dev)
+            met = run_train_iterations(sched, x, y, 0, 1, num_iterations=a.iters, warmup=a.warmup, device=dev,
+                                       measure_bubble=False)
+            mine = {k: v for k, v in ref.items() if k[0] == L and k[1] == H}
+            best_k = max(mine, key=mine.get)
+            row = {"L": L, "H": H, "tokens_per_s": round(met["throughput"], 1),
+                   "ms_per_iter": round(met["elapsed_time"] / a.iters * 1e3, 3), "precision": met["precision"],
+                   "native_runner": met["native_runner"], "lanes": met["lanes"], "ref_best_tok_s": mine[best_k],
+                   "ref_best_run": f"P={best_k[2]} {best_k[3]}", "ref_gpipe_p2_tok_s": mine.get((L, H, 2, "GPipe")),
+                   "x_vs_ref_best": round(met["throughput"] / mine[best_k], 1)}
+            out.append(row)
+            print(json.dumps(row), flush=True)
+            del sched
+            torch.cuda.empty_cache()
+    summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
+                         f"batch 32 x seq 128, m=4, PP=1 on 1 MI355X, {a.precision} on this framework's kernels, "
+                         "reference-compatible API (Schedule1F1B.step, merged logits returned), fwd+bwd only "
+                         "(no optimizer, helper:98-143), HIP graphs + native tape, microbatch lanes",
                "rows": out}
     if a.json:
         with open(a.json, "w") as f:
