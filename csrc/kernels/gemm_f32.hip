@@ -16,15 +16,16 @@
 //  * 64x64 tiles, 8 waves: waves 0-3 own the even 32-deep K-tiles, waves 4-7 the odd ones
 //    (a 32x32 block each, 2x2 over the tile), so two K-tiles are in flight per workgroup
 //    and a SIMD holds 2 waves of it; the two halves are summed through LDS at the end;
-//  * operands staged in LDS as K-contiguous rows [row][32 + 4]: one ds_read_b128 gives a
-//    lane 4 consecutive k, which feed 4 MFMAs -- the k index a lane supplies is permuted
-//    (lane half hl supplies k = 8g + 4 hl + j for MFMA j of group g; A and B agree), so the
-//    LDS reads are conflict-free b128 and there is no per-k shuffling;
-//  * a K-contiguous global operand is copied with float4 loads / ds_write_b128; an
-//    outer-contiguous one (dX's weight, both dW operands) is loaded as 4x4 blocks (4
-//    float4 along the outer dim) and transposed in registers on the way into LDS;
-//  * the next pair of K-tiles is loaded into registers during the current pair's MFMAs
-//    (two LDS buffers, one barrier per pair);
+//  * the k index an MFMA lane supplies is permuted (lane half hl supplies k = 8g + 4 hl + j
+//    for MFMA j of group g; A and B agree): a K-contiguous operand is staged in LDS as
+//    rows [row][32 + 4] and one conflict-free ds_read_b128 feeds 4 MFMAs; an outer-
+//    contiguous one (dX's weight, both dW operands) keeps its global layout in LDS,
+//    [k][64 + 8], read as 4 conflict-free ds_read_b32 -- both are filled by plain float4
+//    copies (ds_write_b128), no register transposes;
+//  * two register sets and two LDS buffers: pair kp + 2 loads while pair kp + 1 waits in
+//    registers and pair kp is in the MFMAs (one barrier per pair; a low-occupancy grid --
+//    one workgroup per CU -- still hides the HBM latency);
+//  * two accumulator chains per wave (even / odd 8-deep k groups), summed at the end;
 //  * few tiles (the reference's 1024-token GEMMs: 192-576 tiles for 256 CUs): split K over
 //    workgroups into f32 slabs, summed by one reduce + epilogue pass -- deterministic.
 #include "mp_common.h"
@@ -76,60 +77,97 @@ __device__ __forceinline__ void epi_store(const Args& p, int row, int col, float
   *cp = v;
 }
 
-// staging of one operand (rows `outer` 0..63 of the tile, k 0..63 of the K-tile pair) via
-// registers: K-contiguous -> 2 float4 per thread; outer-contiguous -> a 4x4 block (4
-// float4) for each thread of the operand's half of the workgroup (`half` 0: threads 0-255)
+// staging of one operand (rows `outer` 0..63 of the tile, k 0..63 of the K-tile pair):
+// 2 float4 per thread, copied as they are -- a K-contiguous operand into the row image
+// [kh][outer 64][KS] (fragment = one ds_read_b128 of 4 consecutive k), an outer-contiguous
+// one into the column image [kh][k 32][CS] (fragment = 4 ds_read_b32 of one column; CS =
+// 72: the two lane halves' rows k and k + 4 land 32 banks apart).  Both images are 2304
+// floats per K-tile.  Loads are unconditional from clamped addresses (no branch around a
+// load: hipcc would wait for it right there); k past K is zeroed when the registers are
+// written to LDS, rows past the edge only feed outputs that are never stored.
+constexpr int CS = BT + 8;
+static_assert(BK * CS == BT * KS, "row and column images must have the same size");
+
 template <bool KC>
 struct Stage {
-  float4 r[KC ? 2 : 4];
-  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int o0, int n_outer, int k0, int K,
-                                       int half) {
+  float4 r[2];
+  uint32_t ok;
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int o0, int n_outer, int k0, int K) {
     const int t = threadIdx.x;
-    if constexpr (KC) {
+    ok = 0;
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int f = t + NTH * u;                  // 1024 float4: [kh 2][row 64][c 8]
+    for (int u = 0; u < 2; ++u) {
+      const int f = t + NTH * u;
+      if constexpr (KC) {        // 1024 float4: [kh 2][row 64][c 8]
         const int kh = f >> 9, row = (f >> 3) & 63, c = f & 7;
-        const int o = o0 + row, k = k0 + 32 * kh + 4 * c;
-        r[u] = (o < n_outer && k < K) ? *reinterpret_cast<const float4*>(P + (int64_t)o * ld + k)
-                                      : float4{0.f, 0.f, 0.f, 0.f};
-      }
-    } else {
-      const int tt = t - 256 * half;
-      if (tt < 0 || tt >= 256) return;
-      const int kh = tt >> 7, q = tt & 127, kq = q >> 4, oq = q & 15;   // [kh 2][kq 8][oq 16]
-      const int o = o0 + 4 * oq;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int k = k0 + 32 * kh + 4 * kq + i;
-        r[i] = (o < n_outer && k < K) ? *reinterpret_cast<const float4*>(P + (int64_t)k * ld + o)
-                                      : float4{0.f, 0.f, 0.f, 0.f};
+        const int o = min(o0 + row, n_outer - 1), k = k0 + 32 * kh + 4 * c;
+        ok |= (k < K ? 1u : 0u) << u;
+        r[u] = *reinterpret_cast<const float4*>(P + (int64_t)o * ld + min(k, K - 4));
+      } else {                   // 1024 float4: [kh 2][k 32][c 16]
+        const int kh = f >> 9, kk = (f >> 4) & 31, c = f & 15;
+        const int o = min(o0 + 4 * c, n_outer - 4), k = k0 + 32 * kh + kk;
+        ok |= (k < K ? 1u : 0u) << u;
+        r[u] = *reinterpret_cast<const float4*>(P + (int64_t)min(k, K - 1) * ld + o);
       }
     }
   }
-  // -> LDS image [kh][row][KS] (k-contiguous rows)
-  __device__ __forceinline__ void store(float* __restrict__ s, int half) const {
+  __device__ __forceinline__ void store(float* __restrict__ s) const {
     const int t = threadIdx.x;
-    if constexpr (KC) {
+    const float4 z = float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int f = t + NTH * u;
+    for (int u = 0; u < 2; ++u) {
+      const int f = t + NTH * u;
+      const float4 v = (ok >> u) & 1u ? r[u] : z;
+      if constexpr (KC) {
         const int kh = f >> 9, row = (f >> 3) & 63, c = f & 7;
-        *reinterpret_cast<float4*>(s + (kh * BT + row) * KS + 4 * c) = r[u];
+        *reinterpret_cast<float4*>(s + (kh * BT + row) * KS + 4 * c) = v;
+      } else {
+        const int kh = f >> 9, kk = (f >> 4) & 31, c = f & 15;
+        *reinterpret_cast<float4*>(s + (kh * BK + kk) * CS + 4 * c) = v;
       }
+    }
+  }
+  // the lane's 4 operand values (k = 8g + 4hl + j, j = 0..3) of outer index w0 + l32
+  static __device__ __forceinline__ float4 frag(const float* __restrict__ s, int w0, int g, int l32, int hl) {
+    if constexpr (KC) {
+      return *reinterpret_cast<const float4*>(s + (w0 + l32) * KS + 8 * g + 4 * hl);
     } else {
-      const int tt = t - 256 * half;
-      if (tt < 0 || tt >= 256) return;
-      const int kh = tt >> 7, q = tt & 127, kq = q >> 4, oq = q & 15;
-      // row 4 oq + j gets k 4 kq .. 4 kq + 3: column j of the 4x4 block
-      float* d = s + (kh * BT + 4 * oq) * KS + 4 * kq;
-      *reinterpret_cast<float4*>(d) = float4{r[0].x, r[1].x, r[2].x, r[3].x};
-      *reinterpret_cast<float4*>(d + KS) = float4{r[0].y, r[1].y, r[2].y, r[3].y};
-      *reinterpret_cast<float4*>(d + 2 * KS) = float4{r[0].z, r[1].z, r[2].z, r[3].z};
-      *reinterpret_cast<float4*>(d + 3 * KS) = float4{r[0].w, r[1].w, r[2].w, r[3].w};
+      const float* c = s + (8 * g + 4 * hl) * CS + w0 + l32;
+      return float4{c[0], c[CS], c[2 * CS], c[3 * CS]};
     }
   }
 };
+
+// one K-tile pair: (issue the loads of pair kp + 2 into the register set that held pair
+// kp) -> MFMAs on LDS buffer `buf` -> (registers of pair kp + 1 -> the other buffer) -> barrier
+template <bool A_KC, bool B_KC>
+__device__ __forceinline__ void pair_step(const Args& p, float* smem, int buf, int kp, int kp1, int m0, int n0,
+                                          int kh, int wm, int wn, int l32, int hl, f32x16& acc0, f32x16& acc1,
+                                          Stage<A_KC>& ld_a, Stage<B_KC>& ld_b, const Stage<A_KC>& st_a,
+                                          const Stage<B_KC>& st_b) {
+  // unconditional (past the end: clamped addresses, never stored) -- a load inside a branch
+  // leaves hipcc unsure how many are in flight, and it then waits for all of them
+  ld_a.load(p.A, p.lda, m0, p.M, (kp + 2) * 2 * BK, p.K);
+  ld_b.load(p.B, p.ldb, n0, p.N, (kp + 2) * 2 * BK, p.K);
+  const float* As = smem + buf * 2 * OPS + kh * BT * KS;
+  const float* Bs = smem + buf * 2 * OPS + OPS + kh * BT * KS;
+#pragma unroll
+  for (int g = 0; g < BK / 8; ++g) {
+    const float4 a = Stage<A_KC>::frag(As, wm, g, l32, hl);
+    const float4 b = Stage<B_KC>::frag(Bs, wn, g, l32, hl);
+    f32x16& acc = (g & 1) ? acc1 : acc0;     // two independent chains
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
+  }
+  if (kp + 1 < kp1) {
+    float* nb = smem + (buf ^ 1) * 2 * OPS;     // last read before the previous barrier
+    st_a.store(nb);
+    st_b.store(nb + OPS);
+  }
+  __syncthreads();
+}
 
 template <bool A_KC, bool B_KC, int EPI>
 __global__ void __launch_bounds__(NTH, 2) gemm_f32_kernel(Args p) {
@@ -144,41 +182,28 @@ __global__ void __launch_bounds__(NTH, 2) gemm_f32_kernel(Args p) {
   const int nsplit = gridDim.y;
   const int kp0 = (int)blockIdx.y * npairs / nsplit, kp1 = ((int)blockIdx.y + 1) * npairs / nsplit;
 
-  Stage<A_KC> sa;
-  Stage<B_KC> sb;
-  f32x16 acc = f32x16{};
+  // two register sets: pair kp + 2 is loading while pair kp + 1 waits in registers and
+  // pair kp is in the MFMAs
+  Stage<A_KC> sa0, sa1;
+  Stage<B_KC> sb0, sb1;
+  f32x16 acc0 = f32x16{}, acc1 = f32x16{};
   if (kp0 < kp1) {
-    sa.load(p.A, p.lda, m0, p.M, kp0 * 2 * BK, p.K, 0);
-    sb.load(p.B, p.ldb, n0, p.N, kp0 * 2 * BK, p.K, 1);
-    sa.store(smem, 0);
-    sb.store(smem + OPS, 1);
+    sa0.load(p.A, p.lda, m0, p.M, kp0 * 2 * BK, p.K);
+    sb0.load(p.B, p.ldb, n0, p.N, kp0 * 2 * BK, p.K);
+    sa1.load(p.A, p.lda, m0, p.M, (kp0 + 1) * 2 * BK, p.K);
+    sb1.load(p.B, p.ldb, n0, p.N, (kp0 + 1) * 2 * BK, p.K);
+    sa0.store(smem);
+    sb0.store(smem + OPS);
   }
   __syncthreads();
-  for (int kp = kp0; kp < kp1; ++kp) {
-    const int buf = (kp - kp0) & 1;
-    const float* As = smem + buf * 2 * OPS + kh * BT * KS;
-    const float* Bs = smem + buf * 2 * OPS + OPS + kh * BT * KS;
-    const bool more = kp + 1 < kp1;
-    if (more) {   // the next pair in flight during this pair's MFMAs
-      sa.load(p.A, p.lda, m0, p.M, (kp + 1) * 2 * BK, p.K, 0);
-      sb.load(p.B, p.ldb, n0, p.N, (kp + 1) * 2 * BK, p.K, 1);
-    }
-#pragma unroll
-    for (int g = 0; g < BK / 8; ++g) {
-      const float4 a = *reinterpret_cast<const float4*>(As + (wm + l32) * KS + 8 * g + 4 * hl);
-      const float4 b = *reinterpret_cast<const float4*>(Bs + (wn + l32) * KS + 8 * g + 4 * hl);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, acc, 0, 0, 0);
-    }
-    if (more) {
-      float* nb = smem + (buf ^ 1) * 2 * OPS;     // last read before the previous barrier
-      sa.store(nb, 0);
-      sb.store(nb + OPS, 1);
-    }
-    __syncthreads();
+  int kp = kp0;
+  for (; kp + 1 < kp1; kp += 2) {
+    pair_step<A_KC, B_KC>(p, smem, 0, kp, kp1, m0, n0, kh, wm, wn, l32, hl, acc0, acc1, sa0, sb0, sa1, sb1);
+    pair_step<A_KC, B_KC>(p, smem, 1, kp + 1, kp1, m0, n0, kh, wm, wn, l32, hl, acc0, acc1, sa1, sb1, sa0, sb0);
   }
+  if (kp < kp1)   // odd count: the last pair
+    pair_step<A_KC, B_KC>(p, smem, 0, kp, kp1, m0, n0, kh, wm, wn, l32, hl, acc0, acc1, sa0, sb0, sa1, sb1);
+  f32x16 acc = acc0 + acc1;
   // the odd-K-tile waves hand their sums to the even ones through LDS
   float* red = smem;
   if (kh == 1) {
@@ -256,21 +281,22 @@ static int launch(Args p, int split, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// split-K factor: fill the 512 workgroup slots (256 CUs x 2) in as few, as full rounds as
-// possible, each split keeping at least 4 K-tile pairs (256 k)
+// split-K factor: minimise the busiest CU's work, in K-tile-pair units: the workgroups it
+// runs (tiles x s over 256 CUs) x (its pairs + ~3 pairs of prologue / epilogue latency),
+// plus ~1 for the slab pass.  Fitted to the measured s = 1..8 sweep of the reference's
+// GEMMs (profiles/r3_f32_gemm_sweep.json): e.g. dX of the LM head (192 tiles, 157 pairs)
+// -> 4, the forward out_proj (192 tiles, 12 pairs) -> 1.
 static int pick_split(int M, int N, int K) {
   const int tiles = ((M + BT - 1) / BT) * ((N + BT - 1) / BT);
   const int npairs = (K + 2 * BK - 1) / (2 * BK);
   int best = 1;
-  double best_eff = 0.0;
+  double best_cost = 1e30;
   for (int s = 1; s <= 8; ++s) {
-    if (s > 1 && npairs / s < 4) break;
-    const int wg = tiles * s;
-    const int rounds = (wg + 511) / 512;
-    // useful fraction of the slots, with a small price per split for the slab pass
-    const double eff = (double)wg / (rounds * 512.0) / (1.0 + 0.04 * (s - 1));
-    if (eff > best_eff + 1e-9) {
-      best_eff = eff;
+    if (s > 1 && npairs < 2 * s) break;
+    const double rounds = (double)((tiles * s + 255) / 256);
+    const double cost = rounds * ((double)npairs / s + 3.0) + (s > 1 ? 1.0 : 0.0);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
       best = s;
     }
   }
