@@ -131,7 +131,7 @@ def max_inflight_microbatches(order, stages) -> int:
 
 
 def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, seq_len: int, device,
-                   head_tokens: int = 0, budget_frac: float = 0.85) -> dict:
+                   head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1) -> dict:
     """HBM plan of one pipeline rank and the recompute decision of ``recompute="auto"``:
     recompute only if the activation stash would not fit ``budget_frac`` of the device.
 
@@ -139,21 +139,27 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
           + in-flight microbatches x local layers x per-layer stash (config.stash_bytes_per_layer)
           + logits of one head token chunk (bf16, gradient written in place; the whole
             microbatch's with MIPIPE_HEAD_CHUNK=0) + 4 GB workspace.
+    The distributed head with ZeRO-1 (``head_shards`` = PP) keeps its f32 master and Adam
+    moments (12 of the 20 bytes) for 1 / head_shards of the matrix: ``head_optimizer_bytes``
+    is that per-rank optimizer state, ``head_state_bytes`` all of the head's.
     Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute."""
     T = mbs * seq_len
     nlayers = sum(layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages)
     emb = cfg.vocab_padded * cfg.d_model
-    nparams = cfg.layer_params() * nlayers + (emb if 0 in my_stages else 0) + (emb if head_tokens else 0)
+    nparams = cfg.layer_params() * nlayers + (emb if 0 in my_stages else 0)
+    head_opt = 12.0 * emb / max(1, head_shards) if head_tokens else 0.0
+    head_state = (8.0 * emb if head_tokens else 0.0) + head_opt
     inflight = max_inflight_microbatches(order, set(my_stages))
     from .models.native import _HEAD_CHUNK
     logit_rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
-    fixed = 20.0 * nparams + 2.0 * logit_rows * cfg.vocab_padded + 4e9
+    fixed = 20.0 * nparams + head_state + 2.0 * logit_rows * cfg.vocab_padded + 4e9
     full = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=False)
     rec = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=True) + \
         cfg.stash_bytes_per_layer(T, recompute=False)
     total = torch.cuda.get_device_properties(device).total_memory if device.type == "cuda" else float("inf")
     return dict(inflight=inflight, layers=nlayers, bytes_no_recompute=full, bytes_recompute=rec, hbm=total,
-                recompute=bool(full > budget_frac * total))
+                recompute=bool(full > budget_frac * total), head_state_bytes=head_state,
+                head_optimizer_bytes=head_opt)
 
 
 def auto_lanes(cfg: NativeConfig, pp: int, v: int, graphs: bool, device, m: int, tokens: int, params: int,
@@ -247,7 +253,8 @@ class PipelineTrainer:
             head_tokens = (self.head_chunks[self.mesh.pp_rank] if self.head_chunks is not None else
                            (mbs * seq_len if (num_stages - 1) in my_stages else 0))
             self.memory_plan = plan_recompute(cfg, layer_ranges, my_stages, order, mbs, seq_len, self.device,
-                                              head_tokens=head_tokens)
+                                              head_tokens=head_tokens,
+                                              head_shards=pp if (self.head_zero and pp > 1) else 1)
             recompute = self.memory_plan["recompute"]
         self.recompute = bool(recompute)
         self.stages: List[NativeStage] = []

@@ -269,7 +269,7 @@ class ParamArena:
         g0 = self.grad_lanes[0]
         rest = self.grad_lanes[1:]
         if g0.is_cuda:
-            if len(rest) <= 3:
+            if len(rest) <= 3 and _FUSED_MERGE_NORM:
                 if self.merged_sumsq is None:
                     self.merged_sumsq = torch.zeros(1, dtype=torch.float32, device=g0.device)
                 self.merged_sumsq.zero_()
@@ -777,6 +777,10 @@ def head_param_specs(cfg: NativeConfig) -> List[ParamSpec]:
         out.append(ParamSpec("output.bias", (cfg.vocab_padded,), "zeros", False))
     return out
 
+
+# MIPIPE_FUSED_MERGE_NORM=0: merge the lane gradients without the fused sum of squares (the
+# optimizer then makes its own pass for the clipping norm) -- the A/B switch of the fusion.
+_FUSED_MERGE_NORM = os.environ.get("MIPIPE_FUSED_MERGE_NORM", "1") != "0"
 
 # MIPIPE_HEAD_CHUNK: how the last stage runs its LM head + CE.
 #   -1 (default): logits GEMM + fused CE in the forward, the dX / dW GEMMs in the backward

@@ -187,6 +187,15 @@ def test_recompute_auto_plan():
             plan = plan_recompute(cfg, lr, [0], order, 1, 8192, torch.device("cuda", 0), head_tokens=8192)
             assert plan["recompute"] is want, plan
         assert 180e9 < plan["bytes_no_recompute"] < 230e9
+        # distributed head, Llama-3 8B PP=8: ZeRO-1 keeps 1/8 of the head's master + Adam
+        # moments per rank (the bf16 weights, W^T copy and f32 gradient stay whole)
+        l8 = balanced_layer_ranges(cfg, 8, 8192, head_on_last=False)
+        o8 = generate("1F1B", 8, 16, 1, "loop")[7]
+        full = plan_recompute(cfg, l8, [7], o8, 1, 8192, torch.device("cuda", 0), head_tokens=1024)
+        zero = plan_recompute(cfg, l8, [7], o8, 1, 8192, torch.device("cuda", 0), head_tokens=1024, head_shards=8)
+        assert zero["head_optimizer_bytes"] <= full["head_optimizer_bytes"] / 8 + 1
+        assert full["bytes_no_recompute"] - zero["bytes_no_recompute"] == pytest.approx(
+            7 / 8 * full["head_optimizer_bytes"])
     finally:
         E.torch.cuda.get_device_properties = orig
     # 1F1B PP=4: rank 0 holds 4 microbatches in flight, the last rank 1; GPipe holds all m

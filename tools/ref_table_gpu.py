@@ -51,6 +51,7 @@ def main():
                     help="fp32: the linears / attention projections on this framework's f32 MFMA GEMM (gemm_f32.hip) "
                          "instead of ATen (hipBLASLt); 2.3x slower today (profiles/r2_probes.md)")
     ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"])
+    ap.add_argument("--only", default=None, help="comma list of LxH configs, e.g. 8x8,4x4 (default: all 9)")
     ap.add_argument("--engine", default="native", choices=["native", "aten", "trainer"],
                     help="native: the reference-compatible API (Schedule1F1B over build_reference_stage: this "
                          "framework's kernels at --precision, HIP graphs + native tape + lanes), fwd+bwd only -- "
@@ -72,6 +73,8 @@ def main():
     out = []
     for L in (4, 8, 12):
         for H in (4, 8, 12):
+            if not _selected(a, L, H):
+                continue
             cfg = NativeConfig.reference(n_layers=L, n_heads=H)
             tr = PipelineTrainer(cfg, pp=1, schedule="1F1B", n_microbatches=m, mbs=B // m, seq_len=S, device=dev,
                                  seed=0, graphs=not a.no_graphs)
@@ -108,6 +111,10 @@ def main():
             json.dump(summary, f, indent=1)
 
 
+def _selected(a, L, H):
+    return a.only is None or f"{L}x{H}" in a.only.split(",")
+
+
 def main_native(a):
     """The reference's workload through the reference-compatible API on this framework's
     kernels: ``native_reference_schedule`` (build_reference_stage at --precision, HIP graphs,
@@ -125,6 +132,8 @@ def main_native(a):
     out = []
     for L in (4, 8, 12):
         for H in (4, 8, 12):
+            if not _selected(a, L, H):
+                continue
             torch.manual_seed(L * 100 + H)
             args = ModelArgs(n_layers=L, n_heads=H)
             sched = native_reference_schedule(args, "1F1B", 0, 1, B, S, m, dev, precision=a.precision)
@@ -173,6 +182,8 @@ def main_fp32(a):
     out = []
     for L in (4, 8, 12):
         for H in (4, 8, 12):
+            if not _selected(a, L, H):
+                continue
             torch.manual_seed(L * 100 + H)
             args = ModelArgs(n_layers=L, n_heads=H)
             stage = manual_model_split(Transformer(args), 0, 1, dev)
