@@ -20,6 +20,7 @@ int mp_embed_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out
 int mp_embed_bwd(const int64_t* idx, const void* dout, float* dwte, float* dwpe, int T, int S, int D, int pos_offset,
                  int f32, hipStream_t st);
 int mp_sumsq(const float* g, int64_t n, float* out, hipStream_t st);
+int mp_scaled_sum(const float* x, int64_t n, float scale, float* out, hipStream_t st);
 int mp_gemm_f32(const float* A, const float* B, float* C, const float* bias, int M, int N, int K, int64_t lda,
                 int a_kc, int64_t ldb, int b_nc, int64_t ldc, float alpha, int accumulate, hipStream_t st);
 int mp_gemm_f32_ex(const float* A, const float* B, float* C, const float* bias, const float* R, float* X, int M, int N,
@@ -224,6 +225,20 @@ void lane_merge(torch::Tensor g0, std::vector<torch::Tensor> lanes, c10::optiona
 void sumsq(torch::Tensor g, torch::Tensor out) {
   req(g, torch::kFloat32, "g");
   check(mp_sumsq(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), cur_stream()), "sumsq");
+}
+
+// contiguous tensor <- 0 with hipMemsetAsync on the current stream (graph-capturable)
+void zero_(torch::Tensor t) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "zero_: contiguous GPU tensor");
+  TORCH_CHECK(hipMemsetAsync(t.data_ptr(), 0, t.numel() * t.element_size(), cur_stream()) == hipSuccess, "zero_");
+}
+
+// out (f32 scalar) = scale * sum(x): one workgroup, deterministic
+void scaled_sum(torch::Tensor x, double scale, torch::Tensor out) {
+  req(x, torch::kFloat32, "x");
+  req(out, torch::kFloat32, "out");
+  check(mp_scaled_sum(x.data_ptr<float>(), x.numel(), (float)scale, out.data_ptr<float>(), cur_stream()),
+        "scaled_sum");
 }
 
 void adamw(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> w16,
@@ -611,6 +626,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed_fwd", &embed_fwd);
   m.def("embed_bwd", &embed_bwd);
   m.def("sumsq", &sumsq);
+  m.def("scaled_sum", &scaled_sum);
+  m.def("zero_", &zero_);
   m.def("gemm_f32", &gemm_f32);
   m.def("gemm_f32_ex", &gemm_f32_ex, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
         pybind11::arg("R"), pybind11::arg("X"), pybind11::arg("epi") = 0, pybind11::arg("alpha") = 1.0,

@@ -164,6 +164,24 @@ static int grid_for(int64_t n) {
   return (int)(b < 2048 ? (b < 1 ? 1 : b) : 2048);
 }
 
+// out[0] = scale * sum(x[0 .. n)) in one workgroup, fixed order (deterministic): the
+// microbatch's mean token loss (the row losses of the fused cross-entropy)
+__global__ void __launch_bounds__(256) scaled_sum_kernel(const float* __restrict__ x, int64_t n, float scale,
+                                                         float* __restrict__ out) {
+  __shared__ float part[4];
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) acc += x[i];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = scale * ((part[0] + part[1]) + (part[2] + part[3]));
+}
+
+extern "C" int mp_scaled_sum(const float* x, int64_t n, float scale, float* out, hipStream_t st) {
+  scaled_sum_kernel<<<1, 256, 0, st>>>(x, n, scale, out);
+  return (int)hipGetLastError();
+}
+
 extern "C" int mp_sumsq(const float* g, int64_t n, float* out, hipStream_t st) {
   sumsq_kernel<<<grid_for(n), 256, 0, st>>>(g, n, out);
   return (int)hipGetLastError();

@@ -188,7 +188,7 @@ class ParamArena:
 
     def zero_grad(self) -> None:
         for g in self.grad_lanes:
-            g.zero_()
+            ops.zero_(g)
 
     # ------------------------------------------------------------------ ZeRO-1
     def shard_master(self, lo: int, hi: int, gather: Callable[[torch.Tensor], torch.Tensor]) -> None:
@@ -272,7 +272,7 @@ class ParamArena:
             if len(rest) <= 3 and _FUSED_MERGE_NORM:
                 if self.merged_sumsq is None:
                     self.merged_sumsq = torch.zeros(1, dtype=torch.float32, device=g0.device)
-                self.merged_sumsq.zero_()
+                ops.zero_(self.merged_sumsq)
                 ops.load_ext().lane_merge(g0, rest, self.merged_sumsq)
                 return
             self.merged_sumsq = None
@@ -968,16 +968,17 @@ class NativeModel:
             if ov is not None:
                 ov.join()
             ctx.misc.update(dhn=dhn)
-            return row_loss.mean()
+            return ops.mean(row_loss)
         logits, _ = ops.linear(hn, self.head_weight(), hb)
         if target is None:
             ctx.misc.update(hn=hn, logits=logits)
             return logits
-        if keep_logits:
-            ctx.misc["logits_out"] = logits.clone()
+        if keep_logits:   # (into the caller's persistent buffer when it gives one: a plain device copy)
+            dst = ctx.misc.pop("logits_dst", None)
+            ctx.misc["logits_out"] = dst.copy_(logits) if dst is not None else logits.clone()
         row_loss = ops.xent_fwd_bwd(logits, target.reshape(-1), cfg.vocab_size, grad_scale=loss_scale / T)
         ctx.misc.update(hn=hn, dlogits=logits)
-        return row_loss.mean()
+        return ops.mean(row_loss)
 
     # ------------------------------------------------------------------ backward
     def backward(self, dy: Optional[torch.Tensor], ctx: MBContext, B: int, S: int, weight_grads: bool = True):

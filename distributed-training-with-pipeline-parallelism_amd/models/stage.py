@@ -56,6 +56,10 @@ class NativeStage(StageBase):
             graphs = False
         self.graphs = GraphCache(str(self.stage_index)) if graphs else None
         self.want_outputs = False   # set per step by the runtime (step(return_outputs=...))
+        self.n_microbatches = 1     # (likewise)
+        # returned logits: microbatch mb's rows of one persistent [m * T, vocab_padded] buffer,
+        # so the schedule hands back the merged [B, S, vocab] as a view (no concatenation)
+        self._merged_logits: Optional[torch.Tensor] = None
         self._gctx = {}
 
     def _graphed(self) -> bool:
@@ -79,6 +83,8 @@ class NativeStage(StageBase):
         # on the GPU the step enters through the device counter (set_dropout_step), so
         # eager and graph-replayed steps draw identical masks; the CPU ops see the seed only
         ctx = MBContext(mb, _seed(self.seed, 0 if self.model.device.type == "cuda" else self.step_id, mb))
+        if want_logits:
+            ctx.misc["logits_dst"] = self._logits_dst(mb)
         x = args[0]
         out = self.model.forward(x, ctx, self.mbs, self.S, target=target if self.is_last else None,
                                  loss_scale=loss_scale, keep_logits=want_logits)
@@ -92,6 +98,15 @@ class NativeStage(StageBase):
                 return (self._logits_view(ctx.misc.pop("logits_out")),), out
             return (out.detach(),), out
         return (out,), None
+
+    def _logits_dst(self, mb: int) -> torch.Tensor:
+        T = self.mbs * self.S
+        m = max(self.n_microbatches, mb + 1)
+        buf = self._merged_logits
+        if buf is None or buf.shape[0] < m * T:
+            buf = self._merged_logits = torch.empty(m * T, self.cfg.vocab_padded, dtype=self.model.arena.dtype,
+                                                    device=self.model.device)
+        return buf[mb * T:(mb + 1) * T]
 
     def _logits_view(self, logits):
         """[T, vocab_padded] -> [mbs, S, vocab] (the reference's output shape)."""
@@ -132,6 +147,8 @@ class NativeStage(StageBase):
 
         def fn(ins):
             ctx = MBContext(mb, _seed(self.seed, 0, mb))
+            if want_logits:
+                ctx.misc["logits_dst"] = self._logits_dst(mb)
             out = self.model.forward(ins[0], ctx, self.mbs, self.S, target=ins[1] if last_loss else None,
                                      loss_scale=loss_scale, keep_logits=want_logits)
             self._gctx[mb] = ctx

@@ -822,6 +822,24 @@ def set_dropout_step(step: int, device: Optional[torch.device] = None) -> None:
     _ext().set_dropout_step(int(step))
 
 
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """t <- 0 (GPU: hipMemsetAsync on the current stream instead of an ATen fill kernel)."""
+    if _gpu(t) and t.is_contiguous():
+        _ext().zero_(t)
+        return t
+    return t.zero_()
+
+
+def mean(x: torch.Tensor) -> torch.Tensor:
+    """Mean of an f32 tensor as a 0-dim f32 tensor (GPU: one deterministic workgroup,
+    optim.hip scaled_sum_kernel -- e.g. the microbatch's mean token loss)."""
+    if _gpu(x) and x.dtype == torch.float32 and x.is_contiguous():
+        out = torch.empty((), device=x.device, dtype=torch.float32)
+        _ext().scaled_sum(x, 1.0 / max(1, x.numel()), out)
+        return out
+    return x.mean()
+
+
 def sumsq(g: torch.Tensor, out: torch.Tensor):
     if _gpu(g):
         _ext().sumsq(g, out)

@@ -87,8 +87,8 @@ class _PipelineSchedule:
         if outs is None or not has_last:
             return None
         if len(outs[0]) == 1:
-            return torch.cat([o[0] for o in outs], dim=0)   # merged last-stage outputs (logits)
-        return tuple(torch.cat([o[i] for o in outs], dim=0) for i in range(len(outs[0])))
+            return _merge([o[0] for o in outs])   # merged last-stage outputs (logits)
+        return tuple(_merge([o[i] for o in outs]) for i in range(len(outs[0])))
 
     def eval(self, *args, target=None, losses=None):
         """Forward-only pass (dependency schedules.py:402-420)."""
@@ -117,6 +117,21 @@ class _PipelineSchedule:
         if not outs:
             return None
         return torch.cat([o[0] for o in outs], dim=0)
+
+
+def _merge(parts):
+    """torch.cat(parts, 0) -- or, when the parts are consecutive row blocks of one buffer (the
+    native stage's persistent logits), the view of that buffer spanning them."""
+    p0 = parts[0]
+    if len(parts) > 1 and all(p.dim() == p0.dim() and p.shape[1:] == p0.shape[1:] and p.stride() == p0.stride()
+                              and p.untyped_storage().data_ptr() == p0.untyped_storage().data_ptr()
+                              for p in parts):
+        step = p0.shape[0] * p0.stride(0)
+        if all(p.shape[0] == p0.shape[0] and p.storage_offset() == p0.storage_offset() + i * step
+               for i, p in enumerate(parts)):
+            return p0.as_strided((p0.shape[0] * len(parts),) + tuple(p0.shape[1:]), p0.stride(),
+                                 p0.storage_offset())
+    return torch.cat(parts, dim=0)
 
 
 class ScheduleGPipe(_PipelineSchedule):

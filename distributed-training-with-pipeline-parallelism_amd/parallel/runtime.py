@@ -586,6 +586,7 @@ class PipelineRuntime:
         for st in self.stages.values():
             st.clear_runtime_states()
             st.want_outputs = bool(return_outputs)
+            st.n_microbatches = self.m
         recv_works: Dict[tuple, List] = {}
         send_keep: List = []
         send_tensors: Dict[tuple, Tuple[torch.Tensor, ...]] = {}

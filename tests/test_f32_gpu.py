@@ -286,3 +286,15 @@ def test_compat_reference_api_runs_native_tape_fp32():
     assert "error" not in m, m
     assert m["precision"] == "fp32" and m["native_runner"], m
     assert m["throughput"] > 0 and m["lanes"] >= 1
+
+
+def test_mean_and_zero_kernels():
+    """ops.mean (one-workgroup deterministic sum, the microbatch loss) and ops.zero_
+    (hipMemsetAsync) -- the step's last ATen reductions / fills."""
+    x = torch.randn(1000, device=DEV)
+    m1, m2 = ops.mean(x), ops.mean(x)
+    assert m1.shape == () and m1.item() == m2.item()
+    close(m1, x.double().mean(), atol=1e-6, rtol=1e-6)
+    y = torch.randn(37, 5, device=DEV)
+    ops.zero_(y)
+    assert int((y != 0).sum()) == 0

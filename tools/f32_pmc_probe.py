@@ -25,6 +25,12 @@ for _ in range(10):
     K_._gemm_f32(x, wq.t(), yq)
 for _ in range(10):
     K_._gemm_f32(dyq.t(), x, dwq, accumulate=True)
+# dX of linear1 (1024 x 768 over K = 2048: 192 tiles, 32 K-tile pairs), no split: one
+# workgroup per CU, the main loop at 2 waves per SIMD
+dy1, w1, dx1 = torch.randn(T, 2048, device=dev), torch.randn(2048, 768, device=dev), torch.empty(T, 768, device=dev)
+ext = ops.load_ext()
+for _ in range(10):
+    ext.gemm_f32_ex(dy1, w1, dx1, None, None, None, 0, 1.0, False, 0.0, 0, 1)
 B, S, H, D = 8, 128, 8, 96
 qkv = torch.randn(B * S, 3 * H * D, device=dev)
 q, k, v = qkv[:, :H * D], qkv[:, H * D:2 * H * D], qkv[:, 2 * H * D:]
