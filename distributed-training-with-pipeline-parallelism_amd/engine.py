@@ -42,7 +42,7 @@ class FlatAdamW:
 
     def __init__(self, arenas: List[ParamArena], lr: float = 3e-4, betas=(0.9, 0.95), eps: float = 1e-8,
                  weight_decay: float = 0.1, max_grad_norm: float = 1.0, pp_group=None, norm_skip=(),
-                 norm_exclude=None, grad_scale: float = 1.0, coll=None):
+                 norm_exclude=None, grad_scale: float = 1.0, coll=None, merged_norm: bool = True):
         self.arenas = arenas
         # parallel/collectives.py: the clip-norm sum over the pipeline group and the
         # all-gather of ZeRO-sharded arenas' updated bf16 weights
@@ -56,6 +56,9 @@ class FlatAdamW:
         # gradients arrive DP-summed (the all-reduces skip a separate divide pass); the
         # 1/dp factor is applied inside the AdamW kernel (and to the clip norm)
         self.grad_scale = float(grad_scale)
+        # the fused lane merge's sum of squares is the clipping norm only when nothing
+        # reduces the gradient after the merge (no DP all-reduce in between)
+        self.merged_norm = bool(merged_norm)
         self.lr, self.betas, self.eps, self.wd = lr, betas, eps, weight_decay
         self.max_norm = max_grad_norm
         self.pp_group = pp_group
@@ -78,7 +81,8 @@ class FlatAdamW:
                 if a.shard is not None:     # this rank's (reduced) range of a sharded arena
                     ops.sumsq(a.opt_views()[1], self.sumsq)
                     continue
-                if len(a.grad_lanes) > 1 and a.merged_sumsq is not None and i not in self.norm_exclude:
+                if (self.merged_norm and len(a.grad_lanes) > 1 and a.merged_sumsq is not None
+                        and i not in self.norm_exclude):
                     self.sumsq.add_(a.merged_sumsq)     # computed by the fused lane merge
                     continue
                 lo = 0
@@ -308,7 +312,8 @@ class PipelineTrainer:
                 self.runtime.head_reduce = self._head_reduce
         self.optimizer = FlatAdamW(arenas, lr=lr, eps=adam_eps, weight_decay=weight_decay, max_grad_norm=max_grad_norm,
                                    pp_group=self.mesh.pp_group if pp > 1 else None, norm_skip=norm_skip,
-                                   norm_exclude=norm_exclude, grad_scale=1.0 / self.mesh.dp, coll=self.coll)
+                                   norm_exclude=norm_exclude, grad_scale=1.0 / self.mesh.dp, coll=self.coll,
+                                   merged_norm=self.mesh.dp == 1)
         self.last_losses: List[torch.Tensor] = []
 
     def _head_reduce(self) -> list:
