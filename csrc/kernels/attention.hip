@@ -27,6 +27,7 @@
 //         accumulates dQ^T += K^T dS^T.
 #include "mp_common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 using namespace mp;
@@ -292,6 +293,207 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
       }
     }
     if (hl == 0) LSE[(int64_t)bh * Sq + qrow] = l_run > 0.f ? m_run + log2f(l_run) : INFINITY;
+  }
+}
+
+// ==========================================================================================
+// forward, short sequences: workgroup = 64 queries, keys split over two wave pairs
+// ==========================================================================================
+// At the reference's shape (B 8, S 128, non-causal, 4-12 heads) the 128-query workgroups
+// above are 32-96 for 256 CUs and every wave walks both 64-key tiles back to back.  Here
+// a workgroup owns 64 queries: waves (qs = w & 1: which 32 queries, kh = w >> 1: which key
+// tiles -- kh, kh + 2, ...).  Each wave pair stages its own K/V tiles (128 threads, the
+// same swizzled image and register double buffer), keeps its own online-softmax state,
+// and the kh = 1 waves hand (O^T, m, l) to their kh = 0 partners through LDS at the end:
+// twice the workgroups, half the serial tile chain per wave.  Non-causal only.
+template <int DP>
+struct StageHalf {   // a [64][DP] tile by the 128 threads of one wave pair
+  static constexpr int PER = DP / 16;
+  u16x8 v[PER];
+  __device__ __forceinline__ void load(const bf16_t* base, int64_t stride, int row0, int nrows, int D, int gt) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = gt + 128 * i;
+      const int r = idx / (DP / 8), c = idx % (DP / 8);
+      const int gr = row0 + r;
+      v[i] = gload8(base + (int64_t)gr * stride, c * 8, D, gr < nrows);
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int gt) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = gt + 128 * i;
+      const int r = idx / (DP / 8), c = idx % (DP / 8);
+      *reinterpret_cast<u16x8*>(lds + lds_off<DP>(r, c)) = v[i];
+    }
+  }
+};
+
+template <int DP, bool DROP>
+__global__ void __launch_bounds__(256, 1) attn_fwd_ks2_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+    float* __restrict__ LSE, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
+    int64_t os, float scale, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;
+  const int bh = (int)blockIdx.y;
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int qsub = w & 1, kh = w >> 1, gt = threadIdx.x & 127;
+  char* gbase = smem + kh * 4 * TILE;   // this pair's K[2] / V[2] tiles
+#define kbuf2(i) (gbase + (i) * TILE)
+#define vbuf2(i) (gbase + (2 + (i)) * TILE)
+  const int m0 = (int)blockIdx.x * 64;
+  const int qrow = m0 + 32 * qsub + l32;
+  const bool qvalid = qrow < Sq;
+  const bf16_t* Qb = Q + (int64_t)b * Sq * qs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * Sk * ks + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * Sk * vs + (int64_t)hk * D;
+  bf16x8 qf[DP / 16];
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    u16x8 t = gload8(Qb + (int64_t)qrow * qs, 16 * s + 8 * hl, D, qvalid);
+    qf[s] = __builtin_bit_cast(bf16x8, t);
+  }
+  const float c = scale * LOG2E;
+  const DropKey dkey = drop_key(seed, (uint32_t)bh);
+  const uint32_t dthr = drop_thr(p_drop), qoff = (uint32_t)qrow * (uint32_t)Sk;
+  const float dinv = 1.0f / (1.0f - p_drop);
+  f32x16 o[DP / 32];
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d) o[d] = {};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int ntiles = (Sk + 63) / 64;
+  const int niter = (ntiles + 1) / 2;   // the same trip count in both pairs (barriers inside)
+  StageHalf<DP> kst, vst;
+  kst.load(Kb, ks, 64 * kh, Sk, D, gt);
+  vst.load(Vb, vs, 64 * kh, Sk, D, gt);
+  kst.store(kbuf2(0), gt);
+  vst.store(vbuf2(0), gt);
+  for (int it = 0; it < niter; ++it) {
+    const int cur = it & 1;
+    const int n0 = 64 * (2 * it + kh);
+    if (it + 1 < niter) {
+      kst.load(Kb, ks, n0 + 128, Sk, D, gt);
+      vst.load(Vb, vs, n0 + 128, Sk, D, gt);
+    }
+    __syncthreads();
+    if (n0 < Sk) {
+      const char* kb = kbuf2(cur);
+      const char* vb = vbuf2(cur);
+      f32x16 s0 = {}, s1 = {};
+#pragma unroll
+      for (int s = 0; s < DP / 16; ++s) {
+        bf16x8 a0 = lds_row8<DP>(kb, l32, 2 * s + hl);
+        bf16x8 a1 = lds_row8<DP>(kb, 32 + l32, 2 * s + hl);
+        s0 = mfma32(a0, qf[s], s0);
+        s1 = mfma32(a1, qf[s], s1);
+      }
+      if (n0 + 64 > Sk) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+          if (n0 + kr >= Sk) s0[r] = -INFINITY;
+          if (n0 + 32 + kr >= Sk) s1[r] = -INFINITY;
+        }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float m_new = fmaxf(m_run, mx * c);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = __builtin_amdgcn_exp2f(m_run - m_use);
+      uint32_t keep = 0xffffffffu;
+      if (DROP) {
+        keep = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t kr = (uint32_t)(n0 + (r & 3) + 8 * (r >> 2) + 4 * hl);
+          keep |= (hash_lo(dkey, qoff + kr) >= dthr ? 1u : 0u) << r;
+          keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
+        }
+      }
+      float rs = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], c, -m_use));
+        float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c, -m_use));
+        rs += p0 + p1;
+        if (DROP) {
+          p0 = (keep >> r) & 1u ? p0 * dinv : 0.f;
+          p1 = (keep >> (16 + r)) & 1u ? p1 * dinv : 0.f;
+        }
+        s0[r] = p0;
+        s1[r] = p1;
+      }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run = l_run * alpha + rs;
+      m_run = m_new;
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) o[d] *= alpha;
+      const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+        const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
+        bf16x8 a;
+        a = cat44(lds_tr4<DP>(vb, 0 + 4 * hl, c0), lds_tr4<DP>(vb, 8 + 4 * hl, c0));
+        o[d] = mfma32(a, p00, o[d]);
+        a = cat44(lds_tr4<DP>(vb, 16 + 4 * hl, c0), lds_tr4<DP>(vb, 24 + 4 * hl, c0));
+        o[d] = mfma32(a, p01, o[d]);
+        a = cat44(lds_tr4<DP>(vb, 32 + 4 * hl, c0), lds_tr4<DP>(vb, 40 + 4 * hl, c0));
+        o[d] = mfma32(a, p10, o[d]);
+        a = cat44(lds_tr4<DP>(vb, 48 + 4 * hl, c0), lds_tr4<DP>(vb, 56 + 4 * hl, c0));
+        o[d] = mfma32(a, p11, o[d]);
+      }
+    }
+    if (it + 1 < niter) {
+      kst.store(kbuf2(cur ^ 1), gt);
+      vst.store(vbuf2(cur ^ 1), gt);
+    }
+  }
+#undef kbuf2
+#undef vbuf2
+  // the kh = 1 pair hands (O^T, m, l) to the kh = 0 pair
+  __syncthreads();
+  float* xo = reinterpret_cast<float*>(smem) + qsub * (DP / 32 * 16 * 64 + 128);
+  if (kh == 1) {
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xo[(d * 16 + r) * 64 + lane] = o[d][r];
+    xo[DP / 32 * 16 * 64 + lane] = m_run;
+    xo[DP / 32 * 16 * 64 + 64 + lane] = l_run;
+  }
+  __syncthreads();
+  if (kh == 1) return;
+  const float m1 = xo[DP / 32 * 16 * 64 + lane], l1 = xo[DP / 32 * 16 * 64 + 64 + lane];
+  const float mm = fmaxf(m_run, m1);
+  const float mu = mm == -INFINITY ? 0.f : mm;
+  const float a0 = __builtin_amdgcn_exp2f(m_run - mu), a1 = __builtin_amdgcn_exp2f(m1 - mu);
+  const float l = l_run * a0 + l1 * a1;
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[d][r] = o[d][r] * a0 + xo[(d * 16 + r) * 64 + lane] * a1;
+  if (qvalid) {
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    bf16_t* orow = O + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 32 * d + 8 * g + 4 * hl;
+        if (col < D) {
+          u16x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = f2bf(o[d][4 * g + e] * inv);
+          *reinterpret_cast<u16x4*>(orow + col) = pk;
+        }
+      }
+    }
+    if (hl == 0) LSE[(int64_t)bh * Sq + qrow] = l > 0.f ? mm + log2f(l) : INFINITY;
   }
 }
 
@@ -769,6 +971,20 @@ template <int DP, bool CAUSAL, bool DROP>
 static int launch_fwd(const void* q, const void* k, const void* v, void* o, float* lse, int B, int Sq, int Sk, int H,
                       int Hkv, int D, int64_t qs, int64_t ks, int64_t vs, int64_t os, float scale, float p,
                       uint64_t seed, hipStream_t st) {
+  // short non-causal problems (fewer 128-query blocks than CUs): the key-split kernel
+  if constexpr (!CAUSAL && DP <= 128) {
+    static const bool ks2_off = [] { const char* e = getenv("MIPIPE_ATTN_KS2"); return e && e[0] == '0'; }();
+    if (!ks2_off && (int64_t)((Sq + 127) / 128) * B * H < 256) {
+      const size_t lds2 = 8 * 64 * DP * 2;
+      auto kern2 = attn_fwd_ks2_kernel<DP, DROP>;
+      if (lds2 > 64 * 1024)
+        hipFuncSetAttribute((const void*)kern2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
+      dim3 grid2((Sq + 63) / 64, B * H);
+      kern2<<<grid2, 256, lds2, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, B, Sq,
+                                      Sk, H, Hkv, D, qs, ks, vs, os, scale, p, seed);
+      return (int)hipGetLastError();
+    }
+  }
   const size_t lds = 4 * 64 * DP * 2;
   auto kern = attn_fwd_kernel<DP, CAUSAL, DROP>;
   if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -51,6 +51,9 @@ def main():
                     help="fp32: the linears / attention projections on this framework's f32 MFMA GEMM (gemm_f32.hip) "
                          "instead of ATen (hipBLASLt); 2.3x slower today (profiles/r2_probes.md)")
     ap.add_argument("--precision", default="fp32", choices=["bf16", "fp32"])
+    ap.add_argument("--fwd-bwd", action="store_true",
+                    help="trainer engine: time the pipeline step alone (forward + backward, no AdamW), the "
+                         "reference's timed loop, for a like-for-like comparison with --engine native")
     ap.add_argument("--only", default=None, help="comma list of LxH configs, e.g. 8x8,4x4 (default: all 9)")
     ap.add_argument("--engine", default="native", choices=["native", "aten", "trainer"],
                     help="native: the reference-compatible API (Schedule1F1B over build_reference_stage: this "
@@ -58,6 +61,7 @@ def main():
                          "exactly the reference's timed loop; aten: the reference's own nn.Module model through the "
                          "same API (ATen f32 compute); trainer: PipelineTrainer with the AdamW step (bf16)")
     a = ap.parse_args()
+    a.precision_set = "--precision" in sys.argv
     if a.engine == "native":
         return main_native(a)
     if a.engine == "aten":
@@ -70,6 +74,8 @@ def main():
     ref = reference_rows()
     dev = torch.device("cuda", 0)
     B, S, m = 32, 128, 4
+    # the trainer's default is bf16; --precision fp32 given explicitly selects f32 arenas
+    trainer_dtype = torch.float32 if a.precision_set and a.precision == "fp32" else torch.bfloat16
     out = []
     for L in (4, 8, 12):
         for H in (4, 8, 12):
@@ -77,18 +83,29 @@ def main():
                 continue
             cfg = NativeConfig.reference(n_layers=L, n_heads=H)
             tr = PipelineTrainer(cfg, pp=1, schedule="1F1B", n_microbatches=m, mbs=B // m, seq_len=S, device=dev,
-                                 seed=0, graphs=not a.no_graphs)
+                                 seed=0, graphs=not a.no_graphs, dtype=trainer_dtype)
             g = torch.Generator(device="cuda").manual_seed(L * 100 + H)
             x = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
             y = torch.randint(0, cfg.vocab_size, (B, S), device=dev, generator=g)
             if not a.no_graphs:
                 tr.capture_graphs(x, y)   # setup (not timed): per-microbatch HIP graphs, dropout-safe
+            if a.fwd_bwd:
+                ins = [(c,) for c in torch.tensor_split(x, m, dim=0)]
+                tgs = list(torch.tensor_split(y, m, dim=0))
+
+                def one():
+                    ls = []
+                    tr.runtime.step(ins, tgs, ls, return_outputs=False)
+                    return torch.stack(ls).mean()
+            else:
+                def one():
+                    return tr.train_step(x, y)
             for _ in range(a.warmup):
-                tr.train_step(x, y)
+                one()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.iters):
-                loss = tr.train_step(x, y)
+                loss = one()
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             tok_s = B * S * a.iters / dt
@@ -103,7 +120,8 @@ def main():
             del tr
             torch.cuda.empty_cache()
     summary = {"config": "reference Transformer(dim 768, vocab 10000, post-LN, cross-attn, ReLU, dropout 0.1), "
-                         "batch 32 x seq 128, m=4, PP=1 on 1 MI355X, bf16, AdamW step included, "
+                         f"batch 32 x seq 128, m=4, PP=1 on 1 MI355X, {'fp32' if trainer_dtype == torch.float32 else 'bf16'}, "
+                         + ("fwd+bwd only, " if a.fwd_bwd else "AdamW step included, ")
                          + ("eager" if a.no_graphs else "HIP graphs") + ", microbatch lanes (MIPIPE_LANES)",
                "rows": out}
     if a.json:
