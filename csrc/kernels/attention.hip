@@ -302,35 +302,40 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
 // At the reference's shape (B 8, S 128, non-causal, 4-12 heads) the 128-query workgroups
 // above are 32-96 for 256 CUs and every wave walks both 64-key tiles back to back.  Here
 // a workgroup owns 64 queries: waves (qs = w & 1: which 32 queries, kh = w >> 1: which key
-// tiles -- kh, kh + 2, ...).  Each wave pair stages its own K/V tiles (128 threads, the
-// same swizzled image and register double buffer), keeps its own online-softmax state,
+// tiles -- kh, kh + 2, ...).  Each wave pair streams its own K/V tiles into the same
+// swizzled image by LDS-DMA (no staging registers), keeps its own online-softmax state,
 // and the kh = 1 waves hand (O^T, m, l) to their kh = 0 partners through LDS at the end:
 // twice the workgroups, half the serial tile chain per wave.  Non-causal only.
 template <int DP>
-struct StageHalf {   // a [64][DP] tile by the 128 threads of one wave pair
-  static constexpr int PER = DP / 16;
-  u16x8 v[PER];
-  __device__ __forceinline__ void load(const bf16_t* base, int64_t stride, int row0, int nrows, int D, int gt) {
-#pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int idx = gt + 128 * i;
-      const int r = idx / (DP / 8), c = idx % (DP / 8);
-      const int gr = row0 + r;
-      v[i] = gload8(base + (int64_t)gr * stride, c * 8, D, gr < nrows);
-    }
+struct GTileP {   // a [64][DP] tile by the 2 waves of one pair, LDS-DMA (the GTile scheme below)
+  static constexpr int CPR = DP / 8;           // 16-byte chunks per row
+  static constexpr int PR = 1024 / (DP * 2);   // rows per 1 KiB piece
+  static constexpr int PPW = (64 / PR) / 2;    // pieces per wave
+  int lr, phys;
+  __device__ __forceinline__ void init() {
+    const int lane = threadIdx.x & 63;
+    lr = lane / CPR;
+    phys = lane % CPR;
   }
-  __device__ __forceinline__ void store(char* lds, int gt) const {
+  __device__ __forceinline__ void issue(const bf16_t* base, int64_t stride, int row0, int nrows, int D, char* img,
+                                        int wv) const {
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int idx = gt + 128 * i;
-      const int r = idx / (DP / 8), c = idx % (DP / 8);
-      *reinterpret_cast<u16x8*>(lds + lds_off<DP>(r, c)) = v[i];
+    for (int i = 0; i < PPW; ++i) {
+      const int p = wv + 2 * i;
+      const int row = p * PR + lr;
+      const int chunk = (phys & ~15) | ((phys & 15) ^ chunk_swz<DP>(row));
+      int col = chunk * 8;
+      col = col < D ? col : 0;
+      int gr = row0 + row;
+      gr = gr < nrows ? gr : nrows - 1;   // rows past the end: masked keys / zero probabilities
+      __builtin_amdgcn_global_load_lds((const void*)(base + (int64_t)gr * stride + col),
+                                       (__attribute__((address_space(3))) void*)(img + p * 1024), 16, 0, 0);
     }
   }
 };
 
 template <int DP, bool DROP>
-__global__ void __launch_bounds__(256, 1) attn_fwd_ks2_kernel(
+__global__ void __launch_bounds__(256, 2) attn_fwd_ks2_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
     float* __restrict__ LSE, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
     int64_t os, float scale, float p_drop, uint64_t seed) {
@@ -340,10 +345,15 @@ __global__ void __launch_bounds__(256, 1) attn_fwd_ks2_kernel(
   const int bh = (int)blockIdx.y;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
-  const int qsub = w & 1, kh = w >> 1, gt = threadIdx.x & 127;
-  char* gbase = smem + kh * 4 * TILE;   // this pair's K[2] / V[2] tiles
+  const int qsub = w & 1, kh = w >> 1;
+  const int ntiles = (Sk + 63) / 64;
+  const int niter = (ntiles + 1) / 2;   // the same trip count in both pairs (barriers inside)
+  // this pair's K / V tiles: double-buffered when it walks more than one tile (S = 128:
+  // one tile per pair, 64 KB of LDS in all, as much as the 128-query kernel)
+  const int nbuf = niter > 1 ? 2 : 1;
+  char* gbase = smem + kh * 2 * nbuf * TILE;
 #define kbuf2(i) (gbase + (i) * TILE)
-#define vbuf2(i) (gbase + (2 + (i)) * TILE)
+#define vbuf2(i) (gbase + (nbuf + (i)) * TILE)
   const int m0 = (int)blockIdx.x * 64;
   const int qrow = m0 + 32 * qsub + l32;
   const bool qvalid = qrow < Sq;
@@ -364,21 +374,19 @@ __global__ void __launch_bounds__(256, 1) attn_fwd_ks2_kernel(
 #pragma unroll
   for (int d = 0; d < DP / 32; ++d) o[d] = {};
   float m_run = -INFINITY, l_run = 0.f;
-  const int ntiles = (Sk + 63) / 64;
-  const int niter = (ntiles + 1) / 2;   // the same trip count in both pairs (barriers inside)
-  StageHalf<DP> kst, vst;
-  kst.load(Kb, ks, 64 * kh, Sk, D, gt);
-  vst.load(Vb, vs, 64 * kh, Sk, D, gt);
-  kst.store(kbuf2(0), gt);
-  vst.store(vbuf2(0), gt);
+  GTileP<DP> gp;
+  gp.init();
+  const int wv = __builtin_amdgcn_readfirstlane(qsub);
+  gp.issue(Kb, ks, 64 * kh, Sk, D, kbuf2(0), wv);
+  gp.issue(Vb, vs, 64 * kh, Sk, D, vbuf2(0), wv);
   for (int it = 0; it < niter; ++it) {
     const int cur = it & 1;
     const int n0 = 64 * (2 * it + kh);
-    if (it + 1 < niter) {
-      kst.load(Kb, ks, n0 + 128, Sk, D, gt);
-      vst.load(Vb, vs, n0 + 128, Sk, D, gt);
+    __syncthreads();   // (waits for this wave's LDS-DMA first: tile `it` is in LDS for the pair)
+    if (it + 1 < niter) {   // the next tile into the buffer the pair finished before this barrier
+      gp.issue(Kb, ks, n0 + 128, Sk, D, kbuf2(cur ^ 1), wv);
+      gp.issue(Vb, vs, n0 + 128, Sk, D, vbuf2(cur ^ 1), wv);
     }
-    __syncthreads();
     if (n0 < Sk) {
       const char* kb = kbuf2(cur);
       const char* vb = vbuf2(cur);
@@ -447,10 +455,6 @@ __global__ void __launch_bounds__(256, 1) attn_fwd_ks2_kernel(
         a = cat44(lds_tr4<DP>(vb, 48 + 4 * hl, c0), lds_tr4<DP>(vb, 56 + 4 * hl, c0));
         o[d] = mfma32(a, p11, o[d]);
       }
-    }
-    if (it + 1 < niter) {
-      kst.store(kbuf2(cur ^ 1), gt);
-      vst.store(vbuf2(cur ^ 1), gt);
     }
   }
 #undef kbuf2
@@ -975,7 +979,8 @@ static int launch_fwd(const void* q, const void* k, const void* v, void* o, floa
   if constexpr (!CAUSAL && DP <= 128) {
     static const bool ks2_off = [] { const char* e = getenv("MIPIPE_ATTN_KS2"); return e && e[0] == '0'; }();
     if (!ks2_off && (int64_t)((Sq + 127) / 128) * B * H < 256) {
-      const size_t lds2 = 8 * 64 * DP * 2;
+      const int niter = ((Sk + 63) / 64 + 1) / 2;
+      const size_t lds2 = (niter > 1 ? 8 : 4) * 64 * DP * 2;
       auto kern2 = attn_fwd_ks2_kernel<DP, DROP>;
       if (lds2 > 64 * 1024)
         hipFuncSetAttribute((const void*)kern2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2);
