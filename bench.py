@@ -2,13 +2,15 @@
 """Flagship benchmark: GPT-2 pipeline-parallel training throughput on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model gpt2-small]
-                    [--schedule 1F1B] [--mbs 16] [--seq 1024] [--microbatches M]
+                    [--schedule 1F1B] [--mbs 32] [--seq 1024] [--microbatches M]
 
 N GPUs = N pipeline stages (PP=N, one process per GPU); for N>1 the driver launches it
 with torch.distributed.run (if launched without it, this script re-launches itself under
 torch.distributed.run).  Work per GPU is fixed as N grows: ``microbatches = 2*N`` (8 at
 PP=4, BASELINE config 2), microbatch = ``mbs`` sequences of ``seq`` tokens, so the global
-batch grows with N ("weak" scaling).  Each timed step is a full training step: all
+batch grows with N ("weak" scaling).  mbs defaults to 32: 32K-token microbatches, and at
+PP=8 a 512 x 1024 = 0.5M-token global batch (GPT-2 / GPT-3-small's batch size); on one
+GPU mbs 32 runs 944.5K tok/s vs 886.9K with mbs 16 (profiles/r3_bench_mbs_ab.txt).  Each timed step is a full training step: all
 microbatch forwards/backwards through the lowered schedule, p2p of activations and
 gradients, grad-norm clip and the fused AdamW update.
 
@@ -65,7 +67,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--schedule", default="1F1B")
-    ap.add_argument("--mbs", type=int, default=16)
+    ap.add_argument("--mbs", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--dp", type=int, default=1)
