@@ -6,11 +6,14 @@
 
 N GPUs = N pipeline stages (PP=N, one process per GPU); for N>1 the driver launches it
 with torch.distributed.run (if launched without it, this script re-launches itself under
-torch.distributed.run).  Work per GPU is fixed as N grows: ``microbatches = 2*N`` (8 at
-PP=4, BASELINE config 2), microbatch = ``mbs`` sequences of ``seq`` tokens, so the global
-batch grows with N ("weak" scaling).  mbs defaults to 32: 32K-token microbatches, and at
-PP=8 a 512 x 1024 = 0.5M-token global batch (GPT-2 / GPT-3-small's batch size); on one
-GPU mbs 32 runs 944.5K tok/s vs 886.9K with mbs 16 (profiles/r3_bench_mbs_ab.txt).  Each timed step is a full training step: all
+torch.distributed.run).  Work per GPU is fixed as N grows: ``microbatches = 4*N``,
+microbatch = ``mbs`` sequences of ``seq`` tokens, so the global batch grows with N
+("weak" scaling: every GPU runs 4 x mbs sequences through all of its layers per step).
+mbs defaults to 32: 32K-token microbatches (on one GPU mbs 32 runs 944.5K tok/s vs 886.9K
+with mbs 16, profiles/r3_bench_mbs_ab.txt).  m = 4P rather than 2P: the 1F1B bubble
+(P-1)/(m+P-1) at P = 8 drops from 0.30 to 0.18 (planned efficiency of the lowered program
+with the distributed head 0.72 -> 0.83, tools/schedule_table.py); at P = 8 the global batch
+is 1024 x 1024 = 1M tokens.  Each timed step is a full training step: all
 microbatch forwards/backwards through the lowered schedule, p2p of activations and
 gradients, grad-norm clip and the fused AdamW update.
 
@@ -243,7 +246,7 @@ def run(a) -> None:
         pp = world // dp
         if pp * dp != world:
             raise SystemExit(f"--dp {dp} does not divide WORLD_SIZE={world}")
-        m = a.microbatches if a.microbatches is not None else max(2, 2 * pp)
+        m = a.microbatches if a.microbatches is not None else 4 * pp
         kw = {"vocab_size": a.vocab} if a.vocab else {}
         cfg = NativeConfig.by_name(a.model, **kw)
         gpu = device.type == "cuda"

@@ -76,7 +76,7 @@ def test_two_stalled_attempts_end_nonzero_within_the_deadline():
 def test_bench_eight_ranks_gpt2_small_layout():
     """The N = 8 launch the driver makes (bench.py --gpus 8 self-launch under
     torch.distributed.run, supervisor, PP = 8 over GPT-2 small's 12 layers with the
-    distributed head, m = 2P = 16) completes on CPU/gloo and prints one valid line."""
+    distributed head, m = 4P = 32) completes on CPU/gloo and prints one valid line."""
     env = dict(os.environ, OMP_NUM_THREADS="1", MIPIPE_BENCH_ATTEMPT_S="200", MASTER_PORT=str(free_port()))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
@@ -88,7 +88,7 @@ def test_bench_eight_ranks_gpt2_small_layout():
     assert len(lines) == 1
     out = json.loads(lines[0])
     c = out["config"]
-    assert out["n_gpus"] == 8 and out["value"] > 0 and c["parallelism"] == "pp8" and c["microbatches"] == 16
+    assert out["n_gpus"] == 8 and out["value"] > 0 and c["parallelism"] == "pp8" and c["microbatches"] == 32
     assert c["model"] == "gpt2-small" and len(c["layer_split"]) == 8
     assert sum(b - a for a, b in c["layer_split"]) == 12
     assert c["head"].startswith("distributed") and out["bubble_fraction"] is not None
