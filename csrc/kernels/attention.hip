@@ -968,6 +968,379 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
 
 #undef kbuf
 #undef vbuf
+
+// ==========================================================================================
+// backward, short non-causal sequences (Sq, Sk <= 128): dQ and dK/dV workgroups in ONE grid
+// ==========================================================================================
+// At the reference's shape (B 8, S 128, H 8, d_h 96) the two kernels above are 64
+// workgroups each for 256 CUs, run back to back (dK/dV reads the delta the dQ kernel
+// writes), and every wave walks both 64-row tiles serially.  Here one launch holds both
+// roles, each on 64-row blocks with the other dimension split over two wave pairs:
+//   blockIdx.x <  nq: dQ of 64 queries.  Wave (qsub = w & 1: which 32 queries, half =
+//                     w >> 1: which 64-key tile) -- the half = 1 pair's partial dQ is added
+//                     to the half = 0 pair's through LDS.
+//   blockIdx.x >= nq: dK / dV of 64 keys.  Wave (ksub = w & 1: which 32 keys, half: which
+//                     64-query tile); partial dK / dV added the same way.
+// Both roles compute delta = rowsum(dO * O) themselves (the dK/dV pairs stream the O tile
+// beside Q / dO and reduce it in LDS), so the roles are independent: 4x the workgroups of
+// one kernel above in one launch, and no serial tile chain.  One tile per pair: every
+// buffer is loaded once (LDS-DMA, the GTileP scheme), no ring.  The math per tile is the
+// two kernels' (same dropout indices, same masks).  Non-causal, H == Hkv, d_h <= 128 (at
+// d_h 256 -- the O slot of the dK/dV pairs refilled with Q after delta, 129 KB of LDS --
+// the two roles' registers spill 69 VGPRs, so the launcher keeps the two-kernel path).
+template <int DP, bool DROP>
+__global__ void __launch_bounds__(256, 1) attn_bwd_short_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
+    bf16_t* __restrict__ dQ, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int Sq, int Sk, int H, int D,
+    int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs, int64_t dks, int64_t dvs, float scale, float p_drop,
+    uint64_t seed, float* __restrict__ CSQ, float* __restrict__ CSK, float* __restrict__ CSV) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;
+  constexpr bool SEQ_O = DP > 128;     // O and Q share one slot (delta first)
+  const int bh = (int)blockIdx.y;
+  const int b = bh / H, h = bh % H;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int sub = w & 1, half = w >> 1;
+  const int nq = (Sq + 63) / 64;
+  const float c = scale * LOG2E;
+  const DropKey dkey = drop_key(seed, (uint32_t)bh);
+  const uint32_t dthr = drop_thr(p_drop);
+  const float dinv = 1.0f / (1.0f - p_drop);
+  GTileP<DP> gp;
+  gp.init();
+  const int wv = __builtin_amdgcn_readfirstlane(sub);
+  const bf16_t* Qb = Q + (int64_t)b * Sq * qs + (int64_t)h * D;
+  const bf16_t* Kb = K + (int64_t)b * Sk * ks + (int64_t)h * D;
+  const bf16_t* Vb = V + (int64_t)b * Sk * vs + (int64_t)h * D;
+  const bf16_t* Ob = O + (int64_t)b * Sq * os + (int64_t)h * D;
+  const bf16_t* Gb = dO + (int64_t)b * Sq * os + (int64_t)h * D;
+
+  if ((int)blockIdx.x < nq) {
+    // =================================== dQ role ===================================
+    const int m0 = (int)blockIdx.x * 64;
+    const int qrow = m0 + 32 * sub + l32;
+    const bool qvalid = qrow < Sq;
+    const int n0 = 64 * half;                 // this pair's key tile
+    char* kb = smem + half * 2 * TILE;
+    char* vb = kb + TILE;
+    if (n0 < Sk) {
+      gp.issue(Kb, ks, n0, Sk, D, kb, wv);
+      gp.issue(Vb, vs, n0, Sk, D, vb, wv);
+    }
+    bf16x8 qf[DP / 16], gf[DP / 16];
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) {
+      qf[s] = __builtin_bit_cast(bf16x8, gload8(Qb + (int64_t)qrow * qs, 16 * s + 8 * hl, D, qvalid));
+      gf[s] = __builtin_bit_cast(bf16x8, gload8(Gb + (int64_t)qrow * os, 16 * s + 8 * hl, D, qvalid));
+    }
+    const float lse = qvalid ? LSE[(int64_t)bh * Sq + qrow] : INFINITY;
+    float dlt = 0.f;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) {
+      const u16x8 ov = gload8(Ob + (int64_t)qrow * os, 16 * s + 8 * hl, D, qvalid);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt += bf2f(ov[j]) * (float)gf[s][j];
+    }
+    dlt += __shfl_xor(dlt, 32, 64);
+    const uint32_t qoff = (uint32_t)qrow * (uint32_t)Sk;
+    f32x16 dq[DP / 32];
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) dq[d] = {};
+    __syncthreads();   // (waits for this wave's LDS-DMA first: the pair's K / V tile is in LDS)
+    if (n0 < Sk) {
+      f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+#pragma unroll
+      for (int s = 0; s < DP / 16; ++s) {
+        bf16x8 ak0 = lds_row8<DP>(kb, l32, 2 * s + hl);
+        bf16x8 ak1 = lds_row8<DP>(kb, 32 + l32, 2 * s + hl);
+        bf16x8 av0 = lds_row8<DP>(vb, l32, 2 * s + hl);
+        bf16x8 av1 = lds_row8<DP>(vb, 32 + l32, 2 * s + hl);
+        s0 = mfma32(ak0, qf[s], s0);
+        s1 = mfma32(ak1, qf[s], s1);
+        p0 = mfma32(av0, gf[s], p0);
+        p1 = mfma32(av1, gf[s], p1);
+      }
+      uint32_t keep = 0xffffffffu;
+      if (DROP) {
+        keep = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t kr = (uint32_t)(n0 + (r & 3) + 8 * (r >> 2) + 4 * hl);
+          keep |= (hash_lo(dkey, qoff + kr) >= dthr ? 1u : 0u) << r;
+          keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
+        }
+      }
+      auto elems = [&](auto masked) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            float sv = hf ? s1[r] : s0[r];
+            float dpv = hf ? p1[r] : p0[r];
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse));
+            if constexpr (decltype(masked)::value) {
+              if (n0 + 32 * hf + kr >= Sk) p = 0.f;
+            }
+            if (DROP) dpv = (keep >> (16 * hf + r)) & 1u ? dpv * dinv : 0.f;
+            const float dsv = p * (dpv - dlt);
+            if (hf) s1[r] = dsv; else s0[r] = dsv;
+          }
+        }
+      };
+      if (n0 + 64 > Sk) elems(std::true_type{});
+      else elems(std::false_type{});
+      const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 1), d10 = pack8(s1, 0), d11 = pack8(s1, 1);
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+        const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
+        bf16x8 a;
+        a = cat44(lds_tr4<DP>(kb, 0 + 4 * hl, c0), lds_tr4<DP>(kb, 8 + 4 * hl, c0));
+        dq[d] = mfma32(a, d00, dq[d]);
+        a = cat44(lds_tr4<DP>(kb, 16 + 4 * hl, c0), lds_tr4<DP>(kb, 24 + 4 * hl, c0));
+        dq[d] = mfma32(a, d01, dq[d]);
+        a = cat44(lds_tr4<DP>(kb, 32 + 4 * hl, c0), lds_tr4<DP>(kb, 40 + 4 * hl, c0));
+        dq[d] = mfma32(a, d10, dq[d]);
+        a = cat44(lds_tr4<DP>(kb, 48 + 4 * hl, c0), lds_tr4<DP>(kb, 56 + 4 * hl, c0));
+        dq[d] = mfma32(a, d11, dq[d]);
+      }
+    }
+    // the half = 1 pair hands its partial dQ^T to the half = 0 pair
+    __syncthreads();
+    float* xo = reinterpret_cast<float*>(smem) + sub * (DP / 32 * 16 * 64);
+    if (half == 1) {
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) xo[(d * 16 + r) * 64 + lane] = dq[d][r];
+    }
+    __syncthreads();
+    if (half == 0) {
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) dq[d][r] += xo[(d * 16 + r) * 64 + lane];
+    }
+    if (CSQ != nullptr) {
+      __syncthreads();   // the hand-off area is free
+      wg_colsum_atomic<DP>(dq, scale, qvalid && half == 0, reinterpret_cast<float*>(smem), CSQ + (int64_t)h * D, D);
+    }
+    if (qvalid && half == 0) {
+      bf16_t* drow = dQ + ((int64_t)b * Sq + qrow) * dqs + (int64_t)h * D;
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = 32 * d + 8 * g + 4 * hl;
+          if (col < D) {
+            u16x4 pk;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pk[e] = f2bf(dq[d][4 * g + e] * scale);
+            *reinterpret_cast<u16x4*>(drow + col) = pk;
+          }
+        }
+      }
+    }
+    return;
+  }
+
+  // ================================= dK / dV role =================================
+  constexpr int BUFB = (SEQ_O ? 2 : 3) * TILE + 512;   // Q, dO, (O), lse[64], delta[64]
+  const int k0 = ((int)blockIdx.x - nq) * 64;
+  const int key = k0 + 32 * sub + l32;
+  const bool kvalid = key < Sk;
+  const int q0 = 64 * half;                  // this pair's query tile
+  char* qb = smem + half * BUFB;
+  char* gb = qb + TILE;
+  char* ob = SEQ_O ? qb : qb + 2 * TILE;     // O (d_h 256: in Q's slot until delta is done)
+  float* ls = reinterpret_cast<float*>(qb + (SEQ_O ? 2 : 3) * TILE);
+  float* dl = ls + 64;
+  const bool qtile = q0 < Sq;
+  if (qtile) {
+    if (!SEQ_O) gp.issue(Qb, qs, q0, Sq, D, qb, wv);
+    gp.issue(Gb, os, q0, Sq, D, gb, wv);
+    gp.issue(Ob, os, q0, Sq, D, ob, wv);
+    if (wv == 0) {   // per-row LSE, 4 bytes per lane (rows past Sq are masked in the math)
+      const int q = min(q0 + lane, Sq - 1);
+      __builtin_amdgcn_global_load_lds((const void*)(LSE + (int64_t)bh * Sq + q),
+                                       (__attribute__((address_space(3))) void*)ls, 4, 0, 0);
+    }
+  }
+  bf16x8 kf[DP / 16], vf[DP / 16];
+  {
+    const bf16_t* Krow = Kb + (int64_t)key * ks;
+    const bf16_t* Vrow = Vb + (int64_t)key * vs;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) {
+      kf[s] = __builtin_bit_cast(bf16x8, gload8(Krow, 16 * s + 8 * hl, D, kvalid));
+      vf[s] = __builtin_bit_cast(bf16x8, gload8(Vrow, 16 * s + 8 * hl, D, kvalid));
+    }
+  }
+  f32x16 dk[DP / 32], dv[DP / 32];
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d) {
+    dk[d] = {};
+    dv[d] = {};
+  }
+  __syncthreads();   // the pair's dO / O (/ Q) tiles and LSE are in LDS
+  // delta of the tile's 64 rows: the pair's 128 lanes, two per row (16-byte chunks c, c + 2, ...)
+  if (qtile) {
+    const int t = 64 * sub + lane, row = t >> 1, part = t & 1;
+    float acc = 0.f;
+#pragma unroll
+    for (int ch = part; ch < DP / 8; ch += 2) {
+      if (8 * ch < D) {
+        const bf16x8 gv = lds_row8<DP>(gb, row, ch), ov = lds_row8<DP>(ob, row, ch);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc += (float)gv[j] * (float)ov[j];
+      }
+    }
+    acc += __shfl_xor(acc, 1, 64);
+    if (part == 0) dl[row] = acc;
+  }
+  __syncthreads();
+  if constexpr (SEQ_O) {   // O is consumed: Q into its slot
+    if (qtile) gp.issue(Qb, qs, q0, Sq, D, qb, wv);
+    __syncthreads();
+  }
+  if (qtile) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f32x16 sacc = {}, pacc = {};
+#pragma unroll
+      for (int s = 0; s < DP / 16; ++s) {
+        bf16x8 aq = lds_row8<DP>(qb, 32 * u + l32, 2 * s + hl);
+        bf16x8 ag = lds_row8<DP>(gb, 32 * u + l32, 2 * s + hl);
+        sacc = mfma32(aq, kf[s], sacc);
+        pacc = mfma32(ag, vf[s], pacc);
+      }
+      f32x16 pm, ds;
+      float4 lsv[4], dlv[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        lsv[g] = *reinterpret_cast<const float4*>(ls + 32 * u + 8 * g + 4 * hl);
+        dlv[g] = *reinterpret_cast<const float4*>(dl + 32 * u + 8 * g + 4 * hl);
+      }
+      uint32_t keep = 0xffffu;
+      if (DROP) {
+        keep = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t q = (uint32_t)(q0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl);
+          keep |= (hash_lo(dkey, q * (uint32_t)Sk + (uint32_t)key) >= dthr ? 1u : 0u) << r;
+        }
+      }
+      auto elems = [&](auto masked) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int q = q0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl;
+          const float lv = (&lsv[r >> 2].x)[r & 3], dv_ = (&dlv[r >> 2].x)[r & 3];
+          float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -lv));
+          if constexpr (decltype(masked)::value) {
+            if (q >= Sq) p = 0.f;
+          }
+          float dpv = pacc[r];
+          float pd = p;
+          if (DROP) {
+            const float msk = (keep >> r) & 1u ? dinv : 0.f;
+            pd = p * msk;
+            dpv = dpv * msk;
+          }
+          pm[r] = pd;
+          ds[r] = p * (dpv - dv_);
+        }
+      };
+      if (q0 + 64 > Sq) elems(std::true_type{});
+      else elems(std::false_type{});
+      const bf16x8 pb0 = pack8(pm, 0), pb1 = pack8(pm, 1);
+      const bf16x8 db0 = pack8(ds, 0), db1 = pack8(ds, 1);
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+        const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
+        const int rb = 32 * u + 4 * hl;
+        bf16x8 ag0 = cat44(lds_tr4<DP>(gb, rb + 0, c0), lds_tr4<DP>(gb, rb + 8, c0));
+        bf16x8 ag1 = cat44(lds_tr4<DP>(gb, rb + 16, c0), lds_tr4<DP>(gb, rb + 24, c0));
+        dv[d] = mfma32(ag0, pb0, dv[d]);
+        dv[d] = mfma32(ag1, pb1, dv[d]);
+        bf16x8 aq0 = cat44(lds_tr4<DP>(qb, rb + 0, c0), lds_tr4<DP>(qb, rb + 8, c0));
+        bf16x8 aq1 = cat44(lds_tr4<DP>(qb, rb + 16, c0), lds_tr4<DP>(qb, rb + 24, c0));
+        dk[d] = mfma32(aq0, db0, dk[d]);
+        dk[d] = mfma32(aq1, db1, dk[d]);
+      }
+    }
+  }
+  // the half = 1 pair hands its partial dK^T / dV^T to the half = 0 pair
+  __syncthreads();
+  float* xk = reinterpret_cast<float*>(smem) + sub * (2 * DP / 32 * 16 * 64);
+  float* xv = xk + DP / 32 * 16 * 64;
+  if (half == 1) {
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        xk[(d * 16 + r) * 64 + lane] = dk[d][r];
+        xv[(d * 16 + r) * 64 + lane] = dv[d][r];
+      }
+  }
+  __syncthreads();
+  if (half == 0) {
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        dk[d][r] += xk[(d * 16 + r) * 64 + lane];
+        dv[d][r] += xv[(d * 16 + r) * 64 + lane];
+      }
+  }
+  if (CSK != nullptr) {
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+    wg_colsum_atomic<DP>(dk, scale, kvalid && half == 0, red, CSK + (int64_t)h * D, D);
+    __syncthreads();
+    wg_colsum_atomic<DP>(dv, 1.f, kvalid && half == 0, red, CSV + (int64_t)h * D, D);
+  }
+  if (kvalid && half == 0) {
+    bf16_t* dkrow = dK + ((int64_t)b * Sk + key) * dks + (int64_t)h * D;
+    bf16_t* dvrow = dV + ((int64_t)b * Sk + key) * dvs + (int64_t)h * D;
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 32 * d + 8 * g + 4 * hl;
+        if (col < D) {
+          u16x4 a, bb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] = f2bf(dk[d][4 * g + e] * scale);
+            bb[e] = f2bf(dv[d][4 * g + e]);
+          }
+          *reinterpret_cast<u16x4*>(dkrow + col) = a;
+          *reinterpret_cast<u16x4*>(dvrow + col) = bb;
+        }
+      }
+    }
+  }
+}
+
+// LDS of attn_bwd_short_kernel: max over the roles' tiles and hand-off areas
+template <int DP>
+constexpr size_t short_bwd_lds() {
+  constexpr size_t tile = 64 * DP * 2;
+  constexpr size_t dq_tiles = 4 * tile;
+  constexpr size_t dkdv_tiles = 2 * ((DP > 128 ? 2 : 3) * tile + 512);
+  constexpr size_t xq = 2 * (DP / 32) * 16 * 64 * 4;
+  constexpr size_t xkv = 2 * xq;
+  constexpr size_t red = 4 * DP * 4;
+  size_t m = dq_tiles;
+  m = dkdv_tiles > m ? dkdv_tiles : m;
+  m = xq > m ? xq : m;
+  m = xkv > m ? xkv : m;
+  m = red > m ? red : m;
+  return m;
+}
+
 // ==========================================================================================
 // launchers
 // ==========================================================================================
@@ -1004,6 +1377,21 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
                       float* delta, void* dq, void* dk, void* dv, int B, int Sq, int Sk, int H, int Hkv, int D,
                       int64_t qs, int64_t ks, int64_t vs, int64_t os, int64_t dqs, int64_t dks, int64_t dvs,
                       float scale, float p, uint64_t seed, float* csq, float* csk, float* csv, hipStream_t st) {
+  // short non-causal problems: dQ and dK/dV in one launch (MIPIPE_ATTN_BWD_SHORT=0: the
+  // two-kernel path, for A/B)
+  if constexpr (!CAUSAL && DP <= 128) {   // (d_h 256: the role-merged register file spills)
+    static const bool short_off = [] { const char* e = getenv("MIPIPE_ATTN_BWD_SHORT"); return e && e[0] == '0'; }();
+    if (!short_off && Sq <= 128 && Sk <= 128 && H == Hkv) {
+      constexpr size_t lds = short_bwd_lds<DP>();
+      auto kern = attn_bwd_short_kernel<DP, DROP>;
+      if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      dim3 grid((Sq + 63) / 64 + (Sk + 63) / 64, B * H);
+      kern<<<grid, 256, lds, st>>>((const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (const bf16_t*)o,
+                                   (const bf16_t*)dout, lse, (bf16_t*)dq, (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, H, D, qs,
+                                   ks, vs, os, dqs, dks, dvs, scale, p, seed, csq, csk, csv);
+      return (int)hipGetLastError();
+    }
+  }
   {
     const size_t lds = (DP <= 128 ? 4 : 2) * 2 * 64 * DP * 2;
     auto kern = attn_bwd_dq_kernel<DP, CAUSAL, DROP>;

@@ -206,7 +206,9 @@ def test_swiglu_and_rope():
 ATTN = [  # B, S, H, Hkv, D, causal
     (2, 256, 4, 4, 64, True), (2, 256, 4, 4, 64, False), (1, 200, 2, 2, 64, True),
     (2, 128, 8, 8, 96, False), (1, 256, 4, 2, 128, True), (1, 128, 4, 4, 192, False), (1, 1024, 2, 2, 64, True),
-    (1, 200, 4, 2, 128, True), (2, 136, 4, 4, 64, False)]
+    (1, 200, 4, 2, 128, True), (2, 136, 4, 4, 64, False),
+    # short non-causal (one-launch backward): partial second tile, one tile only, GQA (two-kernel path)
+    (3, 100, 4, 4, 64, False), (2, 64, 4, 4, 128, False), (2, 128, 4, 2, 96, False)]
 
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,causal", ATTN)
@@ -291,6 +293,43 @@ def test_attention_dropout_mask_exact(p):
     # distinct masks per head and per batch element
     assert not torch.equal(m_f[:, :, 0], m_f[:, :, 1])
     assert not torch.equal(m_f[0], m_f[1])
+
+
+@pytest.mark.parametrize("S,D", [(128, 128), (96, 96), (64, 64)])
+def test_attention_dropout_bwd_matches_reference(S, D):
+    """Dropout attention forward + backward against an f32 reference that uses the kernels'
+    own mask (recovered exactly as in test_attention_dropout_mask_exact: q = k = 0, V = I).
+    Non-causal S <= 128 runs the one-launch short backward (dQ and dK/dV roles in one grid)."""
+    torch.manual_seed(0)
+    B, H, p, seed = 2, 4, 0.1, 4321
+    T = B * S
+    z = torch.zeros(T, H * D, dtype=torch.bfloat16, device=DEV)
+    eye = torch.eye(S, D, dtype=torch.bfloat16, device=DEV).repeat(B, H)
+    om = torch.empty_like(z)
+    lse = torch.empty(B * H * S, device=DEV)
+    ops.attn_fwd(z, z, eye, om, lse, B, S, S, H, H, D, False, p_drop=p, seed=seed)
+    keep = (om.float().view(B, S, H, S) > 0).permute(0, 2, 1, 3).float().cpu() / (1 - p)   # [B, H, q, k]
+    q, k, v, do = (rnd(T, H * D).to(DEV) for _ in range(4))
+    o = torch.empty_like(q)
+    ops.attn_fwd(q, k, v, o, lse, B, S, S, H, H, D, False, p_drop=p, seed=seed)
+    dq, dk, dv = torch.zeros_like(q), torch.zeros_like(q), torch.zeros_like(q)
+    dbias = torch.zeros(3 * H * D, device=DEV)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, S, H, H, D, False, p_drop=p, seed=seed, dbias=dbias)
+    torch.cuda.synchronize()
+    hd = lambda t: t.float().cpu().view(B, S, H, D).permute(0, 2, 1, 3)   # noqa: E731
+    Q, K, V, dO, O = hd(q), hd(k), hd(v), hd(do), hd(o)
+    sc = 1.0 / math.sqrt(D)
+    P = torch.softmax(Q @ K.transpose(-1, -2) * sc, -1)
+    O_ref = (P * keep) @ V
+    dV = (P * keep).transpose(-1, -2) @ dO
+    dP = (dO @ V.transpose(-1, -2)) * keep
+    dS = P * (dP - (dO * O).sum(-1, keepdim=True))
+    dQ, dK = dS @ K * sc, dS.transpose(-1, -2) @ Q * sc
+    close(O, O_ref, atol=2e-2, rtol=2e-2)
+    for got, ref in ((dq, dQ), (dk, dK), (dv, dV)):
+        close(hd(got), ref, atol=5e-2, rtol=5e-2)
+    sums = torch.cat([dq.float().sum(0), dk.float().sum(0), dv.float().sum(0)]).cpu()
+    close(dbias.cpu(), sums, atol=0.05 * T ** 0.5, rtol=2e-2)
 
 
 @pytest.mark.parametrize("p", [0.1, 0.3])
