@@ -17,9 +17,9 @@ m=4), one process per GPU (RCCL) -- or on CPU/gloo -- and writes
     MIPIPE_DIST_BACKEND=gloo python tools/ref_sweep.py --device cuda ...  # ranks share 1 GPU
                                                                           # (timings meaningless)
 
-Precision: ``--engine native`` runs bf16 HIP kernels; ``--engine torch`` runs the
-reference's own nn.Module graph in f32 (ATen) -- only that one is a same-precision
-comparison with the reference's fp32 numbers.
+Precision: ``--engine native`` runs the HIP kernels at ``--precision`` (default fp32, the
+reference's precision: f32 MFMA GEMMs, f32 flash attention, ...); ``--engine torch`` runs the
+reference's own nn.Module graph in f32 on ATen.
 """
 import argparse
 import json
@@ -83,6 +83,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--timeout", type=float, default=600.0)
+    ap.add_argument("--precision", default="fp32", choices=["fp32", "bf16"],
+                    help="native engine compute precision (fp32 = the reference's)")
     ap.add_argument("--out", default=None, help="path prefix: writes <out>.md and <out>.json")
     a = ap.parse_args()
     import torch
@@ -93,14 +95,14 @@ def main():
     df = compat.run_all_experiments(n_heads_list=tuple(a.heads), n_layers_list=tuple(a.layers),
                                     num_processes_list=tuple(a.procs), schedules=tuple(a.schedules),
                                     num_iterations=a.iters, batch_size=a.batch, seq_length=a.seq, device=dev,
-                                    engine=a.engine, timeout=a.timeout)
+                                    engine=a.engine, timeout=a.timeout, precision=a.precision)
     eff = compat.compute_speedup_and_efficiency(df) if len(df) else df
     ref_thr, ref_spd = reference_tables()
     engine = a.engine if a.engine != "auto" else ("native" if dev == "cuda" else "torch")
     header = (f"## Reference sweep on this framework: device={dev}, engine={engine} "
-              f"({'bf16 HIP kernels' if engine == 'native' and dev == 'cuda' else 'f32'}), batch {a.batch} x seq "
+              f"({a.precision + ' HIP kernels' if engine == 'native' and dev == 'cuda' else 'f32 ATen'}), batch {a.batch} x seq "
               f"{a.seq}, m=4, {a.iters} timed iterations after 2 warmup (nb:345-392)"
-              + (", gloo ranks sharing one GPU (timings not meaningful)"
+              + (", all P ranks sharing ONE GPU, p2p staged through host memory by gloo (a lower bound for P GPUs)"
                  if os.environ.get("MIPIPE_DIST_BACKEND") == "gloo" and dev == "cuda" else ""))
     text = fmt_table(df, eff, ref_thr, ref_spd, header) if len(df) else header + "\n(no successful runs)\n"
     print(text)
