@@ -332,6 +332,13 @@ def run(a) -> None:
             lv = torch.tensor([loss_val if loss_val is not None else 0.0], device=device, dtype=torch.float64)
             dist.all_reduce(lv, op=dist.ReduceOp.SUM)
             loss_val = float(lv.item()) / dp
+    hbm_peak = None
+    if gpu:
+        with wd.step(init_to):
+            hp = torch.tensor([torch.cuda.max_memory_allocated(device) / 2 ** 30], device=device, dtype=torch.float64)
+            if world > 1:
+                dist.all_reduce(hp, op=dist.ReduceOp.MAX)
+            hbm_peak = round(float(hp.item()), 1)
     flops = cfg.flops_per_token(a.seq) * value
     rt = trainer.runtime
     out = {
@@ -353,6 +360,7 @@ def run(a) -> None:
         "bubble_source": src,
         "analytic_bubble": round(analytic_bubble(trainer.schedule, pp, m, trainer.v), 4),
         "model_tflops_per_gpu": round(flops / world / 1e12, 1),
+        "hbm_peak_gb_per_gpu": hbm_peak,   # max over ranks of the caching allocator's peak
         "attempt": attempt,
         "config": {"model": a.model, "params": cfg.n_params(), "global_batch": gb, "seq_len": a.seq,
                    "micro_batch": a.mbs, "microbatches": m, "schedule": trainer.schedule, "v": trainer.v,
