@@ -5,6 +5,7 @@ import contextlib
 import importlib.util
 import math
 import os
+import threading
 from typing import Optional, Tuple
 
 import torch
@@ -541,28 +542,43 @@ def linear_f32(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = Non
     return _LinearF32.apply(x, w, b)
 
 
+# f32_linears: ONE process-wide dispatcher is installed over torch.nn.functional.linear the
+# first time the block is entered (and never removed); it routes to the f32 MFMA GEMM only
+# while the CALLING THREAD is inside an f32_linears() block (a thread-local depth), so
+# other threads and modules outside the block keep ATen, and nested / concurrent blocks
+# never restore a stale function over each other.
+_F32_TLS = threading.local()
+_F32_LOCK = threading.Lock()
+_F32_ORIG = None
+
+
+def _f32_linear_dispatch(input, weight, bias=None):
+    if (getattr(_F32_TLS, "depth", 0) > 0 and input.is_cuda and input.dtype == torch.float32 and
+            weight.dtype == torch.float32 and (bias is None or bias.dtype == torch.float32)):
+        return _LinearF32.apply(input, weight, bias)
+    return _F32_ORIG(input, weight, bias)
+
+
 @contextlib.contextmanager
 def f32_linears():
-    """Within the block, ``torch.nn.functional.linear`` on f32 GPU tensors runs on
-    :func:`linear_f32`: every nn.Linear and every nn.MultiheadAttention projection
-    (torch's multi_head_attention_forward calls the module-level ``linear``) of an f32
-    module, forward and backward.  Other dtypes / CPU keep ATen."""
-    import torch.nn.functional as F
-    orig = F.linear
+    """Within the block, ``torch.nn.functional.linear`` on f32 GPU tensors called from this
+    thread runs on :func:`linear_f32`: every nn.Linear and every nn.MultiheadAttention
+    projection (torch's multi_head_attention_forward calls the module-level ``linear``) of
+    an f32 module, forward and backward.  Other dtypes / CPU / other threads keep ATen."""
+    global _F32_ORIG
     if not ext_available():
         yield
         return
-
-    def lin(input, weight, bias=None):
-        if (input.is_cuda and input.dtype == torch.float32 and weight.dtype == torch.float32 and
-                (bias is None or bias.dtype == torch.float32)):
-            return _LinearF32.apply(input, weight, bias)
-        return orig(input, weight, bias)
-    F.linear = lin
+    import torch.nn.functional as F
+    with _F32_LOCK:
+        if _F32_ORIG is None:
+            _F32_ORIG = F.linear
+            F.linear = _f32_linear_dispatch
+    _F32_TLS.depth = getattr(_F32_TLS, "depth", 0) + 1
     try:
         yield
     finally:
-        F.linear = orig
+        _F32_TLS.depth -= 1
 
 
 # MIPIPE_WGRAD_GROUP=0: every weight-gradient GEMM of a job list in its own launch

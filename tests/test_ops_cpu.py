@@ -138,3 +138,26 @@ def test_swiglu_rope_embedding_adamw():
     m, v = torch.zeros(50), torch.zeros(50)
     ops.adamw_(pf, gf, m, v, None, 50, 1e-2, 0.9, 0.95, 1e-8, 0.1, 1)
     torch.testing.assert_close(pf, p.detach(), atol=1e-6, rtol=1e-6)
+
+
+def test_f32_linears_is_thread_local():
+    """ops.f32_linears() installs one dispatcher over F.linear and routes only the calling
+    thread's f32 GPU linears while inside the block (nested blocks count depth; other
+    threads and CPU tensors keep ATen)."""
+    import threading
+    from mipipe.ops import kernels as K
+    if not K.ext_available():
+        pytest.skip("extension not built")
+    seen = {}
+    with K.f32_linears():
+        seen["main"] = K._F32_TLS.depth
+        t = threading.Thread(target=lambda: seen.__setitem__("other", getattr(K._F32_TLS, "depth", 0)))
+        t.start()
+        t.join()
+        with K.f32_linears():
+            seen["nested"] = K._F32_TLS.depth
+        x, w, b = torch.randn(4, 8), torch.randn(3, 8), torch.randn(3)
+        torch.testing.assert_close(F.linear(x, w, b), x @ w.t() + b)   # CPU: ATen
+    seen["after"] = K._F32_TLS.depth
+    assert seen == {"main": 1, "other": 0, "nested": 2, "after": 0}
+    assert F.linear is K._f32_linear_dispatch   # installed once, never swapped back and forth
