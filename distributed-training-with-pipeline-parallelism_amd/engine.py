@@ -68,6 +68,10 @@ class FlatAdamW:
         self.v = [torch.zeros_like(a.opt_views()[0]) for a in arenas]
         dev = arenas[0].device if arenas else torch.device("cpu")
         self.sumsq = torch.zeros(1, device=dev, dtype=torch.float32)
+        # partial sum of squares of the arenas ZeRO-sharded over DP replicas: each replica
+        # holds a disjoint block, so it is summed over DP before joining the rest
+        self.dp_sharded = any(a.shard is not None and a.shard_scope == "dp" for a in arenas)
+        self.sumsq_dp = torch.zeros(1, device=dev, dtype=torch.float32)
 
     def step(self, lr: Optional[float] = None) -> None:
         self.step_count += 1
@@ -75,11 +79,13 @@ class FlatAdamW:
         use_clip = self.max_norm and self.max_norm > 0
         if use_clip:
             self.sumsq.zero_()
+            if self.dp_sharded:
+                self.sumsq_dp.zero_()
             for i, a in enumerate(self.arenas):
                 if i in self.norm_skip:
                     continue
                 if a.shard is not None:     # this rank's (reduced) range of a sharded arena
-                    ops.sumsq(a.opt_views()[1], self.sumsq)
+                    ops.sumsq(a.opt_views()[1], self.sumsq_dp if a.shard_scope == "dp" else self.sumsq)
                     continue
                 if (self.merged_norm and len(a.grad_lanes) > 1 and a.merged_sumsq is not None
                         and i not in self.norm_exclude):
@@ -92,6 +98,9 @@ class FlatAdamW:
                     lo = max(lo, off + n)
                 if lo < a.grad.numel():
                     ops.sumsq(a.grad[lo:] if lo else a.grad, self.sumsq)
+            if self.dp_sharded:
+                self.coll.all_reduce(self.sumsq_dp, "dp").wait()
+                self.sumsq.add_(self.sumsq_dp)
             if self.coll is not None:
                 self.coll.all_reduce(self.sumsq, "pp").wait()
             elif self.pp_group is not None and dist.get_world_size(self.pp_group) > 1:
@@ -105,7 +114,7 @@ class FlatAdamW:
                 lo, hi, _ = a.shard
                 a.grad[:lo].zero_()
                 a.grad[hi:].zero_()
-                self.coll.all_gather(a.w16, "pp").wait()
+                self.coll.all_gather(a.w16, a.shard_scope).wait()
             a.refresh_transposes()
 
     def state_dict(self):
@@ -135,7 +144,8 @@ def max_inflight_microbatches(order, stages) -> int:
 
 
 def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, seq_len: int, device,
-                   head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1) -> dict:
+                   head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1,
+                   stage_shards: int = 1) -> dict:
     """HBM plan of one pipeline rank and the recompute decision of ``recompute="auto"``:
     recompute only if the activation stash would not fit ``budget_frac`` of the device.
 
@@ -145,7 +155,8 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
             microbatch's with MIPIPE_HEAD_CHUNK=0) + 4 GB workspace.
     The distributed head with ZeRO-1 (``head_shards`` = PP) keeps its f32 master and Adam
     moments (12 of the 20 bytes) for 1 / head_shards of the matrix: ``head_optimizer_bytes``
-    is that per-rank optimizer state, ``head_state_bytes`` all of the head's.
+    is that per-rank optimizer state, ``head_state_bytes`` all of the head's.  ZeRO-1 over DP
+    (``stage_shards`` = DP) does the same for the stage parameters: 8 + 12 / dp bytes each.
     Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute."""
     T = mbs * seq_len
     nlayers = sum(layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages)
@@ -156,7 +167,7 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     inflight = max_inflight_microbatches(order, set(my_stages))
     from .models.native import _HEAD_CHUNK
     logit_rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
-    fixed = 20.0 * nparams + head_state + 2.0 * logit_rows * cfg.vocab_padded + 4e9
+    fixed = (8.0 + 12.0 / max(1, stage_shards)) * nparams + head_state + 2.0 * logit_rows * cfg.vocab_padded + 4e9
     full = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=False)
     rec = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=True) + \
         cfg.stash_bytes_per_layer(T, recompute=False)
@@ -251,6 +262,9 @@ class PipelineTrainer:
         # recompute="auto": HBM plan from the schedule's in-flight microbatches (288 GB per
         # MI355X usually holds the whole stash, and recompute costs a forward per layer)
         self.memory_plan = None
+        # ZeRO-1 over DP replicas (see below): known before the HBM plan
+        self.dp_zero = (self.mesh.dp > 1 and os.environ.get("MIPIPE_DP_ZERO", "1") != "0"
+                        and not (tied_pp or self._tie_local))
         if recompute == "auto":
             order = (orders if orders is not None else
                      generate(self.schedule, pp, n_microbatches, v, style)).get(self.mesh.pp_rank, [])
@@ -258,13 +272,20 @@ class PipelineTrainer:
                            (mbs * seq_len if (num_stages - 1) in my_stages else 0))
             self.memory_plan = plan_recompute(cfg, layer_ranges, my_stages, order, mbs, seq_len, self.device,
                                               head_tokens=head_tokens,
-                                              head_shards=pp if (self.head_zero and pp > 1) else 1)
+                                              head_shards=pp if (self.head_zero and pp > 1) else 1,
+                                              stage_shards=self.mesh.dp if self.dp_zero else 1)
             recompute = self.memory_plan["recompute"]
         self.recompute = bool(recompute)
+        # ZeRO-1 over DP replicas (MIPIPE_DP_ZERO=0: replicated master / moments, gradient
+        # all-reduced): each replica owns 1/dp of every stage arena -- its f32 master and Adam
+        # moments; REDUCE_GRAD reduce-scatters the gradient into that block and the step
+        # all-gathers the updated weights.  Not with a tied embedding copied across stages
+        # (its two copies' gradients are summed after the DP reduction).  self.dp_zero: above.
         self.stages: List[NativeStage] = []
         for s in my_stages:
             model = NativeModel(cfg, s, num_stages, self.device, layer_range=layer_ranges[s], seed=seed,
-                                recompute=recompute, mbs=mbs, seq_len=seq_len, dtype=dtype, head=self.head)
+                                recompute=recompute, mbs=mbs, seq_len=seq_len, dtype=dtype, head=self.head,
+                                arena_multiple=8 * self.mesh.dp if self.dp_zero else 8)
             egroup = self.mesh.embed_group if (tied_pp and (s == 0 or s == num_stages - 1)) else None
             self.stages.append(NativeStage(model, mbs, seq_len, dp_group=self.mesh.dp_group, embed_group=egroup,
                                            seed=seed + 1000 * self.mesh.dp_rank, graphs=graphs))
@@ -282,6 +303,17 @@ class PipelineTrainer:
                                             if os.environ.get("MIPIPE_LANES", "auto") == "auto"
                                             else max(1, int(os.environ["MIPIPE_LANES"])))
         arenas = [st.arena for st in self.stages]
+        if self.dp_zero:
+            dp, dr = self.mesh.dp, self.mesh.dp_rank
+            for a in arenas:
+                n = a.numel // dp
+
+                def gather_dp(shard, numel=a.numel, lo=dr * n, n=n):
+                    full = torch.empty(numel, dtype=shard.dtype, device=shard.device)
+                    full[lo:lo + n].copy_(shard)
+                    self.coll.all_gather(full, "dp").wait()
+                    return full
+                a.shard_master(dr * n, dr * n + n, gather_dp, scope="dp")
         norm_skip = []
         norm_exclude = {}
         if (tied_pp or self._tie_local) and (num_stages - 1) in my_stages:

@@ -72,6 +72,7 @@ class ParamArena:
         # ZeRO-1 (shard_master): this rank keeps only master[lo:hi] (and the optimizer
         # moments of that range); ``unsharded()`` gathers the full master when needed
         self.shard: Optional[Tuple[int, int, Callable]] = None
+        self.shard_scope: Optional[str] = None   # "pp" (ZeRO-1 head) | "dp" (ZeRO-1 over DP replicas)
         self.n_decay = 0
         for s in specs:
             if s.decay:
@@ -191,10 +192,12 @@ class ParamArena:
             ops.zero_(g)
 
     # ------------------------------------------------------------------ ZeRO-1
-    def shard_master(self, lo: int, hi: int, gather: Callable[[torch.Tensor], torch.Tensor]) -> None:
+    def shard_master(self, lo: int, hi: int, gather: Callable[[torch.Tensor], torch.Tensor],
+                     scope: str = "pp") -> None:
         """Keep only ``master[lo:hi]`` on this rank (``gather(shard) -> full`` rebuilds the
-        whole f32 master: a collective).  bf16 weights and f32 gradients stay full-size
-        (every rank computes with the whole matrix and accumulates its whole gradient)."""
+        whole f32 master: a collective over ``scope``, the group the arena is sharded over).
+        bf16 weights and f32 gradients stay full-size (every rank computes with the whole
+        matrix and accumulates its whole gradient)."""
         if self.shard is not None:
             raise RuntimeError("arena already sharded")
         if not self.w_is_master:
@@ -203,6 +206,7 @@ class ParamArena:
         # updates master[lo:hi] (opt_views) and the step's all-gather of w16 (= master)
         # refreshes the rest -- only the Adam moments are sharded
         self.shard = (int(lo), int(hi), gather)
+        self.shard_scope = scope
 
     @contextlib.contextmanager
     def unsharded(self):
@@ -859,7 +863,7 @@ class NativeModel:
 
     def __init__(self, cfg: NativeConfig, stage_index: int, num_stages: int, device, layer_range=None,
                  seed: int = 0, recompute: bool = False, mbs: int = 1, seq_len: int = 1024, init: bool = True,
-                 dtype=torch.bfloat16, head: Optional[HeadShard] = None):
+                 dtype=torch.bfloat16, head: Optional[HeadShard] = None, arena_multiple: int = 8):
         self.cfg = cfg
         self.stage_index = stage_index
         self.num_stages = num_stages
@@ -903,7 +907,9 @@ class NativeModel:
                 specs.append(ParamSpec("output.weight", (cfg.vocab_padded, d), "normal", True, cfg.init_std, True))
                 if cfg.bias and cfg.cross_attn:
                     specs.append(ParamSpec("output.bias", (cfg.vocab_padded,), "zeros", False))
-        self.arena = ParamArena(specs, self.device, dtype=dtype, seed=seed, init=init)
+        # arena_multiple: 8 x DP when the arena is ZeRO-1-sharded over DP replicas (equal,
+        # 16-byte aligned blocks for the reduce-scatter / all-gather, engine.py)
+        self.arena = ParamArena(specs, self.device, dtype=dtype, seed=seed, init=init, numel_multiple=arena_multiple)
         rope = None
         if cfg.pos == "rope":
             rope = ops.rope_tables(cfg.max_seq_len, cfg.head_dim, cfg.rope_theta, self.device)

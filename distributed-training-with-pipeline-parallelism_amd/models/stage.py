@@ -196,6 +196,10 @@ class NativeStage(StageBase):
             # SUM: the 1/dp average is folded into the AdamW kernel (engine.FlatAdamW).  One
             # call over the flat arena: RCCL pipelines a large all-reduce internally
             if self.coll is not None:
+                if self.arena.shard is not None and self.arena.shard_scope == "dp":
+                    # ZeRO-1 over DP (engine.py): reduce-scatter -- this replica's block of
+                    # the arena is summed; the optimizer updates it and all-gathers weights
+                    return self.coll.reduce_scatter(self.arena.grad, "dp")[0]
                 return self.coll.all_reduce(self.arena.grad, "dp")
             return allreduce_flat(self.arena.grad, self.dp_group, average=False)
         return None

@@ -64,20 +64,26 @@ def save_checkpoint(trainer, path: str, step: Optional[int] = None, extra: Optio
     mesh = trainer.mesh
     opt = trainer.optimizer
     files: Dict[str, List[str]] = {}
+    params, moments = {}, {}
+    head_params, head_moments = {}, {}
+    for arena, slot, tag in _arenas(trainer):
+        # an arena ZeRO-sharded over DP is gathered by all of its replicas (a collective);
+        # everything else only by DP replica 0, which writes
+        if mesh.dp_rank != 0 and not (arena.shard is not None and arena.shard_scope == "dp"):
+            continue
+        is_head = tag == "head"
+        fm, fv = _full(arena, opt.m[slot]), _full(arena, opt.v[slot])
+        with arena.unsharded():
+            if mesh.dp_rank != 0:
+                continue
+            for name in arena.order:
+                p = arena.master_view(name).detach().float().cpu().contiguous()
+                m = _flat_view(fm, arena, name).detach().float().cpu().contiguous()
+                v = _flat_view(fv, arena, name).detach().float().cpu().contiguous()
+                (head_params if is_head else params)[name] = p
+                (head_moments if is_head else moments)[name + ".exp_avg"] = m
+                (head_moments if is_head else moments)[name + ".exp_avg_sq"] = v
     if mesh.dp_rank == 0:
-        params, moments = {}, {}
-        head_params, head_moments = {}, {}
-        for arena, slot, tag in _arenas(trainer):
-            is_head = tag == "head"
-            fm, fv = _full(arena, opt.m[slot]), _full(arena, opt.v[slot])
-            with arena.unsharded():
-                for name in arena.order:
-                    p = arena.master_view(name).detach().float().cpu().contiguous()
-                    m = _flat_view(fm, arena, name).detach().float().cpu().contiguous()
-                    v = _flat_view(fv, arena, name).detach().float().cpu().contiguous()
-                    (head_params if is_head else params)[name] = p
-                    (head_moments if is_head else moments)[name + ".exp_avg"] = m
-                    (head_moments if is_head else moments)[name + ".exp_avg_sq"] = v
         r = mesh.pp_rank
         if params:
             save_file(params, os.path.join(path, f"stage-pp{r}.safetensors"), metadata={"format": FORMAT})

@@ -271,7 +271,8 @@ def _worker(rank, world, pp, dp, schedule, v, native, steps):
         out.update(recorded=r is not None, kinds=r.kinds() if r else [], channels=r.channels() if r else [],
                    colls=r.collectives() if r else [], runs=r.runs if r else 0, reason=tr.runtime.native_reason,
                    n_reduce_grad=sum(1 for st in tr.stages if st.has_grad_reduction(True)),
-                   head=tr.runtime.head_reduce is not None, placement=tr.runtime.coll_placement)
+                   head=tr.runtime.head_reduce is not None, placement=tr.runtime.coll_placement,
+                   dp_zero=tr.dp_zero)
     return out
 
 
@@ -288,9 +289,12 @@ def test_pp4_tape_is_native_and_replays_exactly(schedule, v, dp):
         assert set(kinds) <= {GRAPH, COPY, POST, WAIT, COLL, SYNC}, kinds    # no CALL
         assert kinds.count(POST) > 0 and kinds.count(GRAPH) > 0
         # collectives: REDUCE_HEAD = reduce-scatter over the pipeline (+ the shard's DP
-        # all-reduce), one DP all-reduce per stage at REDUCE_GRAD; deferred to the step end
+        # all-reduce), one DP reduction per stage at REDUCE_GRAD (a reduce-scatter with
+        # ZeRO-1 over DP, else an all-reduce); deferred to the step end
         head_colls = [(2, 1)] + ([(0, 0)] if dp > 1 else [])
-        assert sorted(o["colls"]) == sorted(head_colls + [(0, 0)] * o["n_reduce_grad"]), o["colls"]
+        assert o["dp_zero"] == (dp > 1)
+        grad_coll = (0, 1) if o["dp_zero"] else (0, 0)
+        assert sorted(o["colls"]) == sorted(head_colls + [grad_coll] * o["n_reduce_grad"]), o["colls"]
         last_post = max(i for i, k in enumerate(kinds) if k == POST)
         assert all(i > last_post for i, k in enumerate(kinds) if k == COLL), "collectives after every p2p group"
         assert o["placement"].startswith("step end")
