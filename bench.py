@@ -2,18 +2,19 @@
 """Flagship benchmark: GPT-2 pipeline-parallel training throughput on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model gpt2-small]
-                    [--schedule 1F1B] [--mbs 32] [--seq 1024] [--microbatches M]
+                    [--schedule 1F1B] [--mbs MBS] [--seq 1024] [--microbatches M]
 
 N GPUs = N pipeline stages (PP=N, one process per GPU); for N>1 the driver launches it
 with torch.distributed.run (if launched without it, this script re-launches itself under
-torch.distributed.run).  Work per GPU is fixed as N grows: ``microbatches = 4*N``,
-microbatch = ``mbs`` sequences of ``seq`` tokens, so the global batch grows with N
-("weak" scaling: every GPU runs 4 x mbs sequences through all of its layers per step).
-mbs defaults to 32: 32K-token microbatches (on one GPU mbs 32 runs 944.5K tok/s vs 886.9K
-with mbs 16, profiles/r3_bench_mbs_ab.txt).  m = 4P rather than 2P: the 1F1B bubble
-(P-1)/(m+P-1) at P = 8 drops from 0.30 to 0.18 (planned efficiency of the lowered program
-with the distributed head 0.72 -> 0.83, tools/schedule_table.py); at P = 8 the global batch
-is 1024 x 1024 = 1M tokens.  Each timed step is a full training step: all
+torch.distributed.run).  Work per GPU is fixed as N grows ("weak" scaling): every GPU
+runs 128 sequences of ``seq`` tokens through all of its layers per step, so the global
+batch is 128 N sequences.  A pipeline (N > 1) splits it into ``microbatches = 4*N`` of
+``mbs = 32`` sequences: m = 4P rather than 2P takes the 1F1B bubble (P-1)/(m+P-1) at P = 8
+from 0.30 to 0.18 (planned efficiency of the lowered program with the distributed head
+0.72 -> 0.83, tools/schedule_table.py); at P = 8 the global batch is 1M tokens.  One GPU
+has no bubble to amortise and runs 2 microbatches of 64 (the two microbatch lanes overlap
+them): 990.5K / 991.8K tok/s vs 978.6K / 978.3K as 4 x 32 (profiles/r3_bench_mbs64_ab.txt;
+one stream: 64 -> 978K, 32 -> 929K, 16 -> 880K, profiles/r3_lane1_mbs_ab.txt).  Each timed step is a full training step: all
 microbatch forwards/backwards through the lowered schedule, p2p of activations and
 gradients, grad-norm clip and the fused AdamW update.
 
@@ -70,7 +71,8 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--schedule", default="1F1B")
-    ap.add_argument("--mbs", type=int, default=32)
+    ap.add_argument("--mbs", type=int, default=None,
+                    help="sequences per microbatch (default: 64 on one GPU, 32 with a pipeline)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--dp", type=int, default=1)
@@ -246,7 +248,15 @@ def run(a) -> None:
         pp = world // dp
         if pp * dp != world:
             raise SystemExit(f"--dp {dp} does not divide WORLD_SIZE={world}")
-        m = a.microbatches if a.microbatches is not None else 4 * pp
+        # 128 sequences per GPU per step by default (weak scaling): one GPU runs two
+        # 64-sequence microbatches (no bubble to amortise; the two microbatch lanes overlap),
+        # a pipeline of P ranks 4P microbatches of 32 (1F1B bubble (P-1)/(5P-1))
+        if a.mbs is None:
+            a.mbs = 64 if (pp == 1 and a.microbatches is None) else 32
+            m_default = 2 if pp == 1 else 4 * pp
+        else:
+            m_default = 4 * pp
+        m = a.microbatches if a.microbatches is not None else m_default
         kw = {"vocab_size": a.vocab} if a.vocab else {}
         cfg = NativeConfig.by_name(a.model, **kw)
         gpu = device.type == "cuda"
