@@ -298,10 +298,16 @@ class PipelineTrainer:
                                        scale_grads=True, style=style, profile=profile, orders=orders,
                                        head=head_plan, head_costs=head_costs, stage_costs=stage_costs,
                                        dp=self.mesh.dp, head_reduce_after_stage0=bool(cfg.tie_embeddings))
-        # microbatch lanes (PipelineRuntime.set_lanes): MIPIPE_LANES=auto|1 (off)|n
-        self.lanes = self.runtime.set_lanes(self._auto_lanes(pp, v, graphs, n_microbatches, mbs, seq_len)
-                                            if os.environ.get("MIPIPE_LANES", "auto") == "auto"
-                                            else max(1, int(os.environ["MIPIPE_LANES"])))
+        # microbatch lanes (PipelineRuntime.set_lanes): MIPIPE_LANES=auto|1 (off)|n.  Not with
+        # plain GEMMs on hipBLASLt (MIPIPE_GEMM=blas|auto): its stream-K kernels synchronise
+        # their workgroups and assume all of them resident; a second lane's kernels holding
+        # CUs left a Llama-3 1B step hung in that mode (profiles/r3_model_families_1gpu.txt)
+        from .ops.kernels import GEMM_BACKEND
+        n_lanes = (self._auto_lanes(pp, v, graphs, n_microbatches, mbs, seq_len)
+                   if os.environ.get("MIPIPE_LANES", "auto") == "auto" else max(1, int(os.environ["MIPIPE_LANES"])))
+        if GEMM_BACKEND != "hip" and n_lanes > 1:
+            n_lanes = 1
+        self.lanes = self.runtime.set_lanes(n_lanes)
         arenas = [st.arena for st in self.stages]
         if self.dp_zero:
             dp, dr = self.mesh.dp, self.mesh.dp_rank
