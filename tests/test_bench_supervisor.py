@@ -92,3 +92,19 @@ def test_bench_eight_ranks_gpt2_small_layout():
     assert c["model"] == "gpt2-small" and len(c["layer_split"]) == 8
     assert sum(b - a for a, b in c["layer_split"]) == 12
     assert c["head"].startswith("distributed") and out["bubble_fraction"] is not None
+
+
+def test_bench_default_batch_is_128_sequences_per_gpu():
+    """Weak-scaling contract of bench.py's defaults: 128 sequences per GPU per step -- one
+    GPU as 2 microbatches of 64, a pipeline of N as 4N microbatches of 32 (global 128 N)."""
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--model", "gpt2-tiny", "--vocab", "256", "--seq", "16",
+           "--steps", "1", "--warmup", "1", "--no-bubble"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    c = out["config"]
+    assert (c["micro_batch"], c["microbatches"], c["global_batch"]) == (64, 2, 128)
+    assert out["scaling"] == "weak" and out["n_gpus"] == 1
