@@ -196,6 +196,14 @@ def test_recompute_auto_plan():
         assert zero["head_optimizer_bytes"] <= full["head_optimizer_bytes"] / 8 + 1
         assert full["bytes_no_recompute"] - zero["bytes_no_recompute"] == pytest.approx(
             7 / 8 * full["head_optimizer_bytes"])
+        # ZeRO-1 over DP = 2 (BASELINE config 5): the stage parameters' f32 master + Adam
+        # moments (12 of their 20 bytes) halve per replica
+        l4 = balanced_layer_ranges(cfg, 4, 8192, head_on_last=False)
+        o4 = generate("1F1B", 4, 8, 1, "loop")[1]
+        rep = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0))
+        dpz = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), stage_shards=2)
+        nparams = cfg.layer_params() * (l4[1][1] - l4[1][0])
+        assert rep["bytes_no_recompute"] - dpz["bytes_no_recompute"] == pytest.approx(6.0 * nparams)
     finally:
         E.torch.cuda.get_device_properties = orig
     # 1F1B PP=4: rank 0 holds 4 microbatches in flight, the last rank 1; GPipe holds all m
