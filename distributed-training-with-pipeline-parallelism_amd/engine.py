@@ -31,7 +31,8 @@ from .parallel.headsplit import HeadPlan, head_token_split, plan_head_schedule
 from .parallel.mesh import Mesh, build_mesh
 from .parallel.runtime import PipelineRuntime
 from .parallel.ir import Op
-from .parallel.schedules import REQUIRED_STYLE, SCHEDULES, canonical_name, generate, rank_stages, stage_to_rank
+from .parallel.schedules import (REQUIRED_STYLE, SCHEDULES, WARMUP_EXTRA, canonical_name, generate, rank_stages,
+                                 stage_to_rank)
 
 
 class FlatAdamW:
@@ -250,8 +251,11 @@ class PipelineTrainer:
             chunks = head_token_split(T, rank_load, head_units, align=align)
             head_costs = {r: 3.0 * head_units * chunks[r] / T for r in range(pp) if chunks[r] > 0}
             base = generate(self.schedule, pp, n_microbatches, v, style)
+            sched = self.schedule
+            regen = ((lambda lag: generate(sched, pp, n_microbatches, v, style, warmup_extra=lag))
+                     if sched in WARMUP_EXTRA else None)
             orders, self.head_lag, self.planned_makespan = plan_head_schedule(base, pp, v, style, head_costs,
-                                                                              stage_costs)
+                                                                              stage_costs, regen=regen)
             # no-bubble time in the same units (F = 1, B = 2 per stage-cost unit)
             self.planned_ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * n_microbatches / pp
             head_plan = HeadPlan(chunks, cfg.d_model, runner=self.head.run, dtype=dtype)

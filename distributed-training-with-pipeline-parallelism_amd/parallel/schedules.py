@@ -55,18 +55,20 @@ def rank_stages(rank: int, pp: int, v: int, style: str = "loop") -> List[int]:
 # ----------------------------------------------------------------------------------------
 
 
-def gen_gpipe(pp: int, m: int, v: int = 1, style: str = "loop") -> Dict[int, List[Action]]:
+def gen_gpipe(pp: int, m: int, v: int = 1, style: str = "loop", warmup_extra: int = 0) -> Dict[int, List[Action]]:
     if v != 1:
         raise ValueError("GPipe runs one stage per rank (use LoopedBFS for v>1)")
     return {r: [Action(r, Op.F, i) for i in range(m)] + [Action(r, Op.B, i) for i in range(m)] for r in range(pp)}
 
 
-def gen_1f1b(pp: int, m: int, v: int = 1, style: str = "loop") -> Dict[int, List[Action]]:
+def gen_1f1b(pp: int, m: int, v: int = 1, style: str = "loop", warmup_extra: int = 0) -> Dict[int, List[Action]]:
+    """``warmup_extra``: forwards added to every rank's warmup (deeper 1F1B; m - 1 or more
+    is GPipe).  The distributed head's planner uses it to give the last stage slack."""
     if v != 1:
         raise ValueError("1F1B runs one stage per rank (use Interleaved1F1B for v>1)")
     out = {}
     for r in range(pp):
-        w = min(pp - r - 1, m)
+        w = min(pp - r - 1 + max(0, warmup_extra), m)
         ops = [Action(r, Op.F, i) for i in range(w)]
         for i in range(m - w):
             ops.append(Action(r, Op.F, w + i))
@@ -84,7 +86,12 @@ def interleave_params(pp: int, m: int) -> Tuple[int, int]:
     return rounds, m // rounds
 
 
-def gen_interleaved_1f1b(pp: int, m: int, v: int = 2, style: str = "loop") -> Dict[int, List[Action]]:
+def gen_interleaved_1f1b(pp: int, m: int, v: int = 2, style: str = "loop",
+                         warmup_extra: int = 0) -> Dict[int, List[Action]]:
+    """torch's interleaved order; ``warmup_extra`` forwards are added to every rank's warmup
+    (0 = torch's).  A uniformly deeper warmup keeps the order valid and deadlock-free (the
+    limit is all-forwards-first) and is how the distributed head's planner buys the last
+    stage slack without re-sorting chunks against each other (headsplit.plan_head_schedule)."""
     if style != "loop":
         raise ValueError("Interleaved1F1B's warmup formula assumes loop placement (use LoopedBFS/ZBH1 for 'v')")
     _, mpr = interleave_params(pp, m)
@@ -92,7 +99,7 @@ def gen_interleaved_1f1b(pp: int, m: int, v: int = 2, style: str = "loop") -> Di
     for r in range(pp):
         stages = rank_stages(r, pp, v, style)  # chunk order
         total = m * v
-        warm = min((v - 1) * mpr + 2 * (pp - 1 - r), total)
+        warm = min((v - 1) * mpr + 2 * (pp - 1 - r) + max(0, warmup_extra), total)
         fwd_next = [0] * v
         bwd_next = [0] * v
         ops: List[Action] = []
@@ -288,7 +295,12 @@ def canonical_name(name: str) -> str:
     return _ALIASES[key]
 
 
-def generate(name: str, pp: int, m: int, v: Optional[int] = None, style: str = "loop") -> Dict[int, List[Action]]:
+# generators that take a ``warmup_extra`` (deeper warmup) argument
+WARMUP_EXTRA = ("GPipe", "1F1B", "Interleaved1F1B")
+
+
+def generate(name: str, pp: int, m: int, v: Optional[int] = None, style: str = "loop",
+             warmup_extra: int = 0) -> Dict[int, List[Action]]:
     name = canonical_name(name)
     gen, dv, multi = SCHEDULES[name]
     v = dv if v is None else v
@@ -296,6 +308,10 @@ def generate(name: str, pp: int, m: int, v: Optional[int] = None, style: str = "
         raise ValueError(f"{name} supports one stage per rank")
     if m < 1 or pp < 1 or v < 1:
         raise ValueError("pp, m, v must be >= 1")
+    if warmup_extra:
+        if name not in WARMUP_EXTRA:
+            raise ValueError(f"{name} has no warmup_extra")
+        return gen(pp, m, v, style, warmup_extra=warmup_extra)
     return gen(pp, m, v, style)
 
 

@@ -224,3 +224,61 @@ def test_zbv_valid_lowerable_and_low_bubble(P):
     zbv = simulate(o, P, 2, "v", stage_costs=[0.5] * (2 * P)).bubble
     f1b = simulate(generate("1F1B", P, m, 1, "loop"), P, 1, "loop").bubble
     assert zbv < 0.6 * f1b
+
+
+# ----------------------------------------------------------------------------- deeper warmup
+@pytest.mark.parametrize("name,v", [("1F1B", 1), ("Interleaved1F1B", 2)])
+@pytest.mark.parametrize("P,m", [(2, 4), (4, 4), (4, 16), (8, 32)])
+def test_warmup_extra_orders_valid_and_hang_free(name, v, P, m):
+    """Every extra-warmup depth (0 = torch's order, large = all forwards first) gives a
+    valid, lowerable order with the same ideal-uniform bubble or better."""
+    base = simulate(generate(name, P, m, v), P, v).makespan
+    for extra in (0, 1, 2, 5, m * v):
+        o = generate(name, P, m, v, warmup_extra=extra)
+        validate(o, P, v, m)
+        check_lowered(lower(o, P, v), P * v)
+        assert simulate(o, P, v).makespan <= base + 1e-9
+    assert generate(name, P, m, v, warmup_extra=0) == generate(name, P, m, v)
+
+
+def test_interleaved_m_equals_p_bubble_is_the_interleaved_ideal():
+    """at m == P == 4, v = 2 torch's order runs every forward
+    before the first backward on rank 0 -- but the simulated bubble is the interleaved
+    ideal (P-1)/(v*m+P-1) = 0.273, not GPipe's 0.429: the fill-drain shape costs stash
+    (m*v chunk activations per rank, i.e. m stage-equivalents, as GPipe), not time."""
+    P, m, v = 4, 4, 2
+    o = generate("Interleaved1F1B", P, m, v)
+    assert [a.op for a in o[0][:m * v]] == [Op.F] * (m * v)
+    sim = simulate(o, P, v)
+    assert sim.bubble == pytest.approx(3 / 11, abs=1e-9) and sim.bubble <= 0.30
+    assert simulate(generate("GPipe", P, m), P).bubble == pytest.approx(3 / 7, abs=1e-9)
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_interleaved_with_head_plans_ahead_of_1f1b_and_gpipe(P):
+    """GPT-2 small, m = 4P (bench.py's pipeline config), distributed head: the planner's
+    regenerated deeper-warmup interleaved order beats 1F1B and GPipe in planned efficiency
+    (without regeneration the lag re-sort deadlocks interleaved orders and only lag 0 was
+    feasible: 0.845 at P=2, below 1F1B's 0.912)."""
+    from mipipe.models.config import NativeConfig
+    from mipipe.models.native import balanced_layer_ranges, stage_cost_model
+    from mipipe.parallel.schedules import WARMUP_EXTRA
+    cfg = NativeConfig.gpt2("small")
+    m, seq, T = 4 * P, 1024, 32 * 1024
+    eff = {}
+    for name, v in (("GPipe", 1), ("1F1B", 1), ("Interleaved1F1B", 2)):
+        S = P * v
+        lr = balanced_layer_ranges(cfg, S, seq, head_on_last=False)
+        lc, hu, ec = stage_cost_model(cfg, seq)
+        sc = [(b - a) * lc + (ec if s == 0 else 0.0) + (0.1 if s == S - 1 else 0.0) for s, (a, b) in enumerate(lr)]
+        load = [sum(sc[s] for s in range(S) if s % P == r) for r in range(P)]
+        ch = head_token_split(T, load, hu, align=256)
+        hc = {r: 3.0 * hu * ch[r] / T for r in range(P) if ch[r] > 0}
+        regen = (lambda lag, name=name, v=v: generate(name, P, m, v, warmup_extra=lag)) if name in WARMUP_EXTRA \
+            else None
+        o, lag, mk = plan_head_schedule(generate(name, P, m, v), P, v, "loop", hc, sc, regen=regen)
+        validate(o, P, v, m)
+        check_lowered(lower(o, P, v, "loop", head_costs=hc, stage_costs=sc), S)
+        eff[name] = (3.0 * sum(sc) + sum(hc.values())) * m / P / mk
+    assert eff["Interleaved1F1B"] > max(eff["1F1B"], eff["GPipe"]) + 0.02, eff
+    assert eff["1F1B"] >= eff["GPipe"] - 1e-6, eff
