@@ -1,40 +1,51 @@
 #!/usr/bin/env python3
-"""Flagship benchmark: GPT-2 pipeline-parallel training throughput on MI355X.
+"""Flagship benchmark: GPT-2 pipeline-parallel training throughput on MI355X, with the
+reference's schedule comparison (GPipe vs 1F1B vs Interleaved1F1B) in the same call.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--model gpt2-small]
-                    [--schedule 1F1B] [--mbs MBS] [--seq 1024] [--microbatches M]
+                    [--schedule 1F1B] [--schedules all] [--ref-fp32 auto]
+                    [--mbs MBS] [--seq 1024] [--microbatches M]
 
 N GPUs = N pipeline stages (PP=N, one process per GPU); for N>1 the driver launches it
 with torch.distributed.run (if launched without it, this script re-launches itself under
 torch.distributed.run).  Work per GPU is fixed as N grows ("weak" scaling): every GPU
 runs 128 sequences of ``seq`` tokens through all of its layers per step, so the global
 batch is 128 N sequences.  A pipeline (N > 1) splits it into ``microbatches = 4*N`` of
-``mbs = 32`` sequences: m = 4P rather than 2P takes the 1F1B bubble (P-1)/(m+P-1) at P = 8
-from 0.30 to 0.18 (planned efficiency of the lowered program with the distributed head
-0.72 -> 0.83, tools/schedule_table.py); at P = 8 the global batch is 1M tokens.  One GPU
-has no bubble to amortise and runs 2 microbatches of 64 (the two microbatch lanes overlap
-them): 990.5K / 991.8K tok/s vs 978.6K / 978.3K as 4 x 32 (profiles/r3_bench_mbs64_ab.txt;
-one stream: 64 -> 978K, 32 -> 929K, 16 -> 880K, profiles/r3_lane1_mbs_ab.txt).  Each timed step is a full training step: all
-microbatch forwards/backwards through the lowered schedule, p2p of activations and
+``mbs = 32`` sequences (1F1B bubble (P-1)/(5P-1)); at P = 8 the global batch is 1M tokens.
+One GPU has no bubble to amortise and runs 2 microbatches of 64 (the two microbatch lanes
+overlap them; profiles/r3_bench_mbs64_ab.txt).  Each timed step is a full training step:
+all microbatch forwards/backwards through the lowered schedule, p2p of activations and
 gradients, grad-norm clip and the fused AdamW update.
+
+One call measures, each in a fresh child process group (so one can never cost another):
+  1. the headline (``value``, ``ms_per_step``, ``config``): ``--schedule`` (1F1B);
+  2. ``schedules``: GPipe, 1F1B and Interleaved1F1B (v=2) on the same model, batch and
+     microbatches -- tok/s, measured + analytic bubble, speedup vs GPipe, planned
+     efficiency, head lag, HBM peak, p2p bytes per step (the reference's whole result,
+     helper:215-220 / nb:402-433);
+  3. ``reference_fp32`` (GPU default): the reference's own config -- fp32 L8 H8 d768, batch
+     32 x 128, m = 4, fwd+bwd only -- through the compat API on the native fp32 kernels,
+     per schedule at P = N, next to the published row of BASELINE.md (``x_vs_nb``).
+Extras only start once the headline is in and only if the time left covers them (global
+deadline below); a skipped or failed extra is reported as such.
 
 Execution path (the same at every N): per-microbatch stage compute replayed as HIP graphs,
 one step recorded as a native instruction tape (csrc/runtime/stage_runner.cpp) and replayed
 from C++; p2p on the native RCCL engine (one communicator + stream per direction,
-csrc/comm/rccl_p2p.h), pre-flight pinged at init with an in-process fallback to torch p2p.
-The JSON reports which path ran (``hip_graphs``, ``native_runner``, ``p2p``).
+csrc/comm/rccl_engine.h), pre-flight pinged at init with an in-process fallback to torch
+p2p.  The JSON reports which path ran (``hip_graphs``, ``native_runner``, ``p2p``) and
+what the transport carried (``p2p_bytes_per_step``, ``rccl_ranks``).
 
-Hang safety (N>1): the pipeline program is PROVEN hang-free before it runs
-(PipelineRuntime._prove: every collective after the step's p2p, serial queue model), and
-every rank runs the benchmark in a child process under a supervisor.  The child arms a
-watchdog over init, warmup, every timed step and the bubble step (on a stall it prints the
-program grid + all stacks and exits non-zero); the process-group timeout is 300 s.  If an
-attempt fails on any rank, all supervisors retry in a more conservative mode (torch p2p,
-then no HIP graphs) on a fresh rendezvous port; the ``attempt`` field says which one
-produced the number.  One global deadline (MIPIPE_BENCH_DEADLINE_S, default 540 s, under
-the driver's 600 s) bounds all attempts together: each gets at most what is left of it
-(and at most MIPIPE_BENCH_ATTEMPT_S, default 240 s), its watchdogs are clamped to that,
-and no attempt starts with less than 30 s left.  Supervisors never touch the GPU.
+Hang safety: the pipeline program is PROVEN hang-free before it runs
+(PipelineRuntime._prove), and every measurement runs in a child process under a
+supervisor.  The child arms a watchdog over init, warmup, every timed step and the bubble
+step (on a stall it prints the program grid + all stacks and exits non-zero); the
+process-group timeout is 300 s.  If the headline fails on any rank, the supervisors retry
+it in a more conservative mode (torch p2p, then no HIP graphs) on a fresh rendezvous
+port; the ``attempt`` field says which one produced the number.  One global deadline
+(MIPIPE_BENCH_DEADLINE_S, default 540 s, under the driver's 600 s) bounds everything:
+each child gets at most what is left of it (and at most MIPIPE_BENCH_ATTEMPT_S, default
+240 s), its watchdogs are clamped to that.  Supervisors never touch the GPU.
 
 The measured bubble comes from one extra profiled step replayed from the same native tape
 (timing events around every graph on the compute stream): ``1 - sum(busy_r) / (P * step)``
@@ -60,8 +71,13 @@ METRIC = ("tokens/sec/node + pipeline bubble fraction, GPT-2 PP=1/2/4/8 (GPipe v
 BASELINE_NOTE = ("no same-config reference number: BASELINE.md only has the reference's fp32 toy model "
                  "(L4-12, d768, seq 128) on a 10-core CPU/gloo; see profiles/ for that table on MI355X")
 
-# supervisor attempts: (p2p transport, HIP graphs + native tape)
+# supervisor attempts of the headline: (p2p transport, HIP graphs + native tape)
 ATTEMPTS = [("auto", 1), ("torch", 1), ("torch", 0)]
+# the reference's three schedules (helper:215-220), measured back to back in one call
+SCHEDULES = ("GPipe", "1F1B", "Interleaved1F1B")
+# published L8 H8 rows of the reference (nb:703-708): (schedule, P) -> tok/s
+NB_L8H8 = {("GPipe", 2): 1671.32, ("1F1B", 2): 1649.53, ("Interleaved1F1B", 2): 1796.30,
+           ("GPipe", 4): 1675.15, ("1F1B", 4): 1680.10, ("Interleaved1F1B", 4): 1739.43}
 
 
 def parse(argv=None):
@@ -70,7 +86,16 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-small")
-    ap.add_argument("--schedule", default="1F1B")
+    ap.add_argument("--schedule", default="1F1B", help="the headline schedule (``value``)")
+    ap.add_argument("--schedules", default="all",
+                    help="schedules also measured after the headline, each in a fresh child process group: "
+                         "'all' (GPipe,1F1B,Interleaved1F1B), 'none', or a comma list")
+    ap.add_argument("--ref-fp32", default="auto", choices=["auto", "0", "1"],
+                    help="also time the reference's own config (fp32 L8 H8, batch 32 x 128, m=4, fwd+bwd) through "
+                         "the compat API on the native fp32 path, per schedule (auto: with a GPU)")
+    ap.add_argument("--ref-args", default="8,8,32,128",
+                    help="reference-config layers,heads,batch,seq (CPU tests shrink it)")
+    ap.add_argument("--phase", default="sched", choices=["sched", "ref"], help=argparse.SUPPRESS)
     ap.add_argument("--mbs", type=int, default=None,
                     help="sequences per microbatch (default: 64 on one GPU, 32 with a pipeline)")
     ap.add_argument("--seq", type=int, default=1024)
@@ -89,18 +114,50 @@ def parse(argv=None):
     ap.add_argument("--trace", default=None, help="write a Chrome trace of the profiled step (per rank)")
     ap.add_argument("--step-timeout", type=float, default=None,
                     help="watchdog limit per timed step in s (default 60; 180 for init and the first steps)")
-    ap.add_argument("--max-attempts", type=int, default=len(ATTEMPTS), help="supervisor attempts (N>1)")
-    ap.add_argument("--no-supervise", action="store_true", help="N>1: run in this process (no retry)")
+    ap.add_argument("--max-attempts", type=int, default=len(ATTEMPTS), help="supervisor attempts (headline)")
+    ap.add_argument("--no-supervise", action="store_true", help="run the headline in this process (no retry, "
+                                                                  "no other schedules)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"], help="default bf16 on GPU, fp32 on CPU")
     ap.add_argument("--vocab", type=int, default=None, help="override the vocabulary (CPU tests)")
     return ap.parse_args(argv)
 
 
+def extra_schedules(a) -> list:
+    s = (a.schedules or "none").strip()
+    if s.lower() in ("none", "0", ""):
+        names = []
+    elif s.lower() == "all":
+        names = list(SCHEDULES)
+    else:
+        names = [_canon(x) for x in s.split(",") if x.strip()]
+    return names
+
+
+def _canon(name: str) -> str:
+    """Schedule name -> canonical (the supervisor imports nothing that could touch HIP)."""
+    key = name.replace("_", "").replace("-", "").lower()
+    table = {"gpipe": "GPipe", "1f1b": "1F1B", "interleaved": "Interleaved1F1B", "interleaved1f1b": "Interleaved1F1B",
+             "zbh1": "ZBH1", "zbv": "ZBV", "loopedbfs": "LoopedBFS"}
+    if key not in table:
+        raise SystemExit(f"unknown schedule {name!r}")
+    return table[key]
+
+
+def ref_fp32_on(a) -> bool:
+    if a.ref_fp32 != "auto":
+        return a.ref_fp32 == "1"
+    import shutil
+    # a GPU box (the supervisor never initialises HIP: device nodes / rocminfo only)
+    return os.path.exists("/dev/kfd") and shutil.which("rocminfo") is not None
+
+
 # ------------------------------------------------------------------------------ supervisor
 def _attempt_dir() -> str:
     # one node (--nnodes=1): every rank's supervisor is a child of the same launcher agent
+    # (one process without a launcher: this process's own id)
+    owner = os.getppid() if int(os.environ.get("WORLD_SIZE", "1")) > 1 else os.getpid()
     d = os.path.join(os.environ.get("TMPDIR", "/tmp"),
-                     f"mipipe_bench_{os.getppid()}_{os.environ.get('MASTER_PORT', '0')}")
+                     f"mipipe_bench_{owner}_{os.environ.get('MASTER_PORT', '0')}")
     os.makedirs(d, exist_ok=True)
     return d
 
@@ -115,6 +172,12 @@ def _wait_file(path: str, timeout_s: float):
     return None
 
 
+def _publish(path: str, text: str) -> None:
+    with open(path + ".tmp", "w") as f:
+        f.write(text)
+    os.replace(path + ".tmp", path)
+
+
 DEADLINE_S = 540.0       # all attempts together (the driver kills the bench at 600 s)
 ATTEMPT_CAP_S = 240.0    # one attempt at most
 MIN_ATTEMPT_S = 30.0     # no attempt starts with less than this left
@@ -127,11 +190,43 @@ def attempt_budget(elapsed: float, deadline: float = DEADLINE_S, cap: float = AT
     return 0.0 if left < MIN_ATTEMPT_S else min(cap, left)
 
 
+def extra_budget(kind: str, left: float, cap: float, head_wall: float, ref_wall=None) -> tuple:
+    """(seconds the next non-headline child may run, 0 = skip it; its estimated need).
+    The need is the headline child's wall time + 25 % + 10 s (same model, one attempt) or
+    the last reference child's; the child is killed at twice that (>= 90 s), and never
+    later than 10 s before the global deadline -- so however the extras end, the whole
+    run stays inside it."""
+    est = ref_wall if (kind == "ref" and ref_wall) else (60.0 if kind == "ref" else head_wall * 1.25 + 10.0)
+    b = min(cap, left - 10.0)
+    if b < max(MIN_ATTEMPT_S, est):
+        return 0.0, est
+    return min(b, max(2.0 * est, 90.0)), est
+
+
+def plan_phases(a, argv) -> list:
+    """The fixed, rank-independent list of child runs: (tag, kind, argv, schedule).  The
+    headline's attempts first, then every other schedule of ``--schedules`` on the same
+    model/config, then the reference's fp32 config per schedule."""
+    tags = [(f"h{k}", "headline", list(argv), a.schedule) for k in range(max(1, a.max_attempts))]
+    head = _canon(a.schedule)
+    for s in extra_schedules(a):
+        if s != head:
+            tags.append((f"x_{s}", "sched", list(argv) + ["--schedule", s], s))
+    if ref_fp32_on(a):
+        for s in SCHEDULES:
+            tags.append((f"r_{s}", "ref", list(argv) + ["--phase", "ref", "--schedule", s], s))
+    return tags
+
+
 def supervise(a, argv) -> int:
-    """Run the benchmark in a child process per attempt (module docstring).  Rank 0 decides
-    after each attempt (did its child print the JSON line?  is there time for another?)
-    and publishes the verdict (done | retry | giveup) in a per-launch directory; the other
-    ranks follow it.  Never initialises the GPU."""
+    """Run every measurement in a child process (module docstring): the headline with up to
+    ``--max-attempts`` increasingly conservative attempts, then -- only once the headline
+    is in -- the other schedules and the reference's fp32 config, one fresh child process
+    group each, each only if the time left in the global deadline covers it (estimated from
+    the headline child's wall time).  A failing or hung extra is recorded as such and never
+    costs the headline.  Rank 0 decides every step and publishes it in a per-launch
+    directory (``<tag>.go``: "go <budget_s> <p2p> <graphs> <attempt>" | "skip"); the other
+    ranks follow.  Rank 0 prints ONE JSON line at the end.  Never initialises the GPU."""
     t_start = time.monotonic()
     rank = int(os.environ.get("RANK", "0"))
     base_port = int(os.environ.get("MASTER_PORT", "29500"))
@@ -151,67 +246,165 @@ def supervise(a, argv) -> int:
     import signal
     signal.signal(signal.SIGTERM, on_term)
     signal.signal(signal.SIGINT, on_term)
-    for k, (p2p, graphs) in enumerate(attempts):
-        per_attempt_s = attempt_budget(time.monotonic() - t_start, deadline, cap)
-        if per_attempt_s <= 0:      # (rank 0 published "giveup" for the previous attempt)
-            break
-        env = dict(os.environ, MIPIPE_BENCH_CHILD="1", MIPIPE_P2P=p2p, MIPIPE_BENCH_ATTEMPT=str(k),
-                   MASTER_PORT=str(base_port + 1 + k), MIPIPE_BENCH_ATTEMPT_S=f"{per_attempt_s:.0f}")
-        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # fresh rendezvous store per attempt
-        cmd = [sys.executable, os.path.abspath(__file__)] + list(argv) + ["--graphs", str(graphs)]
-        printed = False
-        proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE if rank == 0 else None, text=True)
-        current["proc"] = proc
-        t_end = time.monotonic() + per_attempt_s
-        if rank == 0:
-            import threading
 
-            def pump():
-                nonlocal printed
-                for line in proc.stdout:
-                    if line.lstrip().startswith("{") and '"metric"' in line:
-                        printed = True
-                    sys.stdout.write(line)
-                    sys.stdout.flush()
-            th = threading.Thread(target=pump, daemon=True)
-            th.start()
-        # wait for the child; once the result is in (rank 0 printed it / published "done"),
-        # a child still tearing down gets a grace period, then is killed
-        vpath = os.path.join(d, f"attempt{k}.verdict")
+    def left() -> float:
+        return deadline - (time.monotonic() - t_start)
+
+    def run_child(j, tag, child_argv, p2p, graphs, attempt, budget):
+        res_path = os.path.join(d, f"{tag}.json")
+        env = dict(os.environ, MIPIPE_BENCH_CHILD="1", MIPIPE_P2P=p2p, MIPIPE_BENCH_ATTEMPT=str(attempt),
+                   MASTER_PORT=str(base_port + 1 + j), MIPIPE_BENCH_ATTEMPT_S=f"{budget:.0f}",
+                   MIPIPE_BENCH_RESULT=res_path)
+        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # fresh rendezvous store per child
+        cmd = [sys.executable, os.path.abspath(__file__)] + child_argv + ["--graphs", str(graphs)]
+        t0 = time.monotonic()
+        proc = subprocess.Popen(cmd, env=env)
+        current["proc"] = proc
+        t_end = t0 + budget
+        done_path = os.path.join(d, f"{tag}.done")
         done_at = None
+        # wait for the child; once the result is in (rank 0's child wrote it), a child still
+        # tearing down gets a grace period, then is killed
         while proc.poll() is None:
             now = time.monotonic()
-            if done_at is None and (printed if rank == 0 else os.path.exists(vpath)):
+            if done_at is None and os.path.exists(res_path if rank == 0 else done_path):
                 done_at = now
             if now > t_end or (done_at is not None and now - done_at > 30.0):
                 if now > t_end:
-                    sys.stderr.write(f"[bench supervisor] rank {rank}: attempt {k} exceeded {per_attempt_s:.0f}s, "
-                                     f"killed\n")
+                    sys.stderr.write(f"[bench supervisor] rank {rank}: {tag} exceeded {budget:.0f}s, killed\n")
                 proc.kill()
                 break
             time.sleep(0.2)
         rc = proc.wait()
+        current["proc"] = None
+        res = None
+        if rank == 0 and os.path.exists(res_path):
+            with open(res_path) as f:
+                res = json.loads(f.read())
+            _publish(done_path, "1")
+        return rc, res, time.monotonic() - t0
+
+    phases = plan_phases(a, argv)
+    results = {}
+    headline = None
+    head_wall = None
+    head_mode = attempts[0] + (0,)
+    ref_wall = None
+    n_head = len([p for p in phases if p[1] == "headline"])
+    for j, (tag, kind, child_argv, sched) in enumerate(phases):
+        go_path = os.path.join(d, f"{tag}.go")
         if rank == 0:
-            th.join(timeout=10)
-            more = k + 1 < len(attempts) and attempt_budget(time.monotonic() - t_start, deadline, cap) > 0
-            verdict = "done" if printed else ("retry" if more else "giveup")
-            with open(os.path.join(d, f"attempt{k}.verdict.tmp"), "w") as f:
-                f.write(verdict)
-            os.replace(os.path.join(d, f"attempt{k}.verdict.tmp"), os.path.join(d, f"attempt{k}.verdict"))
+            decision = "skip"
+            if kind == "headline":
+                k = int(tag[1:])
+                b = attempt_budget(deadline - left(), deadline, cap)
+                if headline is None and k < len(attempts) and b > 0:
+                    decision = f"go {b:.0f} {attempts[k][0]} {attempts[k][1]} {k}"
+            elif headline is not None:
+                b, est = extra_budget(kind, left(), cap, head_wall, ref_wall)
+                if b > 0:
+                    decision = f"go {b:.0f} {head_mode[0]} {head_mode[1]} {head_mode[2]}"
+                else:
+                    results[tag] = {"skipped": f"time: {left():.0f}s left of the {deadline:.0f}s deadline, "
+                                               f"~{est:.0f}s needed"}
+            _publish(go_path, decision)
         else:
-            verdict = _wait_file(os.path.join(d, f"attempt{k}.verdict"), 30.0)
-        if verdict == "done":
-            return 0
-        sys.stderr.write(f"[bench supervisor] rank {rank}: attempt {k} (p2p={p2p}, graphs={graphs}) failed "
-                         f"(rc={rc}); {'retrying' if verdict == 'retry' else 'giving up'} "
-                         f"({time.monotonic() - t_start:.0f}s of the {deadline:.0f}s deadline used)\n")
-        sys.stderr.flush()
-        if verdict != "retry":
-            break
-    return 1
+            decision = _wait_file(go_path, max(60.0, left() + 60.0)) or "skip"
+        if not decision.startswith("go"):
+            continue
+        _, b, p2p, graphs, att = decision.split()
+        rc, res, wall = run_child(j, tag, child_argv, p2p, int(graphs), int(att), float(b))
+        if rank != 0:
+            continue
+        if kind == "headline":
+            if res is not None:
+                headline, head_wall, head_mode = res, wall, (p2p, int(graphs), int(att))
+            else:
+                more = (int(tag[1:]) + 1 < min(n_head, len(attempts))
+                        and attempt_budget(deadline - left(), deadline, cap) > 0)
+                sys.stderr.write(f"[bench supervisor] headline attempt {tag[1:]} (p2p={p2p}, graphs={graphs}) "
+                                 f"failed (rc={rc}); {'retrying' if more else 'giving up'} "
+                                 f"({deadline - left():.0f}s of the {deadline:.0f}s deadline used)\n")
+        else:
+            if kind == "ref":
+                ref_wall = wall * 1.25 + 5
+            results[tag] = res if res is not None else {"error": f"child exited rc={rc} without a result "
+                                                                 f"after {wall:.0f}s"}
+    final_path = os.path.join(d, "final")
+    if rank != 0:
+        return 0 if _wait_file(final_path, max(60.0, left() + 60.0)) == "ok" else 1
+    _publish(final_path, "ok" if headline is not None else "fail")
+    if headline is None:
+        return 1
+    print(json.dumps(merge_results(headline, results, a)), flush=True)
+    return 0
+
+
+def _sched_entry(r: dict) -> dict:
+    if "error" in r or "skipped" in r:
+        return r
+    keys = ("value", "ms_per_step", "bubble_fraction", "bubble_per_rank", "analytic_bubble", "hbm_peak_gb_per_gpu",
+            "model_tflops_per_gpu", "p2p_bytes_per_step", "rccl_ranks", "attempt")
+    out = {"tok_s": r.get("value")}
+    out.update({k: r.get(k) for k in keys if k != "value" and k in r})
+    c = r.get("config", {})
+    for k in ("v", "microbatches", "micro_batch", "head_lag", "planned_efficiency", "native_runner", "p2p",
+              "layer_split"):
+        if k in c:
+            out[k] = c[k]
+    return out
+
+
+def merge_results(headline: dict, results: dict, a) -> dict:
+    """The headline's JSON line + ``schedules`` (every measured schedule of the same
+    model/config, the headline's own included) + ``reference_fp32``."""
+    out = dict(headline)
+    sched = {headline["config"]["schedule"]: _sched_entry(headline)}
+    for tag, r in results.items():
+        if tag.startswith("x_"):
+            sched[tag[2:]] = _sched_entry(r)
+    out["schedules"] = sched
+    ok = {k: v for k, v in sched.items() if "tok_s" in v and v["tok_s"]}
+    if "GPipe" in ok:
+        for k, v in ok.items():
+            v["speedup_vs_gpipe"] = round(v["tok_s"] / ok["GPipe"]["tok_s"], 4)
+    refs = {tag[2:]: r for tag, r in results.items() if tag.startswith("r_")}
+    if refs:
+        rb = {}
+        P = headline["n_gpus"]
+        for s, r in refs.items():
+            if "error" in r or "skipped" in r:
+                rb[s] = r
+                continue
+            e = dict(r)
+            nb_p = P if (s, P) in NB_L8H8 else 2
+            nb = NB_L8H8.get((s, nb_p)) if a.ref_args == "8,8,32,128" else None
+            if nb and e.get("tok_s"):
+                e["nb_row"] = {"tok_s": nb, "P": nb_p, "source": "BASELINE.md Table 1 (nb:703-708), 10-core CPU"}
+                e["x_vs_nb"] = round(e["tok_s"] / nb, 1)
+            rb[s] = e
+        okr = {k: v for k, v in rb.items() if v.get("tok_s")}
+        if "GPipe" in okr:
+            for k, v in okr.items():
+                v["speedup_vs_gpipe"] = round(v["tok_s"] / okr["GPipe"]["tok_s"], 4)
+        out["reference_fp32"] = {
+            "config": "reference ModelArgs L{0} H{1} d768 vocab 10000, batch {2} x seq {3}, m=4, fp32, fwd+bwd only, "
+                      "dropout 0.1 (helper:23-55, :98-143, :214)".format(*a.ref_args.split(",")),
+            "per_schedule": rb,
+            "tok_s": max((v["tok_s"] for v in okr.values()), default=None)}
+    return out
 
 
 # ------------------------------------------------------------------------------ benchmark
+def emit(out: dict) -> None:
+    """Rank 0's result: into the supervisor's result file (MIPIPE_BENCH_RESULT), else stdout."""
+    path = os.environ.get("MIPIPE_BENCH_RESULT")
+    if path:
+        _publish(path, json.dumps(out))
+    else:
+        print(json.dumps(out), flush=True)
+
+
 def _plain_summary():
     """Plain forward / dX GEMM shapes per backend (ops.kernels MIPIPE_GEMM=auto timing)."""
     from mipipe.ops import kernels as K
@@ -263,7 +456,7 @@ def run(a) -> None:
         if a.graphs is None:
             a.graphs = 1 if gpu else 0
         dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.dtype or ("bf16" if gpu else "fp32")]
-        trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m,
+        trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule, n_microbatches=m,
                                   mbs=a.mbs, seq_len=a.seq, v=a.vstages, device=device,
                                   recompute=a.recompute if a.recompute == "auto" else a.recompute == "1", seed=0,
                                   split_head=False if a.no_split_head else None, graphs=bool(a.graphs) and gpu,
@@ -351,6 +544,17 @@ def run(a) -> None:
             hbm_peak = round(float(hp.item()), 1)
     flops = cfg.flops_per_token(a.seq) * value
     rt = trainer.runtime
+    with wd.step(init_to):
+        # the record proves what the transport carried: pipeline bytes sent per step (all
+        # ranks) and the ranks of the native RCCL communicators (pipeline, DP)
+        pb = torch.tensor([float(rt.p2p_send_bytes())], device=device, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(pb, op=dist.ReduceOp.SUM)
+        p2p_bytes = int(pb.item())
+        eng = getattr(rt.p2p, "engine", None)
+        rccl_ranks = {"pp": int(eng.nranks()) if eng is not None else None,
+                      "dp": int(trainer.coll.dp_engine.nranks()) if getattr(trainer.coll, "dp_engine", None)
+                      is not None else None}
     out = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -397,9 +601,78 @@ def run(a) -> None:
     }
     if loss_val is not None:
         out["last_loss"] = round(loss_val, 4)
+    out["p2p_bytes_per_step"] = p2p_bytes
+    out["rccl_ranks"] = rccl_ranks
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        emit(out)
     with wd.step(init_to):
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+    wd.close()
+
+
+def run_ref(a) -> None:
+    """The reference's own workload (helper:150-235 with nb:306's batch 32 x seq 128, m = 4,
+    fwd+bwd only, no optimizer step) through the compat API on the native path at the
+    reference's precision (fp32 kernels), P = world size, one schedule.  Timing as the
+    reference (wall clock on the last rank over ``--steps`` steps after ``--warmup``) and
+    also max over ranks; plus the measured and analytic bubble."""
+    import torch
+    import torch.distributed as dist
+    import mipipe  # noqa: F401
+    from mipipe.bench.compat import native_reference_schedule, run_train_iterations, stages_per_worker
+    from mipipe.models.ref_transformer import ModelArgs, Transformer, manual_model_split, tokenwise_loss_fn
+    from mipipe.parallel.api import get_schedule_class
+    from mipipe.parallel.mesh import init_distributed
+    from mipipe.utils.metrics import Watchdog
+
+    budget = float(os.environ.get("MIPIPE_BENCH_ATTEMPT_S", "0") or 0)
+    wd = Watchdog(max(10.0, budget - 10.0) if budget > 0 else 180.0)
+    with wd.step():
+        rank, world, local_rank, device = init_distributed()
+        L, H, B, S = (int(x) for x in a.ref_args.split(","))
+        sched = _canon(a.schedule)
+        m = 4
+        if sched != "Interleaved1F1B" and m < world:
+            m = world      # torch needs m >= stages for one stage per rank (schedules.py:578-583)
+        torch.manual_seed(1234 + rank)
+        args = ModelArgs(n_layers=L, n_heads=H)
+        x = torch.randint(0, args.vocab_size, (B, S), dtype=torch.long, device=device)
+        y = torch.randint(0, args.vocab_size, (B, S), dtype=torch.long, device=device)
+        gpu = device.type == "cuda"
+        if gpu:
+            schedule = native_reference_schedule(args, sched, rank, world, B, S, m, device, precision="fp32")
+            engine = "native fp32 kernels"
+        else:
+            spw = stages_per_worker(sched, L, world)
+            stages = [manual_model_split(Transformer(args), rank + world * i, world * spw, device) for i in range(spw)]
+            cls = get_schedule_class(sched)
+            schedule = cls(stages if spw > 1 or sched == "Interleaved1F1B" else stages[0], n_microbatches=m,
+                           loss_fn=tokenwise_loss_fn(args.vocab_size))
+            engine = "torch CPU (autograd)"
+        if world > 1:
+            dist.barrier()
+        met = run_train_iterations(schedule, x, y, rank, world, num_iterations=a.steps, warmup=a.warmup,
+                                   device=device)
+        el = torch.tensor([met["elapsed_time"]], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        rt = schedule.runtime
+        last = torch.tensor([met["throughput"] if rank == world - 1 else 0.0], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(last, op=dist.ReduceOp.SUM)
+    out = {"tok_s": round(met["tokens_processed"] / float(el.item()), 1),
+           "tok_s_last_rank_timer": round(float(last.item()), 1),
+           "ms_per_step": round(float(el.item()) / a.steps * 1e3, 3),
+           "steps": a.steps, "warmup": a.warmup, "P": world, "v": rt.v, "microbatches": rt.m,
+           "bubble_fraction": None if met.get("bubble_fraction") is None else round(met["bubble_fraction"], 4),
+           "analytic_bubble": None if met.get("analytic_bubble") is None else round(met["analytic_bubble"], 4),
+           "precision": met.get("precision", "fp32"), "engine": engine,
+           "native_runner": met.get("native_runner"), "lanes": met.get("lanes"), "p2p": rt.p2p.kind}
+    if rank == 0:
+        emit(out)
+    with wd.step():
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
@@ -419,7 +692,7 @@ def main():
         sys.exit(subprocess.call(cmd))
     if n != world_env and world_env > 1:
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world_env}")
-    if world_env > 1 and os.environ.get("MIPIPE_BENCH_CHILD") != "1" and not a.no_supervise:
+    if os.environ.get("MIPIPE_BENCH_CHILD") != "1" and not a.no_supervise:
         # drop a --graphs the supervisor will set per attempt
         child_argv, skip = [], False
         for x in argv:
@@ -433,7 +706,10 @@ def main():
                 continue
             child_argv.append(x)
         sys.exit(supervise(a, child_argv))
-    run(a)
+    if a.phase == "ref":
+        run_ref(a)
+    else:
+        run(a)
 
 
 if __name__ == "__main__":

@@ -790,6 +790,29 @@ class PipelineRuntime:
             st.backward_weight_mb(a.mb)
 
     # ------------------------------------------------------------------ diagnostics
+    def p2p_send_bytes(self) -> int:
+        """Bytes this rank sends per step over the pipeline transport (activations,
+        gradients, head chunks and their gradients), from the lowered program and the
+        stages' static specs (valid after the first step)."""
+        def nbytes(specs):
+            return sum(math.prod(sh) * torch.empty((), dtype=dt).element_size() for sh, dt in specs)
+        tot = 0
+        for e in self.program:
+            if not isinstance(e, CommGroup):
+                continue
+            for op in e.ops:
+                if not op.action.op.is_send:
+                    continue
+                kind = op.key[0]
+                if kind in ("H", "D"):
+                    h = self.head
+                    tot += h.chunks[op.key[1]] * h.d_model * torch.empty((), dtype=h.dtype).element_size()
+                elif kind == "F":
+                    tot += nbytes(self.stages[op.key[1] - 1].output_specs or [])
+                else:
+                    tot += nbytes(self.stages[op.key[1] + 1].input_specs or [])
+        return int(tot)
+
     def busy_ms(self) -> float:
         """Busy time of the last profiled step: the union of the action intervals (with
         microbatch lanes two actions may overlap)."""

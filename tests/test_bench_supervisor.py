@@ -108,3 +108,52 @@ def test_bench_default_batch_is_128_sequences_per_gpu():
     c = out["config"]
     assert (c["micro_batch"], c["microbatches"], c["global_batch"]) == (64, 2, 128)
     assert out["scaling"] == "weak" and out["n_gpus"] == 1
+
+
+def test_bench_four_ranks_measures_all_three_schedules():
+    """One ``bench.py --gpus 4`` call (CPU/gloo) measures the reference's comparison --
+    GPipe, 1F1B and Interleaved1F1B on the same model/config, each with its measured and
+    analytic bubble -- and the record carries the transport's bytes per step."""
+    import time
+    env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_PORT=str(free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"] + ARGS[:-2]
+    t0 = time.monotonic()
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
+    dt = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    sch = out["schedules"]
+    assert set(sch) == {"GPipe", "1F1B", "Interleaved1F1B"}, sch
+    for name, e in sch.items():
+        assert e["tok_s"] > 0 and e["bubble_fraction"] is not None and e["analytic_bubble"] is not None, (name, e)
+        assert e["p2p_bytes_per_step"] > 0
+    assert sch["Interleaved1F1B"]["v"] == 2 and sch["GPipe"]["v"] == 1
+    assert sch["Interleaved1F1B"]["analytic_bubble"] < sch["1F1B"]["analytic_bubble"]
+    assert sch["GPipe"]["speedup_vs_gpipe"] == 1.0
+    assert out["value"] == sch["1F1B"]["tok_s"] and out["config"]["schedule"] == "1F1B"
+    assert out["p2p_bytes_per_step"] > 0 and "rccl_ranks" in out
+    assert dt < 540, dt
+
+
+def test_extra_phases_never_push_past_the_deadline():
+    """Worst case of the supervisor's plan: the headline succeeds late, then every other
+    schedule and reference child hangs until it is killed at its budget -- the run still
+    ends inside 560 s of the driver's 600 s."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for head_wall in (20.0, 60.0, 150.0, 230.0):
+        t = head_wall + 1.0                 # headline attempt 0 succeeded
+        ref_wall = None
+        for kind in ["sched"] * 2 + ["ref"] * 3:
+            b, est = bench.extra_budget(kind, bench.DEADLINE_S - t, bench.ATTEMPT_CAP_S, head_wall, ref_wall)
+            if b <= 0:
+                continue
+            assert b <= bench.DEADLINE_S - t - 10.0
+            t += b + 5.0                    # hangs to its limit; the kill takes <= 5 s
+            if kind == "ref":
+                ref_wall = b * 1.25 + 5
+        assert t <= 560.0, (head_wall, t)
