@@ -589,6 +589,8 @@ def run(a) -> None:
                    "p2p_fallback": rt.p2p.fallback_reason or None,
                    "collectives": trainer.coll.kind,
                    "collective_placement": rt.coll_placement,
+                   "dp_reduce_dtype": ("bf16" if getattr(trainer.coll, "dp_reduce_dtype", None) == torch.bfloat16
+                                       else "f32") if dp > 1 else None,
                    "head_zero": bool(getattr(trainer, "head_zero", False)) and trainer.head is not None,
                    "recompute": trainer.recompute,
                    "recv_arena_mb": round(rt.recv_arena_bytes / 2 ** 20, 1),

@@ -77,6 +77,11 @@ class FlatAdamW:
     def step(self, lr: Optional[float] = None) -> None:
         self.step_count += 1
         lr = self.lr if lr is None else lr
+        for a in self.arenas:
+            g16 = getattr(a, "grad16", None)
+            if g16 is not None and a.shard is not None and a.shard_scope == "dp":
+                lo, hi, _ = a.shard        # bf16 DP reduce-scatter: widen this replica's block
+                a.grad[lo:hi].copy_(g16[lo:hi])
         use_clip = self.max_norm and self.max_norm > 0
         if use_clip:
             self.sumsq.zero_()
@@ -146,7 +151,7 @@ def max_inflight_microbatches(order, stages) -> int:
 
 def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, seq_len: int, device,
                    head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1,
-                   stage_shards: int = 1) -> dict:
+                   stage_shards: int = 1, dtype=torch.bfloat16) -> dict:
     """HBM plan of one pipeline rank and the recompute decision of ``recompute="auto"``:
     recompute only if the activation stash would not fit ``budget_frac`` of the device.
 
@@ -158,17 +163,24 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     moments (12 of the 20 bytes) for 1 / head_shards of the matrix: ``head_optimizer_bytes``
     is that per-rank optimizer state, ``head_state_bytes`` all of the head's.  ZeRO-1 over DP
     (``stage_shards`` = DP) does the same for the stage parameters: 8 + 12 / dp bytes each.
+    f32 arenas (the reference's precision): the f32 weights ARE the master, so sharding
+    leaves them whole and splits only the Adam moments -- 12 + 8 / shards bytes per
+    parameter (head: 12 + 8 / head_shards).
     Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute."""
     T = mbs * seq_len
     nlayers = sum(layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages)
     emb = cfg.vocab_padded * cfg.d_model
     nparams = cfg.layer_params() * nlayers + (emb if 0 in my_stages else 0)
-    head_opt = 12.0 * emb / max(1, head_shards) if head_tokens else 0.0
-    head_state = (8.0 * emb if head_tokens else 0.0) + head_opt
+    f32 = dtype == torch.float32
+    fixed_b, shard_b = (12.0, 8.0) if f32 else (8.0, 12.0)
+    head_opt = shard_b * emb / max(1, head_shards) if head_tokens else 0.0
+    head_state = (fixed_b * emb if head_tokens else 0.0) + head_opt
     inflight = max_inflight_microbatches(order, set(my_stages))
     from .models.native import _HEAD_CHUNK
     logit_rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
-    fixed = (8.0 + 12.0 / max(1, stage_shards)) * nparams + head_state + 2.0 * logit_rows * cfg.vocab_padded + 4e9
+    logit_b = 4.0 if f32 else 2.0
+    fixed = (fixed_b + shard_b / max(1, stage_shards)) * nparams + head_state + logit_b * logit_rows * \
+        cfg.vocab_padded + 4e9
     full = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=False)
     rec = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=True) + \
         cfg.stash_bytes_per_layer(T, recompute=False)
@@ -277,7 +289,7 @@ class PipelineTrainer:
             self.memory_plan = plan_recompute(cfg, layer_ranges, my_stages, order, mbs, seq_len, self.device,
                                               head_tokens=head_tokens,
                                               head_shards=pp if (self.head_zero and pp > 1) else 1,
-                                              stage_shards=self.mesh.dp if self.dp_zero else 1)
+                                              stage_shards=self.mesh.dp if self.dp_zero else 1, dtype=dtype)
             recompute = self.memory_plan["recompute"]
         self.recompute = bool(recompute)
         # ZeRO-1 over DP replicas (MIPIPE_DP_ZERO=0: replicated master / moments, gradient
@@ -301,7 +313,8 @@ class PipelineTrainer:
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,
                                        scale_grads=True, style=style, profile=profile, orders=orders,
                                        head=head_plan, head_costs=head_costs, stage_costs=stage_costs,
-                                       dp=self.mesh.dp, head_reduce_after_stage0=bool(cfg.tie_embeddings))
+                                       dp=self.mesh.dp, head_reduce_after_stage0=bool(cfg.tie_embeddings),
+                                       vote_group=self.mesh.world_ctrl)
         # microbatch lanes (PipelineRuntime.set_lanes): MIPIPE_LANES=auto|1 (off)|n.  Not with
         # plain GEMMs on hipBLASLt (MIPIPE_GEMM=blas|auto): its stream-K kernels synchronise
         # their workgroups and assume all of them resident; a second lane's kernels holding
@@ -372,9 +385,20 @@ class PipelineTrainer:
             w1, part = self.coll.all_reduce(g, "pp"), g
         if self.mesh.dp == 1:
             return [w1]
-        if not (self.coll.pp_kind == "native" and self.coll.dp_kind == "native"):
-            w1.wait()
-        return [w1, self.coll.all_reduce(part, "dp")]
+        if self.coll.pp_kind == "native" and self.coll.dp_kind == "native":
+            return [w1, self.coll.all_reduce(part, "dp")]
+        # through torch.distributed the DP step needs the pipeline step's result, i.e. a
+        # wait -- taken when the runtime drains its reductions at the step end, not here: a
+        # host block at REDUCE_HEAD would hold this rank's remaining flush hostage to the
+        # other pipeline ranks reaching theirs (a hang with the overlapped placement)
+        coll = self.coll
+
+        class _Chain:
+            def wait(self):
+                w1.wait()
+                coll.all_reduce(part, "dp").wait()
+                return True
+        return [_Chain()]
 
     def _auto_lanes(self, pp: int, v: int, graphs: bool, m: int, mbs: int, seq_len: int) -> int:
         layers = sum(r1 - r0 for r0, r1 in self.layer_ranges)

@@ -199,10 +199,30 @@ class NativeStage(StageBase):
                 if self.arena.shard is not None and self.arena.shard_scope == "dp":
                     # ZeRO-1 over DP (engine.py): reduce-scatter -- this replica's block of
                     # the arena is summed; the optimizer updates it and all-gathers weights
+                    if getattr(self.coll, "dp_reduce_dtype", torch.float32) == torch.bfloat16:
+                        return self.coll.reduce_scatter(self._grad_bf16(), "dp")[0]
                     return self.coll.reduce_scatter(self.arena.grad, "dp")[0]
                 return self.coll.all_reduce(self.arena.grad, "dp")
             return allreduce_flat(self.arena.grad, self.dp_group, average=False)
         return None
+
+    def _grad_bf16(self) -> torch.Tensor:
+        """MIPIPE_DP_REDUCE_DTYPE=bf16: the summed f32 gradient rounded into a bf16 staging
+        buffer (half the bytes over the DP link); the optimizer widens this replica's reduced
+        block back into the f32 gradient (engine.FlatAdamW).  The cast is captured as a graph
+        of its own on graphed stages, so a recorded step replays it natively."""
+        a = self.arena
+        if getattr(a, "grad16", None) is None:
+            a.grad16 = torch.empty(a.numel, dtype=torch.bfloat16, device=a.device)
+
+        def cast(ins=()):
+            ops.cast_f32_bf16(a.grad, a.grad16)
+            return a.grad16
+        if self._graphed():
+            self.graphs.run(("C16", 0), (), cast)
+        else:
+            cast()
+        return a.grad16
 
     def has_grad_reduction(self, scaled_in_loss):
         return (not scaled_in_loss) or (self.dp_group is not None and dist.get_world_size(self.dp_group) > 1)

@@ -39,8 +39,14 @@ class _PipelineSchedule:
 
     def __init__(self, stages: Union[StageBase, Sequence[StageBase]], n_microbatches: int,
                  loss_fn: Optional[Callable] = None, scale_grads: bool = True, group=None,
-                 pipe_ranks: Optional[Sequence[int]] = None, style: str = "loop", profile: bool = False):
+                 pipe_ranks: Optional[Sequence[int]] = None, style: str = "loop", profile: bool = False,
+                 copy_outputs: bool = True):
+        """``copy_outputs`` (default, the reference's semantics): the last rank's ``step()``
+        returns a fresh tensor, as the dependency's ``torch.cat`` merge does.  False: a
+        zero-copy view of the native stage's persistent logits buffer -- valid only until the
+        next ``step()``, which rewrites it in place (eager copy or graph replay)."""
         stages = [stages] if isinstance(stages, StageBase) else list(stages)
+        self.copy_outputs = bool(copy_outputs)
         multi = SCHEDULES[self._name][2]
         if not multi and len(stages) != 1:
             raise ValueError(f"{self._name} takes exactly one stage per rank")
@@ -87,8 +93,8 @@ class _PipelineSchedule:
         if outs is None or not has_last:
             return None
         if len(outs[0]) == 1:
-            return _merge([o[0] for o in outs])   # merged last-stage outputs (logits)
-        return tuple(_merge([o[i] for o in outs]) for i in range(len(outs[0])))
+            return _merge([o[0] for o in outs], self.copy_outputs)   # merged last-stage outputs (logits)
+        return tuple(_merge([o[i] for o in outs], self.copy_outputs) for i in range(len(outs[0])))
 
     def eval(self, *args, target=None, losses=None):
         """Forward-only pass (dependency schedules.py:402-420)."""
@@ -119,9 +125,10 @@ class _PipelineSchedule:
         return torch.cat([o[0] for o in outs], dim=0)
 
 
-def _merge(parts):
+def _merge(parts, copy: bool = True):
     """torch.cat(parts, 0) -- or, when the parts are consecutive row blocks of one buffer (the
-    native stage's persistent logits), the view of that buffer spanning them."""
+    native stage's persistent logits), the view of that buffer spanning them (``copy``: a
+    clone of that view, so the result outlives the next step like the reference's)."""
     p0 = parts[0]
     if len(parts) > 1 and all(p.dim() == p0.dim() and p.shape[1:] == p0.shape[1:] and p.stride() == p0.stride()
                               and p.untyped_storage().data_ptr() == p0.untyped_storage().data_ptr()
@@ -129,8 +136,9 @@ def _merge(parts):
         step = p0.shape[0] * p0.stride(0)
         if all(p.shape[0] == p0.shape[0] and p.storage_offset() == p0.storage_offset() + i * step
                for i, p in enumerate(parts)):
-            return p0.as_strided((p0.shape[0] * len(parts),) + tuple(p0.shape[1:]), p0.stride(),
+            view = p0.as_strided((p0.shape[0] * len(parts),) + tuple(p0.shape[1:]), p0.stride(),
                                  p0.storage_offset())
+            return view.clone() if copy else view
     return torch.cat(parts, dim=0)
 
 
@@ -160,8 +168,8 @@ class ScheduleZBVZeroBubble(_PipelineSchedule):
     _name = "ZBV"
 
     def __init__(self, stages, n_microbatches, loss_fn=None, scale_grads=True, group=None, pipe_ranks=None,
-                 style: str = "v", profile: bool = False):
-        super().__init__(stages, n_microbatches, loss_fn, scale_grads, group, pipe_ranks, "v", profile)
+                 style: str = "v", profile: bool = False, copy_outputs: bool = True):
+        super().__init__(stages, n_microbatches, loss_fn, scale_grads, group, pipe_ranks, "v", profile, copy_outputs)
 
 
 _CLASSES = {"GPipe": ScheduleGPipe, "1F1B": Schedule1F1B, "Interleaved1F1B": ScheduleInterleaved1F1B,

@@ -107,9 +107,13 @@ class Collectives:
         self.pipe_engine = pipe_engine if (pipe_engine is not None and
                                            int(pipe_engine.channels) > PIPE_COLL_CHANNEL) else None
         self.dp_engine = None
-        native_ok = os.environ.get("MIPIPE_COLL", "native") != "torch"
-        if native_ok and self.dp > 1 and self.device.type == "cuda" and dist.is_initialized() and \
-                dist.get_backend(self.dp_group) == "nccl" and (self.pipe_engine is not None or self.pp == 1):
+        # element type of the ZeRO-1 DP gradient reduce-scatter: f32 (default) or bf16
+        # (MIPIPE_DP_REDUCE_DTYPE=bf16: half the bytes on the per-link-bound xGMI ring)
+        rd = os.environ.get("MIPIPE_DP_REDUCE_DTYPE", "f32").lower()
+        if rd not in ("f32", "fp32", "bf16"):
+            raise ValueError(f"MIPIPE_DP_REDUCE_DTYPE={rd}: f32 or bf16")
+        self.dp_reduce_dtype = torch.bfloat16 if rd == "bf16" else torch.float32
+        if self.dp > 1 and self.dp_transport_native(mesh):
             dp_ranks = [d * self.pp + mesh.pp_rank for d in range(self.dp)]
             self.dp_engine = make_dp_engine(self.dp_group, dp_ranks, mesh.dp_rank, self.device)
         if self.pp > 1 and self.pipe_engine is None:
@@ -120,6 +124,25 @@ class Collectives:
             self.dp_kind = "native" if self.dp_engine is not None else "torch"
         else:
             self.dp_kind = "none"
+
+    def _dp_native_wanted(self) -> bool:
+        """This rank's own view: RCCL backend on a GPU and a native pipeline engine (or no
+        pipeline) -- a pipeline whose pre-flight fell back to torch p2p has no engine."""
+        return (os.environ.get("MIPIPE_COLL", "native") != "torch" and self.device.type == "cuda"
+                and dist.is_initialized() and dist.get_backend(self.dp_group) == "nccl"
+                and (self.pipe_engine is not None or self.pp == 1))
+
+    def dp_transport_native(self, mesh) -> bool:
+        """The DP transport, decided ALIKE on every rank: the pre-flight vote of a
+        pipeline covers only that pipeline, so one replica may run native p2p while another
+        fell back -- its DP peers would then never enter the engine's broadcast + blocking
+        communicator init.  The native engine is used only if every rank of the world wants
+        it (MIN vote over the world control group, gloo when the world is RCCL)."""
+        want = self._dp_native_wanted()
+        if not dist.is_initialized() or dist.get_world_size() <= 1:
+            return want
+        from .comm import agree
+        return agree(want, getattr(mesh, "world_ctrl", None), self.device)
 
     @property
     def kind(self) -> str:

@@ -70,6 +70,7 @@ class Mesh:
     dp_group: Optional[object]
     embed_group: Optional[object]   # first + last stage of my pipeline (tied embeddings)
     ctrl_group: Optional[object] = None   # gloo group of my pipeline: control-plane votes
+    world_ctrl: Optional[object] = None   # gloo group of every rank (None: the world is gloo)
 
     @property
     def is_first(self) -> bool:
@@ -88,7 +89,7 @@ def build_mesh(pp: int, dp: int = 1, backend_device: Optional[torch.device] = No
     if pp * dp != world:
         raise ValueError(f"pp({pp}) x dp({dp}) != world size {world}")
     dp_rank, pp_rank = divmod(rank, pp)
-    pp_group = dp_group = embed_group = ctrl_group = None
+    pp_group = dp_group = embed_group = ctrl_group = world_ctrl = None
     pipe_ranks = [dp_rank * pp + i for i in range(pp)]
     if world > 1:
         # host-side (gloo) group per pipeline for control-plane agreement (the native p2p
@@ -102,6 +103,10 @@ def build_mesh(pp: int, dp: int = 1, backend_device: Optional[torch.device] = No
                 g = dist.new_group(ranks, backend="gloo") if pp > 1 else None
             if d == dp_rank:
                 ctrl_group = g
+        # world-wide control plane: decisions every rank must take alike (the DP transport,
+        # the collective placement) are voted over it
+        if not gloo_default:
+            world_ctrl = dist.new_group(list(range(world)), backend="gloo")
         # every rank must create every group, in the same order
         for d in range(dp):
             ranks = [d * pp + i for i in range(pp)]
@@ -133,4 +138,5 @@ def build_mesh(pp: int, dp: int = 1, backend_device: Optional[torch.device] = No
             torch.cuda.synchronize()
     if ctrl_group is None and world > 1 and dist.get_backend() == "gloo":
         ctrl_group = pp_group
-    return Mesh(rank, world, pp, dp, pp_rank, dp_rank, pipe_ranks, pp_group, dp_group, embed_group, ctrl_group)
+    return Mesh(rank, world, pp, dp, pp_rank, dp_rank, pipe_ranks, pp_group, dp_group, embed_group, ctrl_group,
+                world_ctrl)

@@ -114,8 +114,13 @@ class PipelineRuntime:
                  style: str = "loop", program: Optional[Dict[int, List[Entry]]] = None, profile: bool = False,
                  orders: Optional[Dict[int, List[Action]]] = None, head: Optional[HeadPlan] = None,
                  head_costs: Optional[Dict[int, float]] = None, stage_costs: Optional[Sequence[float]] = None,
-                 debug: Optional[int] = None, dp: int = 1, head_reduce_after_stage0: bool = False):
+                 debug: Optional[int] = None, dp: int = 1, head_reduce_after_stage0: bool = False,
+                 vote_group="pipeline"):
         self.stages: Dict[int, StageBase] = {s.stage_index: s for s in stages}
+        # group over which decisions every rank must take alike are voted (the collective
+        # placement): "pipeline" = the pipeline's control group; the trainer passes the
+        # world's (its DP replicas run collectives with each other)
+        self.vote_group = getattr(p2p, "ctrl_group", None) if vote_group == "pipeline" else vote_group
         self.schedule = canonical_name(schedule)
         self.m = n_microbatches
         self.rank = pp_rank
@@ -190,16 +195,18 @@ class PipelineRuntime:
         """Choose where the step's collectives go and PROVE the resulting program cannot
         hang under the queue model that holds on this machine (simulate.check_lowered).
 
-        Default: collectives deferred to the end of the step (after every p2p group), and the
-        program must pass the *serial* model -- one FIFO per rank, the worst case of any
+        Default (``MIPIPE_COLL_OVERLAP=probe``): each collective stays where it was placed
+        (DP all-reduce / reduce-scatter right after the stage's last backward, head reduction
+        after the rank's last head chunk) to overlap the flush.  That needs the *independent*
+        queue model, so it is used only if the hardware-queue probe (parallel/queues.py)
+        finds every comm stream on a queue of its own on EVERY rank (a MIN vote), with the
+        native engine carrying the p2p.  Otherwise -- or with ``MIPIPE_COLL_OVERLAP=0`` --
+        collectives are deferred to the end of the step (after every p2p group), and the
+        program must pass the *serial* model: one FIFO per rank, the worst case of any
         stream -> hardware-queue mapping (GPU_MAX_HW_QUEUES per priority; RCCL's own
-        internal streams included), so nothing about the mapping needs to be known.
-        ``MIPIPE_COLL_OVERLAP=1`` keeps each collective where it was placed (DP all-reduce
-        right after the stage's last backward, head reduction after the rank's last head
-        chunk) to overlap the flush; that needs the *independent* model, so it is used only
-        if the hardware-queue probe (parallel/queues.py) finds every comm stream on a queue
-        of its own.  With two p2p channels the per-direction order is proven as well
-        (independent model), else the p2p falls back to one channel.  A program that no
+        internal streams included), so nothing about the mapping needs to be known.  With
+        two p2p channels the per-direction order is proven as well (independent model), else
+        the p2p falls back to one channel.  A program that no
         model admits raises instead of running."""
         from .simulate import check_lowered
         S = self.num_stages
@@ -208,13 +215,29 @@ class PipelineRuntime:
         self.coll_placement = "none"
         self.queue_report = None
         if has_coll:
-            overlap = os.environ.get("MIPIPE_COLL_OVERLAP", "0") == "1" and getattr(p2p, "kind", "") == "native"
-            if overlap and self.device.type == "cuda":
+            # MIPIPE_COLL_OVERLAP: probe (default) = overlap wherever the hardware-queue probe
+            # clears it; 1 = same; 0 = always defer
+            mode = os.environ.get("MIPIPE_COLL_OVERLAP", "probe").lower()
+            kind = getattr(p2p, "kind", "")
+            overlap = False
+            if mode in ("1", "probe") and kind == "native" and self.device.type == "cuda":
                 from .queues import comm_queues_independent
                 overlap, self.queue_report = comm_queues_independent(self.device)
+            elif mode in ("1", "probe") and kind in ("torch", "gloo-staged") and self._gloo(p2p):
+                # gloo moves bytes on the host: a process group's collectives run on that
+                # group's own worker threads, p2p on tagged unbound buffers -- no shared
+                # device FIFO, i.e. the independent model (CPU plumbing, shared-GPU rehearsal)
+                overlap = True
+                self.queue_report = {"gloo": "host transport: independent per group"}
+            if dist.is_initialized() and dist.get_world_size() > 1:
+                # every rank takes the same placement: the proof below assumes
+                # one program for all, so overlap only if every rank's probe cleared it
+                from .comm import agree
+                overlap = agree(overlap, self.vote_group, self.device)
             if overlap:
                 check_lowered(program, S, channels=getattr(p2p, "channels", 1), dp=self.dp)
-                self.coll_placement = "overlapped (independent queues, probed)"
+                self.coll_placement = ("overlapped (independent queues, probed)" if kind == "native"
+                                       else "overlapped (gloo host transport)")
             else:
                 program = defer_collectives(program)
                 self.coll_placement = "step end (serial-model proof)"
@@ -224,9 +247,17 @@ class PipelineRuntime:
             except RuntimeError as e:
                 log.warning("two-channel p2p order not provably safe (%s): single channel", e)
                 p2p.use_single_channel()
-        if self.coll_placement != "overlapped (independent queues, probed)":
+        if not self.coll_placement.startswith("overlapped"):
             check_lowered(program, S, serial=True, dp=self.dp)
         return program
+
+    @staticmethod
+    def _gloo(p2p) -> bool:
+        g = getattr(p2p, "group", None)
+        try:
+            return dist.is_initialized() and dist.get_backend(g) == "gloo"
+        except Exception:   # noqa: BLE001 - no group
+            return False
 
     # ------------------------------------------------------------------ lanes
     def set_lanes(self, n: int) -> int:

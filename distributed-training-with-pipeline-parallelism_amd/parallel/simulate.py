@@ -164,7 +164,7 @@ def to_grid(res: SimResult, pp: int) -> Dict[int, List[Optional[Action]]]:
 
 def message_channel(key: tuple) -> int:
     """Engine channel of a message: 0 = activations down the pipeline (F, H), 1 =
-    gradients back up (B, D) -- one RCCL communicator + stream each (csrc/comm/rccl_p2p.h)."""
+    gradients back up (B, D) -- one RCCL communicator + stream each (csrc/comm/rccl_engine.h)."""
     return 0 if key[0] in ("F", "H") else 1
 
 

@@ -69,3 +69,28 @@ def test_run_train_iterations_reports_bubble():
     assert "error" not in m, m
     assert 0.0 <= m["bubble_fraction"] < 1.0
     assert m["analytic_bubble"] == pytest.approx(1 / 5)
+
+
+def test_step_outputs_outlive_the_next_step_by_default():
+    """the native last stage merges its logits as a view of a persistent buffer
+    that the next step rewrites.  Default (reference semantics, torch.cat): a fresh
+    tensor, unchanged by later steps; ``copy_outputs=False``: the documented alias."""
+    import torch
+    from mipipe.models.ref_transformer import ModelArgs, tokenwise_loss_fn
+    from mipipe.models.stage import build_reference_stage
+    from mipipe.parallel.api import Schedule1F1B
+    torch.manual_seed(0)
+    a = ModelArgs(dim=64, n_layers=1, n_heads=4, vocab_size=100, dim_feedforward=128, dropout=0.0)
+    for copy in (True, False):
+        st = build_reference_stage(a, 0, 1, torch.device("cpu"), mbs=2, seq_len=8)
+        sched = Schedule1F1B(st, n_microbatches=2, loss_fn=tokenwise_loss_fn(a.vocab_size), copy_outputs=copy)
+        x1, x2 = torch.randint(0, 100, (4, 8)), torch.randint(0, 100, (4, 8))
+        y = torch.randint(0, 100, (4, 8))
+        o1 = sched.step(x1, target=y, losses=[])
+        keep = o1.clone()
+        o2 = sched.step(x2, target=y, losses=[])
+        assert not torch.equal(o2, keep)
+        if copy:
+            assert torch.equal(o1, keep) and o1.data_ptr() != o2.data_ptr()
+        elif o1.data_ptr() == o2.data_ptr():      # the alias: o1 now shows step 2's logits
+            assert torch.equal(o1, o2)

@@ -204,6 +204,18 @@ def test_recompute_auto_plan():
         dpz = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), stage_shards=2)
         nparams = cfg.layer_params() * (l4[1][1] - l4[1][0])
         assert rep["bytes_no_recompute"] - dpz["bytes_no_recompute"] == pytest.approx(6.0 * nparams)
+        # f32 arenas: the f32 weights are the master and stay whole, only the Adam
+        # moments (8 bytes) shard: 12 + 8/dp per parameter, so DP=2 saves 4 bytes, not 6
+        rep32 = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), dtype=torch.float32)
+        dpz32 = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), stage_shards=2,
+                               dtype=torch.float32)
+        assert rep32["bytes_no_recompute"] - dpz32["bytes_no_recompute"] == pytest.approx(4.0 * nparams)
+        assert dpz32["bytes_no_recompute"] > dpz["bytes_no_recompute"]
+        h32 = plan_recompute(cfg, l8, [7], o8, 1, 8192, torch.device("cuda", 0), head_tokens=1024, head_shards=8,
+                             dtype=torch.float32)
+        emb = cfg.vocab_padded * cfg.d_model
+        assert h32["head_optimizer_bytes"] == pytest.approx(8.0 * emb / 8)
+        assert h32["head_state_bytes"] == pytest.approx(12.0 * emb + 8.0 * emb / 8)
     finally:
         E.torch.cuda.get_device_properties = orig
     # 1F1B PP=4: rank 0 holds 4 microbatches in flight, the last rank 1; GPipe holds all m
@@ -246,9 +258,10 @@ def test_recv_arena_planned_up_front(split_head):
         assert res[1]["n_dh"] == M
 
 
-def _zero_worker(rank, world, name, pp, dp, zero, split_head=True, save=None, load=None):
+def _zero_worker(rank, world, name, pp, dp, zero, split_head=True, save=None, load=None, reduce_dtype="f32"):
     import os
     os.environ["MIPIPE_DP_ZERO"] = "1" if zero else "0"
+    os.environ["MIPIPE_DP_REDUCE_DTYPE"] = reduce_dtype
     cfg = CFG[name]()
     tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule="1F1B", n_microbatches=M, mbs=MBS, seq_len=S,
                          device=torch.device("cpu"), dtype=torch.float32, lr=1.0, adam_eps=1.0,
@@ -291,6 +304,24 @@ def test_dp_zero1_matches_replicated_dp(name, pp):
         for k, v in on[r]["sd"].items():
             torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(off[r]["sd"][k]), atol=1e-5, rtol=1e-5,
                                        msg=lambda m: f"{k}: {m}")
+
+
+def test_dp_bf16_reduce_scatter_tracks_f32():
+    """MIPIPE_DP_REDUCE_DTYPE=bf16 (half the bytes of the DP gradient reduce-scatter): the
+    replicas' weights stay identical and training tracks the f32 reduction to bf16
+    rounding of the gradient."""
+    world = 4
+    f32 = run_world(_zero_worker, world, "gpt2", 2, 2, True, True, None, None, "f32")
+    b16 = run_world(_zero_worker, world, "gpt2", 2, 2, True, True, None, None, "bf16")
+    for r in range(world):
+        assert b16[r]["losses"] == pytest.approx(f32[r]["losses"], rel=2e-2)
+        for k, v in b16[r]["sd"].items():
+            torch.testing.assert_close(torch.from_numpy(v), torch.from_numpy(f32[r]["sd"][k]), atol=3e-2, rtol=3e-2)
+    for r in range(2):   # DP peers (ranks r and r + pp) hold the same stage weights
+        for k, v in b16[r]["sd"].items():
+            assert (v == b16[r + 2]["sd"][k]).all(), k
+    # ... and the bf16 path did run: the rounding shows up somewhere
+    assert any((v != f32[r]["sd"][k]).any() for r in range(world) for k, v in b16[r]["sd"].items())
 
 
 def test_dp_zero1_checkpoint_resume(tmp_path):

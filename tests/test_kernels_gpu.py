@@ -581,11 +581,20 @@ def test_native_rccl_engine_self_transfer():
     h4 = eng.coll(2, 2, g, out)                      # all-gather into another buffer
     mx = torch.tensor([3.0], device=DEV)
     h5 = eng.coll(2, 3, mx, mx)                      # all-reduce max
-    for x in (h, h2, h3, h4, h5):
+    # reduce-scatter (the ZeRO-1 head / DP gradient path): 1 rank -> send numel == recv
+    # numel, in place (recv = send[0:n]) and into another buffer, f32 and bf16
+    rs = torch.randn(8192, device=DEV)
+    rs_ref = rs.clone()
+    h6 = eng.coll(2, 1, rs, rs[:8192])
+    rs16 = torch.randn(8192, device=DEV).to(torch.bfloat16)
+    rs16_out = torch.empty_like(rs16)
+    h7 = eng.coll(2, 1, rs16, rs16_out)
+    for x in (h, h2, h3, h4, h5, h6, h7):
         eng.wait(x)
     torch.cuda.synchronize()
     assert torch.equal(dst, src) and torch.equal(dst2, src2)
     assert torch.equal(g, ref) and torch.equal(out, ref) and float(mx) == 3.0
+    assert torch.equal(rs, rs_ref) and torch.equal(rs16_out, rs16)
     assert eng.query(h) and eng.query(h2)
     assert eng.async_error() == ""
     eng.close()
