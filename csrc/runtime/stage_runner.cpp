@@ -16,15 +16,18 @@
 //                    of an engine (the pipeline's or the DP group's): the gradient
 //                    reductions of REDUCE_GRAD and of the distributed head, ordered after
 //                    the compute stream on the collective stream slot; fills a slot
-//   WAIT   slot      the compute stream waits for that group's completion event
+//   WAIT   slot, s   stream s (the compute stream or a lane) waits for that group's
+//                    completion event
 //   CALL   fn        a Python callable (anything not expressible above: gloo transfers and
 //                    collectives on CPU) -- the GIL is taken only here; a GPU tape with the
 //                    native engines holds none
 //   SYNC   w, s      stream w waits for everything issued so far on stream s (an event)
 //
-// GRAPH and COPY carry the stream they were issued on (0 = the compute stream): with
-// microbatch lanes (parallel/runtime.py, PP = 1) the odd microbatches' graphs replay on a
-// second stream, forked from and joined back into the compute stream by SYNCs.
+// GRAPH, COPY and WAIT carry the stream they were issued on (0 = the compute stream): with
+// microbatch lanes (parallel/runtime.py) the odd microbatches' graphs replay on a second
+// stream, forked from and joined back into the compute stream by SYNCs; at PP > 1 a
+// receive feeding a lane's compute is waited for on that lane, and a POST carrying a
+// lane's output follows a SYNC of the compute stream on that lane.
 //
 // parallel/native_runner.py records the tape from one instrumented Python step and
 // `run()` replays it with the GIL released: no per-action Python, no allocator calls, no
@@ -130,11 +133,14 @@ class StageRunner {
     return tape_.back().slot;
   }
 
-  void add_wait(int64_t slot) {
+  // stream: the waiting stream (0 = the compute stream; a microbatch lane's stream when the
+  // receive feeds a compute issued on that lane)
+  void add_wait(int64_t slot, int64_t stream) {
     TORCH_CHECK(slot >= 0 && slot < nslots_, "stage runner: bad slot ", slot);
     Instr i;
     i.kind = WAIT;
     i.slot = slot;
+    i.stream = stream;
     tape_.push_back(std::move(i));
   }
 
@@ -192,7 +198,7 @@ class StageRunner {
           break;
         case WAIT:
           TORCH_CHECK(handles[i.slot] >= 0, "stage runner: WAIT before its POST (slot ", i.slot, ")");
-          engines[i.slot]->wait_raw(handles[i.slot], st);
+          engines[i.slot]->wait_raw(handles[i.slot], on(i.stream));
           handles[i.slot] = -2;  // consumed
           break;
         case CALL: {
@@ -269,7 +275,7 @@ class StageRunner {
     int kind = GRAPH;
     int64_t a = 0, b = 0, c = 0;
     int64_t slot = -1;
-    int64_t stream = 0;  // GRAPH / COPY: issuing stream (0 = compute stream)
+    int64_t stream = 0;  // GRAPH / COPY / WAIT: issuing (waiting) stream (0 = compute stream)
     int channel = 0;
     int op = 0;
     ncclDataType_t dtype = ncclFloat32;
@@ -315,7 +321,7 @@ void register_runner(py::module& m) {
       .def("add_sync", &StageRunner::add_sync, py::arg("waiter"), py::arg("signal"))
       .def("add_post", &StageRunner::add_post)
       .def("add_coll", &StageRunner::add_coll)
-      .def("add_wait", &StageRunner::add_wait)
+      .def("add_wait", &StageRunner::add_wait, py::arg("slot"), py::arg("stream") = 0)
       .def("add_call", &StageRunner::add_call)
       .def("run", &StageRunner::run)
       .def("set_profile", &StageRunner::set_profile)

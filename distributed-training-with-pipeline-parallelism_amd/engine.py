@@ -200,9 +200,13 @@ def auto_lanes(cfg: NativeConfig, pp: int, v: int, graphs: bool, device, m: int,
     stream's hardware queue: fixed by the queue probe, parallel/runtime.py), 594K with 4;
     GPT-2 small (16K-token microbatches, m = 2) 850K -> 888K with 2."""
     device = torch.device(device)
-    if not (pp == 1 and v == 1 and graphs and device.type == "cuda" and m >= 2):
+    if not (v == 1 and graphs and device.type == "cuda" and m >= 2):
+        return 1
+    if pp > 1 and os.environ.get("MIPIPE_PP_LANES", "1") == "0":
         return 1
     lanes = min(m, 4 if tokens <= 4096 else 2)
+    if pp > 1:
+        lanes = min(lanes, 2)   # a pipeline rank has at most F(i+w) and B(i) ready at once
     per_lane = 4.0 * params + layers * cfg.stash_bytes_per_layer(tokens, recompute=recompute)
     hbm = torch.cuda.get_device_properties(device).total_memory
     while lanes > 1 and (lanes - 1) * per_lane > 0.2 * hbm:
@@ -271,6 +275,7 @@ class PipelineTrainer:
             # no-bubble time in the same units (F = 1, B = 2 per stage-cost unit)
             self.planned_ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * n_microbatches / pp
             head_plan = HeadPlan(chunks, cfg.d_model, runner=self.head.run, dtype=dtype)
+            head_plan.arena = self.head.arena   # per-lane head gradients (PipelineRuntime.set_lanes)
             if graphs and self.device.type == "cuda":
                 from .parallel.graphs import GraphCache
                 head_plan.graphs = GraphCache(f"{self.mesh.pp_rank}")
@@ -401,9 +406,10 @@ class PipelineTrainer:
         return [_Chain()]
 
     def _auto_lanes(self, pp: int, v: int, graphs: bool, m: int, mbs: int, seq_len: int) -> int:
-        layers = sum(r1 - r0 for r0, r1 in self.layer_ranges)
-        return auto_lanes(self.cfg, pp, v, graphs, self.device, m, mbs * seq_len,
-                          sum(st.arena.numel for st in self.stages), layers, self.recompute)
+        layers = sum(self.layer_ranges[st.stage_index][1] - self.layer_ranges[st.stage_index][0]
+                     for st in self.stages)
+        params = sum(st.arena.numel for st in self.stages) + (self.head.arena.numel if self.head is not None else 0)
+        return auto_lanes(self.cfg, pp, v, graphs, self.device, m, mbs * seq_len, params, layers, self.recompute)
 
     @property
     def is_first(self) -> bool:

@@ -223,6 +223,7 @@ class HeadPlan:
     dtype: object = None
     offsets: List[int] = field(default_factory=list)
     graphs: object = None   # GraphCache: chunks replayed as HIP graphs after the first step
+    arena: object = None    # the head's ParamArena (per-lane gradients with microbatch lanes)
 
     def __post_init__(self):
         self.offsets = [sum(self.chunks[:r]) for r in range(len(self.chunks))]

@@ -120,7 +120,8 @@ class TapeRecorder:
                                     code)
 
     def native_wait(self, slot: int) -> None:
-        self.runner.add_wait(slot)
+        """The current stream (compute, or a microbatch lane) waits for the slot's group."""
+        self.runner.add_wait(slot, self._stream())
 
     def call(self, fn: Callable[[], None]) -> None:
         self.runner.add_call(fn)

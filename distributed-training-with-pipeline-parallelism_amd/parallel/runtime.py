@@ -268,46 +268,82 @@ class PipelineRuntime:
         attention grids) and pay a dependent-kernel boundary per launch; two microbatches'
         graphs replayed concurrently overlap both (tools/lane_probe.py, reference model: F||F
         1.53x, B||B 1.57x, F||B 1.27x).  Each lane accumulates into its own gradient buffer
-        (ParamArena.lane), summed into lane 0 at the join; the dW side stream is turned off
-        (a forked graph did not overlap with the other lane).  Only at PP = 1 with one stage
-        per rank: there are no transfers to order against.  Returns the lanes in use."""
+        (ParamArena.lane) -- the stage's and the distributed head's -- summed into lane 0 at
+        the join; the dW side stream is turned off (a forked graph did not overlap with the
+        other lane).
+
+        PP > 1 (one stage per rank): in the 1F1B steady state F(i+w) and B(i) are both ready;
+        on two lanes they overlap (a 32-sequence GPT-2 microbatch on one stream runs at 0.95x
+        of two concurrent ones, profiles/r3_lane1_mbs_ab.txt).  A receive is waited for on
+        the lane of the compute it feeds; a post carrying a lane's output is ordered after
+        that lane (SYNC); the head's lanes are merged at REDUCE_HEAD, the stage's at
+        REDUCE_GRAD.  Lane streams must have hardware queues of their own -- apart from the
+        compute stream and, at PP > 1, every comm stream (the probe) -- or lanes stay off.
+        Returns the lanes in use."""
         n = max(1, int(n))
-        if n > 1 and (self.pp != 1 or len(self.stages) != 1 or self.device.type != "cuda" or self.m < 2):
+        if n > 1 and (len(self.stages) != 1 or self.device.type != "cuda" or self.m < 2):
             n = 1
         self.lane_streams = [None]
         idx = (self.device.index if self.device.index is not None else torch.cuda.current_device()) if n > 1 else 0
         # one set of lane streams per device and process: HIP maps each stream onto one of
-        # GPU_MAX_HW_QUEUES (4) hardware queues when it is created, and two lanes (or a lane
-        # and the compute stream) sharing a queue serialise.  torch's pool hands streams out
+        # GPU_MAX_HW_QUEUES hardware queues when it is created, and two lanes (or a lane and
+        # the compute stream) sharing a queue serialise.  torch's pool hands streams out
         # round-robin, so trainers built later in a process would get other queue mappings
         # (the reference 9-config table measured 444K tok/s for L8H8 vs 594K in a fresh
         # process); the first ones taken are reused instead
         cache = _LANE_STREAMS.setdefault(idx, [])
         main_s = torch.cuda.current_stream(idx).cuda_stream if n > 1 else None
+        avoid = [main_s]
+        if n > 1 and self.pp > 1:
+            kind = getattr(self.p2p, "kind", "")
+            if kind == "native":
+                from .queues import comm_streams
+                avoid += list(comm_streams(self.device).values())
+            elif kind != "gloo-staged":
+                n = 1       # torch p2p: its communicators' streams are not ours to probe
+            # (gloo-staged -- ranks sharing one GPU in a rehearsal -- moves bytes through the
+            # host on the issuing stream: no comm stream to keep clear)
         # ... and a lane must not land on the compute stream's hardware queue or another
         # lane's: the spin/flag probe (parallel/queues.py, profiles/r3_queue_probe.json)
         # found torch's second pool stream on the compute stream's queue -- the 3-lane
         # anomaly of round 2 (456K tok/s vs 495K with 2 lanes, 594K with 4).  Candidates are
         # drawn from the pool until one has a queue of its own (at most 4 per priority).
+        chosen: List[torch.cuda.Stream] = []
+        if n > 1:
+            for c in cache:
+                if len(chosen) < n - 1 and self._own_queue(c, avoid + [x.cuda_stream for x in chosen]):
+                    chosen.append(c)
         tried = 0
-        while len(cache) < n - 1 and tried < 64:
+        while n > 1 and len(chosen) < n - 1 and tried < 64:
             tried += 1
             ls = torch.cuda.Stream(device=idx)
-            if ls.cuda_stream == main_s or any(ls.cuda_stream == c.cuda_stream for c in cache):
+            if ls.cuda_stream in avoid or any(ls.cuda_stream == c.cuda_stream for c in cache):
                 continue
-            if not self._own_queue(ls, [main_s] + [c.cuda_stream for c in cache]):
+            if not self._own_queue(ls, avoid + [c.cuda_stream for c in chosen]):
                 continue
             cache.append(ls)
-        n = min(n, len(cache) + 1)
+            chosen.append(ls)
+        n = min(n, len(chosen) + 1)
+        if n > 1 and self.pp > 1 and self.coll_placement.startswith("overlapped"):
+            # the exact program with its lane queues, under the model the placement relies on
+            from .simulate import check_lowered
+            check_lowered(self.program_all, self.num_stages, channels=getattr(self.p2p, "channels", 1), dp=self.dp,
+                          lanes=n)
         self.lanes = n
-        self.lane_streams += cache[: n - 1]
+        self.lane_streams += chosen[: n - 1]
         for st in self.stages.values():
             st.arena.set_lanes(n)
             if hasattr(st, "model"):
                 st.model.wgrad_side = n == 1
+        ha = self._head_arena()
+        if ha is not None:
+            ha.set_lanes(n)
         self.native_runner = None   # a recorded tape does not know about lanes
         self._tapes.clear()
         return n
+
+    def _head_arena(self):
+        return getattr(self.head, "arena", None) if self.head is not None else None
 
     def _own_queue(self, s: torch.cuda.Stream, others) -> bool:
         """True if stream ``s`` shares a hardware queue with none of ``others`` (probe; true
@@ -322,16 +358,53 @@ class PipelineRuntime:
             return True
 
     def _lane_ctx(self, a: Action, st):
-        """Stream + gradient-lane context of one compute action."""
-        if self.lanes == 1 or a.op not in (Op.F, Op.B, Op.I, Op.W):
+        """Stream + gradient-lane context of one compute action (every arena it may
+        accumulate into: the stage's, and the distributed head's -- which a tied
+        embedding's backward on stage 0 writes too)."""
+        self._cur_lane = 0
+        if self.lanes == 1 or a.op not in (Op.F, Op.B, Op.I, Op.W, Op.H):
             return contextlib.nullcontext()
         ln = a.mb % self.lanes
+        self._cur_lane = ln
         if ln == 0:
             return contextlib.nullcontext()
         cm = contextlib.ExitStack()
         cm.enter_context(torch.cuda.stream(self.lane_streams[ln]))
-        cm.enter_context(st.arena.lane(ln))
+        if st is not None:
+            cm.enter_context(st.arena.lane(ln))
+        ha = self._head_arena()
+        if ha is not None and (st is None or ha is not st.arena):
+            cm.enter_context(ha.lane(ln))
         return cm
+
+    def _order_posts_after_lanes(self, lanes_used, rec) -> None:
+        """A group sending tensors produced on a lane: the compute stream (which orders the
+        engine's post) first waits for that lane."""
+        if self.lanes == 1:
+            return
+        main = torch.cuda.current_stream(self.device)
+        for ln in sorted(lanes_used):
+            if ln:
+                ls = self.lane_streams[ln]
+                main.wait_stream(ls)
+                if rec is not None:
+                    rec.sync(main, ls)
+
+    def _join_head_lanes(self, rec) -> None:
+        """REDUCE_HEAD: the compute stream waits for every lane, and the head arena's lane
+        gradients are summed into lane 0 before its reduction is issued."""
+        ha = self._head_arena()
+        if self.lanes == 1 or ha is None:
+            return
+        main = torch.cuda.current_stream(self.device)
+        for ls in self.lane_streams[1:]:
+            main.wait_stream(ls)
+            if rec is not None:
+                rec.sync(main, ls)
+        if self.head.graphs is not None and self._steps > 1:
+            self.head.graphs.run(("M", 0), (), lambda ins: ha.merge_lanes())
+        else:
+            ha.merge_lanes()
 
     def _fork_lanes(self, rec) -> None:
         if self.lanes == 1:
@@ -656,17 +729,23 @@ class PipelineRuntime:
             if deps is not None:
                 deps.on_produce(key, action, tensors)
             (handoff if local else send_tensors)[key] = tensors
+            if not local:
+                send_lane[key] = self._cur_lane
 
         def rng(a):
             if not self.ranges:
                 return contextlib.nullcontext()
             return _Range(f"PP:{a}")
 
+        send_lane: Dict[tuple, int] = {}
+        self._cur_lane = 0
         self._fork_lanes(rec)
         for idx, e in enumerate(self.program):
             try:
                 if isinstance(e, CommGroup):
                     sends, recvs, rkeys, sch, rch = [], [], [], [], []
+                    self._order_posts_after_lanes({send_lane.pop(op.key, 0) for op in e.ops
+                                                   if op.action.op.is_send}, rec)
                     for op in e.ops:
                         ch = message_channel(op.key)
                         if op.action.op.is_send:
@@ -690,6 +769,7 @@ class PipelineRuntime:
                     continue
                 a = e
                 if a.op == Op.REDUCE_HEAD:
+                    self._join_head_lanes(rec)
                     if self.head_reduce is not None:
                         reduce_works.extend(self.head_reduce())
                     continue
@@ -711,7 +791,7 @@ class PipelineRuntime:
                     if w is not None:
                         reduce_works.append(w)
                     continue
-                with self._lane_ctx(a, st):
+                with self._lane_ctx(a, st if a.op != Op.H else None):
                     t_s = self.timer.mark() if self.profile else None
                     ready[0] = None
                     with rng(a):

@@ -169,7 +169,7 @@ def message_channel(key: tuple) -> int:
 
 
 def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: int = 1, serial: bool = False,
-                  dp: int = 1) -> None:
+                  dp: int = 1, lanes: int = 1) -> None:
     """Raise RuntimeError if the lowered program can hang under RCCL semantics.
 
     Queues of a rank (each a FIFO in host issue order = program order):
@@ -191,7 +191,15 @@ def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: in
     when it starts; a p2p group when every message in it has both endpoint groups started;
     a collective when every member has started it (``REDUCE_HEAD``: every rank of the
     program; ``REDUCE_GRAD``: the same stage of the DP replicas, which run this program
-    symmetrically).  A fixpoint that does not drain every queue means a possible hang."""
+    symmetrically).  A fixpoint that does not drain every queue means a possible hang.
+
+    ``lanes`` (independent model): microbatch lanes (PipelineRuntime.set_lanes) -- the
+    compute of microbatch mb is a FIFO of its own per lane ``mb % lanes`` (the lane streams
+    have hardware queues of their own, probed); a comm group or collective still waits for
+    every compute issued before it (the runtime orders a post after the lanes whose output
+    it sends, a reduction after all of them).  Splitting the compute FIFO only removes
+    ordering edges, so a program proven with ``lanes=1`` is safe with any lane count; the
+    parameter lets the runtime prove the exact program it runs."""
     comp_orders = {r: [e for e in es if isinstance(e, Action) and e.op.is_compute] for r, es in program.items()}
     split = uses_split_backward(comp_orders)
     head = head_ranks_of(comp_orders)
@@ -211,7 +219,8 @@ def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: in
                 for ch in sorted(by_ch):
                     lst.append((0 if serial else ("p", ch), "g", by_ch[ch], ncomp - 1))
             elif e.op.is_compute:
-                lst.append((0 if serial else "c", "c", e, ncomp - 1))
+                cq = "c" if (lanes <= 1 or e.mb is None) else ("c", e.mb % lanes)
+                lst.append((0 if serial else cq, "c", e, ncomp - 1))
                 ncomp += 1
             elif e.op == Op.REDUCE_HEAD:
                 lst.append((0 if serial else "x", "x", ("RH",), ncomp - 1))

@@ -55,6 +55,10 @@ def test_multirank_gpu_matches_single(reference, n, schedule, graphs, split, dp)
     # with graphs, steps after the first replay run from the native stage runner's tape
     # (gloo transfers recorded as CALLs)
     assert res["native_runner"] == bool(graphs), res["native_reason"]
+    # microbatch lanes at PP > 1 too (one stage per rank, graphs): two lane streams with
+    # per-lane stage + head gradients, sends ordered after their lane
+    if graphs and schedule in ("1F1B", "GPipe"):
+        assert res["lanes"] >= 2, res
 
 
 @pytest.mark.parametrize("n,graphs,split", [(2, 1, 1), (4, 1, 1), (4, 0, 0)])

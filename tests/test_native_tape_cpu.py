@@ -217,7 +217,7 @@ class FakeRunner:
     def collectives(self):
         return [(x[1], x[2]) for k, x in self.tape if k == COLL]
 
-    def add_wait(self, slot):
+    def add_wait(self, slot, stream=0):
         self.tape.append((WAIT, slot))
 
     def add_call(self, fn):

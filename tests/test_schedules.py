@@ -282,3 +282,23 @@ def test_interleaved_with_head_plans_ahead_of_1f1b_and_gpipe(P):
         eff[name] = (3.0 * sum(sc) + sum(hc.values())) * m / P / mk
     assert eff["Interleaved1F1B"] > max(eff["1F1B"], eff["GPipe"]) + 0.02, eff
     assert eff["1F1B"] >= eff["GPipe"] - 1e-6, eff
+
+
+@pytest.mark.parametrize("name,v", [("GPipe", 1), ("1F1B", 1), ("Interleaved1F1B", 2)])
+@pytest.mark.parametrize("P", [2, 4, 8])
+@pytest.mark.parametrize("dp", [1, 2])
+def test_overlapped_programs_proven_with_and_without_lanes(name, v, P, dp):
+    """every PP x DP x schedule program with its collectives left in place
+    (REDUCE_GRAD right after the stage's last backward, REDUCE_HEAD after the last head
+    chunk) passes the independent-queue model on 1 and 2 channels, and with two
+    microbatch lanes per rank; the deferred placement passes the serial model."""
+    from mipipe.parallel.lower import add_head_reduce, defer_collectives
+    m = 4 * P
+    orders = generate(name, P, m, v)
+    hc = {r: 0.5 for r in range(P)}
+    ho, _, _ = plan_head_schedule(orders, P, v, "loop", hc)
+    prog = add_head_reduce(lower(ho, P, v, "loop", head_costs=hc))
+    for ch in (1, 2):
+        for lanes in (1, 2):
+            check_lowered(prog, P * v, channels=ch, dp=dp, lanes=lanes)
+    check_lowered(defer_collectives(prog), P * v, serial=True, dp=dp)

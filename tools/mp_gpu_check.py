@@ -57,7 +57,8 @@ def main():
         print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses,
                           "native_runner": tr.runtime.native_runner is not None,
                           "native_reason": tr.runtime.native_reason,
-                          "p2p": getattr(tr.runtime.p2p, "kind", None)}), flush=True)
+                          "p2p": getattr(tr.runtime.p2p, "kind", None), "lanes": tr.runtime.lanes,
+                          "placement": tr.runtime.coll_placement}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -72,11 +72,12 @@ def main():
         "graph_pairs": graph_pairs,
         "shared_pairs": shared,
         "comm_streams_independent_of_rank_streams": not comm_shared,
-        "runtime_conclusion": ("collectives may overlap the flush (MIPIPE_COLL_OVERLAP=1 admissible)"
+        "runtime_conclusion": ("collectives overlap the flush (the default MIPIPE_COLL_OVERLAP=probe admits it)"
                                if not comm_shared else
-                               "comm streams share queues: collectives must run at the step end (default)"),
-        "note": ("the runtime's default (collectives at the step end, serial-model proof) does not depend on "
-                 "this map; it decides only whether the opt-in overlap is admissible"),
+                               "comm streams share queues: collectives deferred to the step end (serial model)"),
+        "note": ("PipelineRuntime._prove runs this probe per rank and MIN-votes the verdict over the world; "
+                 "microbatch lanes at PP > 1 are accepted only on streams with queues apart from compute "
+                 "and every comm stream"),
     }
     txt = json.dumps(out, indent=1)
     print(txt)
