@@ -28,6 +28,8 @@
 //  * two accumulator chains per wave (even / odd 8-deep k groups), summed at the end;
 //  * few tiles (the reference's 1024-token GEMMs: 192-576 tiles for 256 CUs): split K over
 //    workgroups into f32 slabs, summed by one reduce + epilogue pass -- deterministic.
+#include <cstdlib>
+
 #include "mp_common.h"
 
 using namespace mp;
@@ -281,6 +283,174 @@ static int launch(Args p, int split, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// 128x128 engine (the guide's "128x128x32 block, 2x2 tiles of 32x32 per wave" shape, cdna
+// guide §3 'FP32-input MFMA': 122 TF untuned at 4096^3).  Per byte staged it does twice the
+// MFMA work of the 64x64 engine (32 vs 16 FLOP/B of operand), and each wave keeps FOUR
+// independent 32x32 accumulators (64 AGPRs) -- the f32 MFMA's 64-cycle dependent latency
+// equals its issue interval, so 4 chains keep the pipe full from one wave per SIMD:
+//  * 256 threads = 4 waves, wave (wr, wc) owns rows 64 wr.., cols 64 wc.. of the tile;
+//  * K-tile 32, two LDS buffers (row image [128][36] or column image [32][136] per
+//    operand, 18 KiB each); the next K-tile's 4 float4 per thread per operand are loaded
+//    into registers while the current one feeds 64 MFMAs per wave, then stored to the
+//    other buffer -- one barrier per K-tile;
+//  * fragments, k permutation, split-K slabs and epilogue as the 64x64 engine.
+constexpr int NTH2 = 256, BT2 = 128, CS2 = BT2 + 8;
+constexpr int OPS2 = BT2 * KS;      // 4608 floats >= BK * CS2 = 4352
+static_assert(BK * CS2 <= OPS2, "column image must fit the operand slot");
+
+template <bool KC>
+struct Stage2 {
+  float4 r[4];
+  uint32_t ok;
+  __device__ __forceinline__ void load(const float* __restrict__ P, int64_t ld, int o0, int n_outer, int k0, int K) {
+    const int t = threadIdx.x;
+    ok = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = t + NTH2 * u;
+      if constexpr (KC) {        // 1024 float4: [row 128][c 8]
+        const int row = f >> 3, c = f & 7;
+        const int o = min(o0 + row, n_outer - 1), k = k0 + 4 * c;
+        ok |= (k < K ? 1u : 0u) << u;
+        r[u] = *reinterpret_cast<const float4*>(P + (int64_t)o * ld + min(k, K - 4));
+      } else {                   // 1024 float4: [k 32][c 32]
+        const int kk = f >> 5, c = f & 31;
+        const int o = min(o0 + 4 * c, n_outer - 4), k = k0 + kk;
+        ok |= (k < K ? 1u : 0u) << u;
+        r[u] = *reinterpret_cast<const float4*>(P + (int64_t)min(k, K - 1) * ld + o);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* __restrict__ s) const {
+    const int t = threadIdx.x;
+    const float4 z = float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int f = t + NTH2 * u;
+      const float4 v = (ok >> u) & 1u ? r[u] : z;
+      if constexpr (KC) {
+        const int row = f >> 3, c = f & 7;
+        *reinterpret_cast<float4*>(s + row * KS + 4 * c) = v;
+      } else {
+        const int kk = f >> 5, c = f & 31;
+        *reinterpret_cast<float4*>(s + kk * CS2 + 4 * c) = v;
+      }
+    }
+  }
+  // the lane's 4 operand values (k = 8g + 4hl + j) of outer index w0 + l32
+  static __device__ __forceinline__ float4 frag(const float* __restrict__ s, int w0, int g, int l32, int hl) {
+    if constexpr (KC) {
+      return *reinterpret_cast<const float4*>(s + (w0 + l32) * KS + 8 * g + 4 * hl);
+    } else {
+      const float* c = s + (8 * g + 4 * hl) * CS2 + w0 + l32;
+      return float4{c[0], c[CS2], c[2 * CS2], c[3 * CS2]};
+    }
+  }
+};
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ void __launch_bounds__(NTH2, 2) gemm_f32_big_kernel(Args p) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * OPS2];   // [buf][A|B][image]
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hl = lane >> 5;
+  const int wave = tid >> 6, wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int gn = (p.N + BT2 - 1) / BT2;
+  const int tile = blockIdx.x;
+  const int m0 = (tile / gn) * BT2, n0 = (tile % gn) * BT2;
+  const int nkt = (p.K + BK - 1) / BK;
+  const int nsplit = gridDim.y;
+  const int kt0 = (int)blockIdx.y * nkt / nsplit, kt1 = ((int)blockIdx.y + 1) * nkt / nsplit;
+
+  Stage2<A_KC> sa;
+  Stage2<B_KC> sb;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) acc[i][0] = acc[i][1] = f32x16{};
+  if (kt0 < kt1) {
+    sa.load(p.A, p.lda, m0, p.M, kt0 * BK, p.K);
+    sb.load(p.B, p.ldb, n0, p.N, kt0 * BK, p.K);
+    sa.store(smem);
+    sb.store(smem + OPS2);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) {     // next K-tile in flight while this one is in the MFMAs
+      sa.load(p.A, p.lda, m0, p.M, (kt + 1) * BK, p.K);
+      sb.load(p.B, p.ldb, n0, p.N, (kt + 1) * BK, p.K);
+    }
+    const float* As = smem + buf * 2 * OPS2;
+    const float* Bs = As + OPS2;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      float4 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = Stage2<A_KC>::frag(As, wm + 32 * i, g, l32, hl);
+        b[i] = Stage2<B_KC>::frag(Bs, wn + 32 * i, g, l32, hl);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      float* nb = smem + (buf ^ 1) * 2 * OPS2;   // last read before the previous barrier
+      sa.store(nb);
+      sb.store(nb + OPS2);
+    }
+    __syncthreads();
+  }
+  uint32_t thr = 0;
+  float inv = 1.f;
+  uint64_t seed = p.seed;
+  if ((EPI == E_BIAS_RELU || EPI == E_DRELU) && p.p_drop > 0.f && p.ws == nullptr) {
+    seed = step_seed(seed);
+    thr = drop_thr(p.p_drop);
+    inv = 1.f / (1.f - p.p_drop);
+  }
+  float* slab = p.ws != nullptr ? p.ws + (int64_t)blockIdx.y * p.M * p.N : nullptr;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    // acc[i][j] element r -> row m0 + wm + 32 i + (r & 3) + 8 (r >> 2) + 4 hl, col n0 + wn + 32 j + l32
+    const int col = n0 + wn + 32 * j + l32;
+    if (col >= p.N) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hl;
+        if (row >= p.M) continue;
+        if (slab != nullptr) slab[(int64_t)row * p.N + col] = acc[i][j][r];
+        else epi_store<EPI>(p, row, col, acc[i][j][r], thr, inv, seed);
+      }
+  }
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+static int launch_big(Args p, int split, hipStream_t st) {
+  const int tiles = ((p.M + BT2 - 1) / BT2) * ((p.N + BT2 - 1) / BT2);
+  gemm_f32_big_kernel<A_KC, B_KC, EPI><<<dim3(tiles, split), NTH2, 0, st>>>(p);
+  if (split > 1) {
+    const int64_t n4 = (int64_t)p.M * p.N / 4;
+    reduce_kernel<EPI><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(p, split);
+  }
+  return (int)hipGetLastError();
+}
+
 // split-K factor: minimise the busiest CU's work, in K-tile-pair units: the workgroups it
 // runs (tiles x s over 256 CUs) x (its pairs + ~3 pairs of prologue / epilogue latency),
 // plus ~1 for the slab pass.  Fitted to the measured s = 1..8 sweep of the reference's
@@ -303,11 +473,60 @@ static int pick_split(int M, int N, int K) {
   return best;
 }
 
+// the 128x128 engine's split and cost in the same units as pick_split's (one 64x64 K-tile
+// pair = 2 K-tiles of 64x64x32; a 128x128 K-tile is 2 such pairs' MFMA work): rounds of
+// 256 CUs x (pairs + fixed latency), with the measured MFMA efficiencies folded in
+static int pick_split_big(int M, int N, int K, double* cost_out) {
+  const int tiles = ((M + BT2 - 1) / BT2) * ((N + BT2 - 1) / BT2);
+  const int nkt = (K + BK - 1) / BK;
+  int best = 1;
+  double best_cost = 1e30;
+  for (int s = 1; s <= 8; ++s) {
+    if (s > 1 && nkt < 2 * s) break;
+    const double rounds = (double)((tiles * s + 255) / 256);
+    const double cost = rounds * (2.0 * nkt / s + 4.0) + (s > 1 ? 1.0 : 0.0);
+    if (cost < best_cost - 1e-9) {
+      best_cost = cost;
+      best = s;
+    }
+  }
+  if (cost_out) *cost_out = best_cost;
+  return best;
+}
+
+// engine + split: MIPIPE_F32_TILE = 64 | 128 | auto.  auto takes the 128x128 engine only
+// when its grid fills whole rounds of 2 workgroups per CU (>= 85 % of the last round) --
+// measured on the reference's 1024-token shapes (profiles/r4_f32_gemm_sweep_64_vs_128.txt):
+// the dW of the LM head (474 tiles) 152 vs 164 us, while every few-tile layer GEMM needs a
+// split the 64x64 engine does better (dX of qkv: 48 tiles, 56 us at split 8 vs 47 us)
+struct Plan {
+  bool big;
+  int split;
+};
+static Plan plan(int M, int N, int K, int force_split) {
+  static const int mode = [] {
+    const char* e = getenv("MIPIPE_F32_TILE");
+    if (e && e[0] == '6') return 64;
+    if (e && e[0] == '1') return 128;
+    return 0;
+  }();
+  bool big = mode == 128;
+  if (mode == 0) {
+    const int tiles = ((M + BT2 - 1) / BT2) * ((N + BT2 - 1) / BT2);
+    const int rounds = (tiles + 511) / 512;
+    big = tiles >= 448 && (double)tiles >= 0.85 * 512.0 * rounds;
+  }
+  int split = big ? pick_split_big(M, N, K, nullptr) : pick_split(M, N, K);
+  if (big && mode == 0) split = 1;      // a full grid needs no split
+  if (force_split > 0) split = force_split;
+  return Plan{big, split};
+}
+
 }  // namespace gf32
 
 // floats of split-K workspace a problem needs (0: no split)
 extern "C" int64_t mp_gemm_f32_ws_elems(int M, int N, int K, int force_split) {
-  const int s = force_split > 0 ? force_split : gf32::pick_split(M, N, K);
+  const int s = gf32::plan(M, N, K, force_split).split;
   return (s > 1 && M % 4 == 0 && N % 4 == 0) ? (int64_t)s * M * N : 0;
 }
 
@@ -324,12 +543,19 @@ extern "C" int mp_gemm_f32_ex(const float* A, const float* B, float* C, const fl
   if (M <= 0 || N <= 0) return 0;
   if (K % 4 || M % 4 || N % 4 || lda % 4 || ldb % 4) return -1;
   if ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(B)) & 15) return -1;
-  int split = force_split > 0 ? force_split : pick_split(M, N, K);
+  const Plan pl = plan(M, N, K, force_split);
+  int split = pl.split;
   if (ws == nullptr) split = 1;
   Args p{A, B, C, bias, R, X, split > 1 ? ws : nullptr, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, accumulate,
          p_drop, seed};
 #define MP_E(E)                                                                                      \
   case E:                                                                                            \
+    if (pl.big) {                                                                                    \
+      if (a_kc && b_kc) return launch_big<true, true, E>(p, split, st);                              \
+      if (a_kc) return launch_big<true, false, E>(p, split, st);                                     \
+      if (b_kc) return launch_big<false, true, E>(p, split, st);                                     \
+      return launch_big<false, false, E>(p, split, st);                                              \
+    }                                                                                                \
     if (a_kc && b_kc) return launch<true, true, E>(p, split, st);                                    \
     if (a_kc) return launch<true, false, E>(p, split, st);                                           \
     if (b_kc) return launch<false, true, E>(p, split, st);                                           \

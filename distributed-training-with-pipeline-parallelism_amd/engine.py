@@ -312,7 +312,7 @@ class PipelineTrainer:
                                            seed=seed + 1000 * self.mesh.dp_rank, graphs=graphs))
         p2p = P2P(self.mesh.pp_group, self.mesh.pipe_ranks, self.device, ctrl_group=self.mesh.ctrl_group)
         # every collective of the step (DP all-reduce, head reduction, clip norm, losses)
-        self.coll = Collectives(self.mesh, self.device, pipe_engine=p2p.engine)
+        self.coll = Collectives(self.mesh, self.device, pipe_engine=p2p.engine, embed=tied_pp)
         for st in self.stages:
             st.coll = self.coll
         self.runtime = PipelineRuntime(self.stages, self.schedule, n_microbatches, self.mesh.pp_rank, pp, p2p,

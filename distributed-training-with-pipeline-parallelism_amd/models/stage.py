@@ -229,7 +229,13 @@ class NativeStage(StageBase):
 
     def post_step(self):
         if self.embed_group is not None and self.cfg.tie_embeddings and self.arena.has("tok_embeddings.weight"):
-            dist.all_reduce(self.arena.g("tok_embeddings.weight"), group=self.embed_group)
+            g = self.arena.g("tok_embeddings.weight")
+            if self.coll is not None:
+                # parallel/collectives.py "embed" scope: the native 2-rank engine on GPUs (a
+                # stream-ordered RCCL all-reduce, no host block), torch.distributed elsewhere
+                self.coll.all_reduce(g, "embed").wait()
+            else:
+                dist.all_reduce(g, group=self.embed_group)
 
 
 def build_reference_stage(args, stage_index: int, num_stages: int, device, mbs: int = 8, seq_len: int = 128,

@@ -12,6 +12,7 @@ head grad reduce       ``pp``    ``REDUCE_HEAD``: reduce-scatter of the replicat
 clip-norm sum          ``pp``    FlatAdamW.step (4 bytes)
 loss sum               ``pp``    PipelineTrainer.train_step (one float per microbatch)
 head weight gather     ``pp``    all-gather of the updated bf16 head shards
+tied embedding sum     ``embed`` first + last stage (no distributed head): NativeStage.post_step
 =====================  ========  ============================================================
 
 On GPUs with the RCCL backend the pipeline group's collectives run on the pipeline
@@ -99,7 +100,7 @@ class Collectives:
     backend, GPUs) and ``dp > 1``.  Each call returns a work handle (``wait()``), or one
     that is already complete when the group has a single rank."""
 
-    def __init__(self, mesh, device: torch.device, pipe_engine=None):
+    def __init__(self, mesh, device: torch.device, pipe_engine=None, embed: bool = False):
         self.mesh = mesh
         self.device = torch.device(device)
         self.pp_group, self.dp_group = mesh.pp_group, mesh.dp_group
@@ -116,6 +117,15 @@ class Collectives:
         if self.dp > 1 and self.dp_transport_native(mesh):
             dp_ranks = [d * self.pp + mesh.pp_rank for d in range(self.dp)]
             self.dp_engine = make_dp_engine(self.dp_group, dp_ranks, mesh.dp_rank, self.device)
+        # the tied embedding's two copies (first + last stage, no distributed head): a
+        # 2-rank engine over mesh.embed_group on the same collective slot
+        self.embed_group = getattr(mesh, "embed_group", None) if embed else None
+        self.embed_engine = None
+        if (self.embed_group is not None and self.pipe_engine is not None and self.device.type == "cuda"
+                and os.environ.get("MIPIPE_COLL", "native") != "torch"):
+            d = mesh.dp_rank
+            ranks = sorted({d * self.pp, d * self.pp + self.pp - 1})
+            self.embed_engine = make_dp_engine(self.embed_group, ranks, ranks.index(mesh.rank), self.device)
         if self.pp > 1 and self.pipe_engine is None:
             self.pp_kind = "torch"
         else:
@@ -149,14 +159,20 @@ class Collectives:
         return f"pp:{self.pp_kind},dp:{self.dp_kind}"
 
     def _size(self, scope: str) -> int:
+        if scope == "embed":
+            return dist.get_world_size(self.embed_group) if self.embed_group is not None else 1
         return self.pp if scope == "pp" else self.dp
 
     def _engine(self, scope: str):
         if scope == "pp":
             return self.pipe_engine, PIPE_COLL_CHANNEL
+        if scope == "embed":
+            return self.embed_engine, 0
         return self.dp_engine, 0
 
     def _group(self, scope: str):
+        if scope == "embed":
+            return self.embed_group
         return self.pp_group if scope == "pp" else self.dp_group
 
     # ------------------------------------------------------------------ issue
@@ -235,6 +251,8 @@ class Collectives:
         return self._torch(lambda: dist.all_gather_into_tensor(full, shard.clone(), group=g, async_op=True))
 
     def close(self) -> None:
-        if self.dp_engine is not None:
-            self.dp_engine.close()
-            self.dp_engine = None
+        for name in ("dp_engine", "embed_engine"):
+            eng = getattr(self, name)
+            if eng is not None:
+                eng.close()
+                setattr(self, name, None)
