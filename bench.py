@@ -41,8 +41,10 @@ Hang safety: the pipeline program is PROVEN hang-free before it runs
 supervisor.  The child arms a watchdog over init, warmup, every timed step and the bubble
 step (on a stall it prints the program grid + all stacks and exits non-zero); the
 process-group timeout is 300 s.  If the headline fails on any rank, the supervisors retry
-it in a more conservative mode (torch p2p, then no HIP graphs) on a fresh rendezvous
-port; the ``attempt`` field says which one produced the number.  One global deadline
+it in a more conservative mode (the native engine with collectives deferred to the step
+end and one compute stream per rank, then torch p2p, then no HIP graphs) on a fresh
+rendezvous port; ``attempt`` / ``attempt_mode`` say which one produced the number, and
+the other schedules run in that mode.  One global deadline
 (MIPIPE_BENCH_DEADLINE_S, default 540 s, under the driver's 600 s) bounds everything:
 each child gets at most what is left of it (and at most MIPIPE_BENCH_ATTEMPT_S, default
 240 s), its watchdogs are clamped to that.  Supervisors never touch the GPU.
@@ -71,8 +73,10 @@ METRIC = ("tokens/sec/node + pipeline bubble fraction, GPT-2 PP=1/2/4/8 (GPipe v
 BASELINE_NOTE = ("no same-config reference number: BASELINE.md only has the reference's fp32 toy model "
                  "(L4-12, d768, seq 128) on a 10-core CPU/gloo; see profiles/ for that table on MI355X")
 
-# supervisor attempts of the headline: (p2p transport, HIP graphs + native tape)
-ATTEMPTS = [("auto", 1), ("torch", 1), ("torch", 0)]
+# supervisor attempts of the headline: (p2p transport, HIP graphs + native tape).  "-safe":
+# the native engine with the round-4 concurrency features off -- collectives deferred to
+# the step end (serial-model proof) and one compute stream per pipeline rank
+ATTEMPTS = [("auto", 1), ("auto-safe", 1), ("torch", 1), ("torch", 0)]
 # the reference's three schedules (helper:215-220), measured back to back in one call
 SCHEDULES = ("GPipe", "1F1B", "Interleaved1F1B")
 # published L8 H8 rows of the reference (nb:703-708): (schedule, P) -> tok/s
@@ -252,9 +256,11 @@ def supervise(a, argv) -> int:
 
     def run_child(j, tag, child_argv, p2p, graphs, attempt, budget):
         res_path = os.path.join(d, f"{tag}.json")
-        env = dict(os.environ, MIPIPE_BENCH_CHILD="1", MIPIPE_P2P=p2p, MIPIPE_BENCH_ATTEMPT=str(attempt),
+        env = dict(os.environ, MIPIPE_BENCH_CHILD="1", MIPIPE_P2P=p2p.split("-")[0], MIPIPE_BENCH_ATTEMPT=str(attempt),
                    MASTER_PORT=str(base_port + 1 + j), MIPIPE_BENCH_ATTEMPT_S=f"{budget:.0f}",
-                   MIPIPE_BENCH_RESULT=res_path)
+                   MIPIPE_BENCH_RESULT=res_path, MIPIPE_BENCH_MODE=p2p)
+        if p2p.endswith("-safe"):
+            env.update(MIPIPE_COLL_OVERLAP="0", MIPIPE_PP_LANES="0")
         env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # fresh rendezvous store per child
         cmd = [sys.executable, os.path.abspath(__file__)] + child_argv + ["--graphs", str(graphs)]
         t0 = time.monotonic()
@@ -476,8 +482,10 @@ def run(a) -> None:
             torch.cuda.synchronize()
 
     step_no = 0
-    for _ in range(a.warmup):
-        with wd.step(init_to):
+    for w in range(a.warmup):
+        # the first step records the native tape; later warmups replay it (a hang there is
+        # caught in 90 s, not the init limit)
+        with wd.step(init_to if w == 0 else min(init_to, max(step_to, 90.0))):
             maybe_stall(rank, step_no, attempt)
             trainer.train_step(tokens, targets)
             step_no += 1
@@ -576,6 +584,7 @@ def run(a) -> None:
         "model_tflops_per_gpu": round(flops / world / 1e12, 1),
         "hbm_peak_gb_per_gpu": hbm_peak,   # max over ranks of the caching allocator's peak
         "attempt": attempt,
+        "attempt_mode": os.environ.get("MIPIPE_BENCH_MODE", "in-process"),
         "config": {"model": a.model, "params": cfg.n_params(), "global_batch": gb, "seq_len": a.seq,
                    "micro_batch": a.mbs, "microbatches": m, "schedule": trainer.schedule, "v": trainer.v,
                    "parallelism": f"pp{pp}" + (f"_dp{dp}" if dp > 1 else ""),
