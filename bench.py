@@ -560,8 +560,8 @@ def run(a) -> None:
             dist.all_reduce(pb, op=dist.ReduceOp.SUM)
         p2p_bytes = int(pb.item())
         eng = getattr(rt.p2p, "engine", None)
-        rccl_ranks = {"pp": int(eng.nranks()) if eng is not None else None,
-                      "dp": int(trainer.coll.dp_engine.nranks()) if getattr(trainer.coll, "dp_engine", None)
+        rccl_ranks = {"pp": int(eng.nranks) if eng is not None else None,
+                      "dp": int(trainer.coll.dp_engine.nranks) if getattr(trainer.coll, "dp_engine", None)
                       is not None else None}
     out = {
         "metric": METRIC,

@@ -14,6 +14,8 @@ void register_rccl(py::module& m) {
       .def("post", &RcclEngine::post, py::arg("channel"), py::arg("sends"), py::arg("recvs"))
       .def("coll", &RcclEngine::coll, py::arg("channel"), py::arg("op"), py::arg("send"), py::arg("recv"))
       .def("wait", &RcclEngine::wait)
+      .def("wait_keep", &RcclEngine::wait_keep)
+      .def("release", &RcclEngine::release)
       .def("query", &RcclEngine::query)
       .def("synchronize", &RcclEngine::synchronize)
       .def("close", &RcclEngine::close)

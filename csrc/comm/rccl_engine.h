@@ -320,6 +320,23 @@ class RcclEngine {
   // make the current stream wait for a posted group (idempotent)
   void wait(int64_t h) { wait_raw(h, c10::hip::getCurrentHIPStream(device_).stream()); }
 
+  // non-consuming wait: every stream that reads a group's receives waits on its completion
+  // event (microbatch lanes: one grouped post may feed computes on two streams); the
+  // handle stays valid until `release`
+  void wait_keep_raw(int64_t h, hipStream_t compute) {
+    auto it = pending_.find(h);
+    if (it == pending_.end()) return;
+    MP_HIP(hipStreamWaitEvent(compute, it->second, 0));
+  }
+  void wait_keep(int64_t h) { wait_keep_raw(h, c10::hip::getCurrentHIPStream(device_).stream()); }
+  // return a handle's event to the pool (after its last wait_keep)
+  void release(int64_t h) {
+    auto it = pending_.find(h);
+    if (it == pending_.end()) return;
+    pool_.push_back(it->second);
+    pending_.erase(it);
+  }
+
   // host-side completion test (pre-flight ping polls it against a deadline)
   bool query(int64_t h) {
     auto it = pending_.find(h);

@@ -158,6 +158,7 @@ class StageRunner {
     hipStream_t st = c10::hip::getCurrentHIPStream(device_).stream();
     std::vector<int64_t> handles(nslots_, -1);
     std::vector<RcclEngine*> engines(nslots_, nullptr);
+    std::vector<char> waited(nslots_, 0);
     const bool prof = profile_;
     if (prof) prepare_events();
     while ((int64_t)sync_ev_.size() < nsync_) {
@@ -197,9 +198,10 @@ class StageRunner {
           engines[i.slot] = i.engine;
           break;
         case WAIT:
+          // non-consuming: a group feeding computes on two lanes is waited on by both
           TORCH_CHECK(handles[i.slot] >= 0, "stage runner: WAIT before its POST (slot ", i.slot, ")");
-          engines[i.slot]->wait_raw(handles[i.slot], on(i.stream));
-          handles[i.slot] = -2;  // consumed
+          engines[i.slot]->wait_keep_raw(handles[i.slot], on(i.stream));
+          waited[i.slot] = 1;
           break;
         case CALL: {
           py::gil_scoped_acquire gil;
@@ -208,9 +210,13 @@ class StageRunner {
         }
       }
     }
-    // groups whose completion nobody consumed (sends): order them before the next step
-    for (int64_t s = 0; s < nslots_; ++s)
-      if (handles[s] >= 0) engines[s]->wait_raw(handles[s], st);
+    // groups whose completion nobody waited for (sends): order them before the next step;
+    // then every handle's event goes back to its engine's pool
+    for (int64_t s = 0; s < nslots_; ++s) {
+      if (handles[s] < 0) continue;
+      if (!waited[s]) engines[s]->wait_keep_raw(handles[s], st);
+      engines[s]->release(handles[s]);
+    }
     if (prof) {
       MP_HIPCHK(hipEventRecord(ev_[1], st));
       profiled_ = true;

@@ -58,18 +58,31 @@ class _StagedSend:
 
 class _NativeWork:
     """Handle of one grouped transfer on the native RCCL engine; ``wait`` makes the
-    current stream wait (no host block), like torch's NCCL Work.  Under a recording step
-    (:mod:`.native_runner`) the wait is also put on the tape."""
+    current stream wait (no host block), like torch's NCCL Work -- once per stream: a
+    group whose receives feed computes on two microbatch lanes is waited on by both
+    streams (a non-consuming engine wait; ``release`` returns the event at the step end).
+    Under a recording step (:mod:`.native_runner`) each such wait is also put on the tape
+    with its stream."""
 
     def __init__(self, engine, handle: int, rec=None, slot: int = -1):
         self.engine, self.handle, self.rec, self.slot = engine, handle, rec, slot
+        self.streams = set()
+        self.released = False
 
     def wait(self):
-        self.engine.wait(self.handle)
+        sid = int(torch.cuda.current_stream().cuda_stream) if torch.cuda.is_available() else 0
+        if sid in self.streams:
+            return True
+        self.streams.add(sid)
+        self.engine.wait_keep(self.handle)
         if self.rec is not None:
             self.rec.native_wait(self.slot)
-            self.rec = None     # one WAIT per handle, however often it is waited on
         return True
+
+    def release(self):
+        if not self.released:
+            self.released = True
+            self.engine.release(self.handle)
 
 
 def load_native_rccl(ext) -> None:
@@ -184,6 +197,7 @@ class P2P:
         self.engine = None
         self.channels = 1
         self.fallback_reason = ""
+        self._live: List = []       # native works of the current step (release_works)
         capable = (device.type == "cuda" and dist.is_initialized() and not self.host_staged and len(self.ranks) > 1)
         if mode != "torch" and capable:
             timeout = preflight_timeout if preflight_timeout is not None else \
@@ -217,6 +231,13 @@ class P2P:
             return "none"
         return "gloo-staged" if self.host_staged else "torch"
 
+    def release_works(self) -> None:
+        """End of a step: the native groups' completion events go back to the engine pool
+        (their waits are stream-ordered, so releasing after the last one is issued is safe)."""
+        for w in self._live:
+            w.release()
+        self._live.clear()
+
     def use_single_channel(self) -> None:
         """Post both directions on channel 0 (the lowered program's two-channel order was
         not proven deadlock-free, see simulate.check_lowered)."""
@@ -245,6 +266,7 @@ class P2P:
                 h = self.engine.post(ch, s_, r_)
                 slot = rec.native_post(self.engine, ch, s_, r_) if rec is not None else -1
                 w = _NativeWork(self.engine, h, rec, slot)
+                self._live.append(w)
                 for i in range(len(sends)):
                     if sc[i] == ch:
                         works_s[i] = w

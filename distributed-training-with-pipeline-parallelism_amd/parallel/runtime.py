@@ -810,6 +810,8 @@ class PipelineRuntime:
                 w.wait()
         for w in reduce_works:
             w.wait()
+        if hasattr(self.p2p, "release_works"):
+            self.p2p.release_works()
         for st in self.stages.values():
             st.post_step()
         if self.profile:

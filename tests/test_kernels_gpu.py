@@ -596,6 +596,21 @@ def test_native_rccl_engine_self_transfer():
     assert torch.equal(g, ref) and torch.equal(out, ref) and float(mx) == 3.0
     assert torch.equal(rs, rs_ref) and torch.equal(rs16_out, rs16)
     assert eng.query(h) and eng.query(h2)
+    # non-consuming waits (microbatch lanes): two streams wait on one group, then release
+    src3 = torch.randn(1 << 16, device=DEV)
+    dst3 = torch.empty_like(src3)
+    h8 = eng.post(0, [(src3, 0)], [(dst3, 0)])
+    side = torch.cuda.Stream()
+    eng.wait_keep(h8)
+    with torch.cuda.stream(side):
+        eng.wait_keep(h8)
+        out_side = dst3 * 2.0
+    torch.cuda.current_stream().wait_stream(side)
+    out_main = dst3 * 3.0
+    eng.release(h8)
+    eng.release(h8)     # idempotent
+    torch.cuda.synchronize()
+    assert torch.equal(out_side, src3 * 2.0) and torch.equal(out_main, src3 * 3.0)
     assert eng.async_error() == ""
     eng.close()
     # a second engine (e.g. the DP group's, one channel on the collective slot) reuses the

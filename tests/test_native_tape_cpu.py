@@ -182,6 +182,12 @@ class FakeEngine:
         for w in self.pending.pop(h, []):
             w.wait()
 
+    def wait_keep(self, h):     # host-side stand-in: completes the group (idempotent)
+        self.wait(h)
+
+    def release(self, h):
+        self.pending.pop(h, None)
+
     def query(self, h):
         return True
 
@@ -250,8 +256,8 @@ class FakeRunner:
                 eng, ch, op, snd, rcv, slot = x
                 handles[slot] = (eng, eng.coll(ch, op, snd, rcv))
             elif k == WAIT:
-                eng, h = handles.pop(x)
-                eng.wait(h)
+                eng, h = handles[x]
+                eng.wait_keep(h)
             else:
                 x()
         for eng, h in handles.values():

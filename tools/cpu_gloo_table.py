@@ -89,37 +89,54 @@ def main():
     ap.add_argument("--layers", default="4,8,12")
     ap.add_argument("--heads", default="4,8,12")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=1, help="repetitions per (config, engine), interleaved; md = median")
+    ap.add_argument("--append", default=None, help="earlier rows (JSON) to merge in as repetitions")
     a = ap.parse_args()
     from mipipe.bench import compat
     engines = [e for e in a.engines.split(",") if e and (e != "reference" or os.path.exists(REF))]
     rows = []
+    if a.append:
+        with open(os.path.join(ROOT, a.append)) as f:
+            rows = [dict(r, rep=r.get("rep", 0)) for r in json.load(f)]
+    rep0 = 1 + max((r["rep"] for r in rows), default=-1)
     path_json = os.path.join(ROOT, a.out + ".json")
     for L in [int(x) for x in a.layers.split(",")]:
         for H in [int(x) for x in a.heads.split(",")]:
             for P in [int(x) for x in a.procs.split(",")]:
-                for sched in SCHEDS:
-                    for eng in engines:
-                        t0 = time.time()
-                        if eng == "reference":
-                            m = run_reference(L, H, P, sched, iters=a.iters)
-                        else:
-                            m = compat.run_one_experiment(L, H, P, sched, batch_size=32, seq_length=128,
-                                                          num_iterations=a.iters, device="cpu", engine=eng,
-                                                          timeout=900)
-                        row = dict(n_layers=L, n_heads=H, num_processes=P, schedule=sched, engine=eng,
-                                   wall_s=round(time.time() - t0, 1), published=PUB.get((L, H, P, sched)))
-                        row.update({k: v for k, v in m.items() if isinstance(v, (int, float, str, bool)) or v is None})
-                        rows.append(row)
-                        print(json.dumps(row), flush=True)
-                        with open(path_json, "w") as f:
-                            json.dump(rows, f, indent=1)
+                for rep in range(rep0, rep0 + a.reps):
+                    for sched in SCHEDS:
+                        for eng in engines:
+                            t0 = time.time()
+                            if eng == "reference":
+                                m = run_reference(L, H, P, sched, iters=a.iters)
+                            else:
+                                m = compat.run_one_experiment(L, H, P, sched, batch_size=32, seq_length=128,
+                                                              num_iterations=a.iters, device="cpu", engine=eng,
+                                                              timeout=900)
+                            row = dict(n_layers=L, n_heads=H, num_processes=P, schedule=sched, engine=eng, rep=rep,
+                                       wall_s=round(time.time() - t0, 1), published=PUB.get((L, H, P, sched)))
+                            row.update({k: v for k, v in m.items()
+                                        if isinstance(v, (int, float, str, bool)) or v is None})
+                            rows.append(row)
+                            print(json.dumps(row), flush=True)
+                            with open(path_json, "w") as f:
+                                json.dump(rows, f, indent=1)
     write_md(rows, os.path.join(ROOT, a.out + ".md"), engines)
 
 
 def write_md(rows, path, engines):
-    by = {(r["n_layers"], r["n_heads"], r["num_processes"], r["schedule"], r["engine"]): r for r in rows}
+    import statistics
+    grp = {}
+    for r in rows:
+        if r.get("throughput"):
+            grp.setdefault((r["n_layers"], r["n_heads"], r["num_processes"], r["schedule"], r["engine"]),
+                           []).append(r["throughput"])
+    # median over repetitions
+    by = {k: {"throughput": statistics.median(v), "n": len(v)} for k, v in grp.items()}
+    nrep = max((v["n"] for v in by.values()), default=1)
     lines = ["# CPU/gloo, the reference's configs (batch 32 x 128, m = 4, 5 timed steps), this container's 8 CPUs",
-             "", "tok/s per engine; speedup = tok/s / GPipe tok/s of the same engine and (L, H, P); "
+             "", f"tok/s per engine (median of up to {nrep} interleaved repetitions); "
+             "speedup = tok/s / GPipe tok/s of the same engine and (L, H, P); "
              "`pub` = the notebook's published speedup (nb:802-837, 10-core CPU).", ""]
     hdr = "| L | H | P | schedule | " + " | ".join(f"{e} tok/s | {e} speedup" for e in engines) + " | pub tok/s | pub speedup |"
     lines += [hdr, "|" + "---|" * (hdr.count("|") - 1)]
