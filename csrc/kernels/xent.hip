@@ -8,6 +8,8 @@
 // Columns >= V (vocab padded to a multiple of 64 for the GEMMs, e.g. GPT-2's 50257
 // -> 50304) are excluded from the softmax and get zero gradient.  Targets equal to
 // ignore_index produce zero loss and zero gradient.
+#include <cstdlib>
+
 #include "mp_common.h"
 
 using namespace mp;
@@ -83,8 +85,9 @@ __device__ __forceinline__ void keep_packed(u16x8 (&v)[CPT]) {
   }
 }
 
-template <int CPT, bool WRITE_GRAD, int NTH = 512>
-__global__ void __launch_bounds__(NTH) xent_reg_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ target,
+// MINB: blocks per CU to fit (waves per SIMD = MINB x NTH / 256)
+template <int CPT, bool WRITE_GRAD, int NTH = 512, int MINB = 1>
+__global__ void __launch_bounds__(NTH) __attribute__((amdgpu_waves_per_eu(MINB * NTH / 256, 8))) xent_reg_kernel(bf16_t* __restrict__ logits, const int64_t* __restrict__ target,
                                                        float* __restrict__ loss, int T, int V, int Vp,
                                                        float grad_scale, int64_t ignore_index) {
   __shared__ float red[16];
@@ -174,6 +177,31 @@ extern "C" int mp_xent_fwd_bwd(void* logits, const int64_t* target, float* loss,
     return (int)hipGetLastError();
   }
   const int nchunk = Vp / 8;
+  // MIPIPE_XENT=occ3 | t1024: occupancy variants of the register-resident kernel (A/B)
+  static const int variant = [] {
+    const char* e = getenv("MIPIPE_XENT");
+    if (e && e[0] == 'o') return 1;
+    if (e && e[0] == 't') return 2;
+    return 0;
+  }();
+  if (variant == 1 && nchunk <= 512 * 13) {   // 3 blocks of 512 threads per CU
+    if (write_grad)
+      xent_reg_kernel<13, true, 512, 3><<<T, 512, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,
+                                                           ignore_index);
+    else
+      xent_reg_kernel<13, false, 512, 3><<<T, 512, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,
+                                                            ignore_index);
+    return (int)hipGetLastError();
+  }
+  if (variant == 2 && nchunk <= 1024 * 7) {   // 1024 threads, 7 chunks each
+    if (write_grad)
+      xent_reg_kernel<7, true, 1024, 2><<<T, 1024, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,
+                                                         ignore_index);
+    else
+      xent_reg_kernel<7, false, 1024, 2><<<T, 1024, 0, st>>>((bf16_t*)logits, target, loss, T, V, Vp, grad_scale,
+                                                          ignore_index);
+    return (int)hipGetLastError();
+  }
 #define MP_XR(CPT)                                                                                               \
   if (nchunk <= 512 * CPT) {                                                                                     \
     if (write_grad)                                                                                              \

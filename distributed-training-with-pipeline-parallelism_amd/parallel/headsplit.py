@@ -89,7 +89,7 @@ def insert_head_ops(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: i
     compute orders by list scheduling: whenever a rank is free it runs whichever is
     startable first -- its next scheduled action or its next head chunk (ties go to
     the head chunk, which the last stage is waiting for)."""
-    costs = dict(DEFAULT_COSTS, **(costs or {}))
+    costs = {**DEFAULT_COSTS, **(costs or {})}
     S = pp * v
     s2r = [stage_to_rank(s, pp, style) for s in range(S)]
     base = {r: [a for a in orders.get(r, []) if a is not None and a.op.is_compute] for r in range(pp)}

@@ -98,7 +98,7 @@ def simulate(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: int = 1,
              head_costs: Optional[Dict[int, float]] = None) -> SimResult:
     """Time a per-rank compute order.  ``stage_costs`` scales each stage's op costs
     (non-uniform partitions); ``head_costs[r]`` is the cost of rank r's head chunk."""
-    costs = dict(DEFAULT_COSTS, **(costs or {}))
+    costs = {**DEFAULT_COSTS, **(costs or {})}
     S = pp * v
     split = uses_split_backward(orders)
     head = head_ranks_of(orders)
