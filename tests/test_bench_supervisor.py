@@ -157,3 +157,30 @@ def test_extra_phases_never_push_past_the_deadline():
             if kind == "ref":
                 ref_wall = b * 1.25 + 5
         assert t <= 560.0, (head_wall, t)
+
+
+def test_merge_results_reference_block_and_speedups():
+    """bench.merge_results: the headline line + every schedule (the headline's own included)
+    with speedup vs GPipe, and the reference fp32 block next to the published row of the
+    same (schedule, P) -- P = 2's row at N = 1, where the reference published none."""
+    sys.path.insert(0, ROOT)
+    import argparse
+    import bench
+    head = {"value": 100.0, "n_gpus": 1, "ms_per_step": 10.0, "bubble_fraction": 0.0, "analytic_bubble": 0.0,
+            "config": {"schedule": "1F1B", "v": 1, "microbatches": 2}}
+    res = {"x_GPipe": {"value": 80.0, "config": {"schedule": "GPipe", "v": 1}},
+           "x_Interleaved1F1B": {"error": "child exited rc=17 without a result after 50s"},
+           "r_GPipe": {"tok_s": 167132.0, "P": 1}, "r_1F1B": {"tok_s": 184000.0, "P": 1},
+           "r_Interleaved1F1B": {"skipped": "time"}}
+    a = argparse.Namespace(ref_args="8,8,32,128")
+    out = bench.merge_results(head, res, a)
+    s = out["schedules"]
+    assert s["1F1B"]["tok_s"] == 100.0 and s["GPipe"]["speedup_vs_gpipe"] == 1.0
+    assert s["1F1B"]["speedup_vs_gpipe"] == 1.25 and "error" in s["Interleaved1F1B"]
+    r = out["reference_fp32"]
+    assert r["per_schedule"]["1F1B"]["nb_row"]["tok_s"] == 1649.53 and r["per_schedule"]["1F1B"]["nb_row"]["P"] == 2
+    assert r["per_schedule"]["GPipe"]["x_vs_nb"] == 100.0 and r["tok_s"] == 184000.0
+    assert "skipped" in r["per_schedule"]["Interleaved1F1B"]
+    # a shrunken reference config gets no published row to compare with
+    out2 = bench.merge_results(head, res, argparse.Namespace(ref_args="2,2,8,16"))
+    assert "nb_row" not in out2["reference_fp32"]["per_schedule"]["1F1B"]
