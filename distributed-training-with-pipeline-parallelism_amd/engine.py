@@ -200,7 +200,7 @@ def auto_lanes(cfg: NativeConfig, pp: int, v: int, graphs: bool, device, m: int,
     stream's hardware queue: fixed by the queue probe, parallel/runtime.py), 594K with 4;
     GPT-2 small (16K-token microbatches, m = 2) 850K -> 888K with 2."""
     device = torch.device(device)
-    if not (v == 1 and graphs and device.type == "cuda" and m >= 2):
+    if not (graphs and device.type == "cuda" and m >= 2):
         return 1
     if pp > 1 and os.environ.get("MIPIPE_PP_LANES", "1") == "0":
         return 1

@@ -186,6 +186,7 @@ class PipelineRuntime:
         self.lanes = 1
         self.lane_streams: List[Optional[torch.cuda.Stream]] = [None]
         self._joined = True
+        self._merged: set = set()
         self._in_bufs: Dict[int, Tuple[torch.Tensor, ...]] = {}
         self._tgt_bufs: Dict[int, torch.Tensor] = {}
         self._loss_bufs: Dict[tuple, torch.Tensor] = {}
@@ -272,7 +273,9 @@ class PipelineRuntime:
         the join; the dW side stream is turned off (a forked graph did not overlap with the
         other lane).
 
-        PP > 1 (one stage per rank): in the 1F1B steady state F(i+w) and B(i) are both ready;
+        Several stages per rank (interleaved): each stage's lanes are merged at its own
+        REDUCE_GRAD, after which the lanes wait for the merge before running the other
+        stages' remaining backwards.  PP > 1: in the 1F1B steady state F(i+w) and B(i) are both ready;
         on two lanes they overlap (a 32-sequence GPT-2 microbatch on one stream runs at 0.95x
         of two concurrent ones, profiles/r3_lane1_mbs_ab.txt).  A receive is waited for on
         the lane of the compute it feeds; a post carrying a lane's output is ordered after
@@ -281,7 +284,7 @@ class PipelineRuntime:
         compute stream and, at PP > 1, every comm stream (the probe) -- or lanes stay off.
         Returns the lanes in use."""
         n = max(1, int(n))
-        if n > 1 and (len(self.stages) != 1 or self.device.type != "cuda" or self.m < 2):
+        if n > 1 and (self.device.type != "cuda" or self.m < 2):
             n = 1
         self.lane_streams = [None]
         idx = (self.device.index if self.device.index is not None else torch.cuda.current_device()) if n > 1 else 0
@@ -405,6 +408,10 @@ class PipelineRuntime:
             self.head.graphs.run(("M", 0), (), lambda ins: ha.merge_lanes())
         else:
             ha.merge_lanes()
+        for ls in self.lane_streams[1:]:     # later lane work must not race the merge's zeroing
+            ls.wait_stream(main)
+            if rec is not None:
+                rec.sync(ls, main)
 
     def _fork_lanes(self, rec) -> None:
         if self.lanes == 1:
@@ -415,9 +422,14 @@ class PipelineRuntime:
             if rec is not None:
                 rec.sync(ls, main)
         self._joined = False
+        self._merged = set()
 
-    def _join_lanes(self, rec) -> None:
-        """Compute stream waits for every lane; lane gradients summed into lane 0."""
+    def _join_lanes(self, rec, stage: Optional[int] = None) -> None:
+        """Compute stream waits for every lane; lane gradients summed into lane 0 -- of
+        ``stage`` only (its REDUCE_GRAD: with several stages per rank the others still run
+        backwards on the lanes, which then wait for the merge, as it zeroes their buffers),
+        or of every stage not merged yet (the end of the step).  Each stage is merged once
+        per step (the fused merge also leaves its clipping sum of squares)."""
         if self.lanes == 1 or self._joined:
             return
         main = torch.cuda.current_stream(self.device)
@@ -425,12 +437,23 @@ class PipelineRuntime:
             main.wait_stream(ls)
             if rec is not None:
                 rec.sync(main, ls)
-        for st in self.stages.values():
+        todo = [stage] if stage is not None else list(self.stages)
+        for s in todo:
+            if s in self._merged:
+                continue
+            self._merged.add(s)
+            st = self.stages[s]
             if getattr(st, "_graphed", lambda: False)():
                 st.graphs.run(("M", 0), (), lambda ins, st=st: st.arena.merge_lanes())
             else:
                 st.arena.merge_lanes()
-        self._joined = True
+        if len(self._merged) == len(self.stages):
+            self._joined = True
+        elif stage is not None:
+            for ls in self.lane_streams[1:]:
+                ls.wait_stream(main)
+                if rec is not None:
+                    rec.sync(ls, main)
 
     # ------------------------------------------------------------------ init
     def _needs_inference(self) -> bool:
@@ -775,7 +798,7 @@ class PipelineRuntime:
                     continue
                 st = self.stages.get(a.stage)
                 if a.op == Op.REDUCE_GRAD:
-                    self._join_lanes(rec)
+                    self._join_lanes(rec, a.stage)
                     if rec is not None and not st.has_grad_reduction(self.scale_grads):
                         continue    # nothing to issue (no DP, scale folded into the loss)
                     if rec is not None and not getattr(st, "records_own_collectives", False):

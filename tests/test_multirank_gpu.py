@@ -70,6 +70,8 @@ def test_multirank_gpu_interleaved_matches_single(reference8, n, graphs, split):
                "--split-head", str(split), port=29860 + n + 10 * graphs + 20 * split)
     assert res["losses"] == pytest.approx(reference8, rel=2e-3)
     assert res["native_runner"] == bool(graphs), res["native_reason"]
+    if graphs:   # two lanes with two stages per rank: each stage merged at its own REDUCE_GRAD
+        assert res["lanes"] == 2, res
 
 
 @pytest.mark.parametrize("n,schedule,graphs,split,dp", [(2, "1F1B", 1, 1, 1), (4, "1F1B", 1, 1, 1),
