@@ -110,12 +110,18 @@ def analyse(recs, P):
     orders = {int(r): [Action.parse(a) for a in acts] for r, acts in recs[0]["orders"].items()}
     dur = {}
     busy = []
+    import re
+    lab = re.compile(r"^(\d+)(FL|F|B|I|W|H|M|C16)(\d+)$")   # native-tape graph labels (graphs.py)
     for rec in recs:
         b = 0.0
         for label, s, e in rec["timeline"]:
-            a = Action.parse(label)
-            dur.setdefault((a.stage, a.op.value), []).append(e - s)
             b += e - s
+            mt = lab.match(label)
+            if mt is None:
+                continue
+            op = "F" if mt.group(2) == "FL" else mt.group(2)
+            if op in ("F", "B"):
+                dur.setdefault((int(mt.group(1)), op), []).append(e - s)
         busy.append(b)
     S = P * v
     # per-stage F and B costs (ms); the simulator takes op costs x per-stage scale: F = 1 x
