@@ -90,7 +90,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--model", default="gpt2-small")
-    ap.add_argument("--schedule", default="1F1B", help="the headline schedule (``value``)")
+    ap.add_argument("--schedule", default="auto",
+                    help="the headline schedule (``value``); auto: the best planned of GPipe / 1F1B / "
+                         "Interleaved1F1B (engine.pick_schedule; 1F1B at one GPU)")
     ap.add_argument("--schedules", default="all",
                     help="schedules also measured after the headline, each in a fresh child process group: "
                          "'all' (GPipe,1F1B,Interleaved1F1B), 'none', or a comma list")
@@ -141,7 +143,7 @@ def _canon(name: str) -> str:
     """Schedule name -> canonical (the supervisor imports nothing that could touch HIP)."""
     key = name.replace("_", "").replace("-", "").lower()
     table = {"gpipe": "GPipe", "1f1b": "1F1B", "interleaved": "Interleaved1F1B", "interleaved1f1b": "Interleaved1F1B",
-             "zbh1": "ZBH1", "zbv": "ZBV", "loopedbfs": "LoopedBFS"}
+             "zbh1": "ZBH1", "zbv": "ZBV", "loopedbfs": "LoopedBFS", "auto": "auto"}
     if key not in table:
         raise SystemExit(f"unknown schedule {name!r}")
     return table[key]
@@ -212,10 +214,9 @@ def plan_phases(a, argv) -> list:
     headline's attempts first, then every other schedule of ``--schedules`` on the same
     model/config, then the reference's fp32 config per schedule."""
     tags = [(f"h{k}", "headline", list(argv), a.schedule) for k in range(max(1, a.max_attempts))]
-    head = _canon(a.schedule)
+    # every schedule gets a slot; the one the headline ran (known once it is in) is skipped
     for s in extra_schedules(a):
-        if s != head:
-            tags.append((f"x_{s}", "sched", list(argv) + ["--schedule", s], s))
+        tags.append((f"x_{s}", "sched", list(argv) + ["--schedule", s], s))
     if ref_fp32_on(a):
         for s in SCHEDULES:
             tags.append((f"r_{s}", "ref", list(argv) + ["--phase", "ref", "--schedule", s], s))
@@ -306,6 +307,8 @@ def supervise(a, argv) -> int:
                 b = attempt_budget(deadline - left(), deadline, cap)
                 if headline is None and k < len(attempts) and b > 0:
                     decision = f"go {b:.0f} {attempts[k][0]} {attempts[k][1]} {k}"
+            elif headline is not None and kind == "sched" and sched == headline["config"]["schedule"]:
+                pass        # the headline's own schedule: already measured
             elif headline is not None:
                 b, est = extra_budget(kind, left(), cap, head_wall, ref_wall)
                 if b > 0:
@@ -458,6 +461,11 @@ def run(a) -> None:
         m = a.microbatches if a.microbatches is not None else m_default
         kw = {"vocab_size": a.vocab} if a.vocab else {}
         cfg = NativeConfig.by_name(a.model, **kw)
+        planned = {}
+        was_auto = _canon(a.schedule) == "auto"
+        if was_auto:
+            from mipipe.engine import pick_schedule
+            a.schedule, planned = pick_schedule(cfg, pp, m, a.mbs, a.seq)
         gpu = device.type == "cuda"
         if a.graphs is None:
             a.graphs = 1 if gpu else 0
@@ -608,7 +616,9 @@ def run(a) -> None:
                    else "last stage",
                    "head_lag": getattr(trainer, "head_lag", None),
                    "planned_efficiency": None if getattr(trainer, "planned_makespan", None) is None else
-                   round(trainer.planned_ideal / trainer.planned_makespan, 3)},
+                   round(trainer.planned_ideal / trainer.planned_makespan, 3),
+                   "schedule_choice": ({"auto": {k: round(v_, 3) for k, v_ in planned.items()}} if planned
+                                       else ("auto (one GPU: 1F1B)" if was_auto else "given"))},
     }
     if loss_val is not None:
         out["last_loss"] = round(loss_val, 4)

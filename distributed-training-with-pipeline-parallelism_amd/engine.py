@@ -16,7 +16,7 @@ from __future__ import annotations
 
 import math
 import os
-from typing import List, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -190,6 +190,59 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
                 head_optimizer_bytes=head_opt)
 
 
+def plan_head_pipeline(cfg: NativeConfig, pp: int, schedule: str, m: int, mbs: int, seq_len: int,
+                       v: Optional[int] = None, style: str = "loop", layer_ranges=None,
+                       head_align: Optional[int] = None) -> dict:
+    """The distributed-head pipeline plan of one schedule (what PipelineTrainer runs at
+    PP > 1): layer split, per-stage costs (stage_cost_model units), water-filled head token
+    chunks, and the head-aware compute orders with their simulated makespan
+    (headsplit.plan_head_schedule).  ``ideal`` is the no-bubble time in the same units, so
+    ideal / makespan is the planned pipeline efficiency."""
+    schedule = canonical_name(schedule)
+    style = REQUIRED_STYLE.get(schedule, style)
+    if v is None:
+        v = SCHEDULES[schedule][1]
+    if not SCHEDULES[schedule][2]:
+        v = 1
+    S = pp * v
+    if layer_ranges is None:
+        layer_ranges = balanced_layer_ranges(cfg, S, seq_len, head_on_last=False)
+    lc, head_units, ec = stage_cost_model(cfg, seq_len)
+    stage_costs = [(r1 - r0) * lc + (ec if s == 0 else 0.0) + (0.1 if s == S - 1 else 0.0)
+                   for s, (r0, r1) in enumerate(layer_ranges)]
+    rank_load = [sum(stage_costs[s] for s in range(S) if stage_to_rank(s, pp, style) == r) for r in range(pp)]
+    T = mbs * seq_len
+    align = head_align or next(a for a in (256, 128, 64, 32, 16, 8, 1) if T % a == 0)
+    chunks = head_token_split(T, rank_load, head_units, align=align)
+    head_costs = {r: 3.0 * head_units * chunks[r] / T for r in range(pp) if chunks[r] > 0}
+    base = generate(schedule, pp, m, v, style)
+    regen = ((lambda lag: generate(schedule, pp, m, v, style, warmup_extra=lag)) if schedule in WARMUP_EXTRA
+             else None)
+    orders, lag, makespan = plan_head_schedule(base, pp, v, style, head_costs, stage_costs, regen=regen)
+    # no-bubble time in the same units (F = 1, B = 2 per stage-cost unit)
+    ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * m / pp
+    return dict(schedule=schedule, v=v, style=style, layer_ranges=layer_ranges, stage_costs=stage_costs,
+                chunks=chunks, head_costs=head_costs, orders=orders, lag=lag, makespan=makespan, ideal=ideal,
+                efficiency=ideal / makespan if makespan > 0 else 0.0)
+
+
+def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
+                  candidates=("GPipe", "1F1B", "Interleaved1F1B")) -> Tuple[str, Dict[str, float]]:
+    """``schedule="auto"``: the candidate with the highest planned efficiency of the
+    head-aware plan (1F1B at PP = 1, where every schedule is bubble-free and 1F1B keeps one
+    stage per rank).  Returns (name, {name: planned efficiency})."""
+    if pp == 1:
+        return "1F1B", {}
+    eff = {}
+    for c in candidates:
+        try:
+            eff[c] = plan_head_pipeline(cfg, pp, c, m, mbs, seq_len)["efficiency"]
+        except (ValueError, RuntimeError):
+            continue
+    best = max(eff, key=lambda k: (eff[k], k == "1F1B"))
+    return best, eff
+
+
 def auto_lanes(cfg: NativeConfig, pp: int, v: int, graphs: bool, device, m: int, tokens: int, params: int,
                layers: int, recompute: bool = False) -> int:
     """Microbatch lanes (PipelineRuntime.set_lanes) at PP = 1 with HIP graphs: up to 4 for
@@ -257,23 +310,11 @@ class PipelineTrainer:
         self.head_zero = self.split_head and os.environ.get("MIPIPE_HEAD_ZERO", "1") != "0"
         if self.split_head:
             self.head = HeadShard(cfg, self.device, seed=seed, dtype=dtype, shards=pp if self.head_zero else 1)
-            lc, head_units, ec = stage_cost_model(cfg, seq_len)
-            stage_costs = [(r1 - r0) * lc + (ec if s == 0 else 0.0) + (0.1 if s == num_stages - 1 else 0.0)
-                           for s, (r0, r1) in enumerate(layer_ranges)]
-            rank_load = [sum(stage_costs[s] for s in range(num_stages) if stage_to_rank(s, pp, style) == r)
-                         for r in range(pp)]
-            T = mbs * seq_len
-            align = head_align or next(a for a in (256, 128, 64, 32, 16, 8, 1) if T % a == 0)
-            chunks = head_token_split(T, rank_load, head_units, align=align)
-            head_costs = {r: 3.0 * head_units * chunks[r] / T for r in range(pp) if chunks[r] > 0}
-            base = generate(self.schedule, pp, n_microbatches, v, style)
-            sched = self.schedule
-            regen = ((lambda lag: generate(sched, pp, n_microbatches, v, style, warmup_extra=lag))
-                     if sched in WARMUP_EXTRA else None)
-            orders, self.head_lag, self.planned_makespan = plan_head_schedule(base, pp, v, style, head_costs,
-                                                                              stage_costs, regen=regen)
-            # no-bubble time in the same units (F = 1, B = 2 per stage-cost unit)
-            self.planned_ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * n_microbatches / pp
+            plan = plan_head_pipeline(cfg, pp, self.schedule, n_microbatches, mbs, seq_len, v, style, layer_ranges,
+                                      head_align)
+            orders, self.head_lag, self.planned_makespan = plan["orders"], plan["lag"], plan["makespan"]
+            stage_costs, head_costs, chunks = plan["stage_costs"], plan["head_costs"], plan["chunks"]
+            self.planned_ideal = plan["ideal"]
             head_plan = HeadPlan(chunks, cfg.d_model, runner=self.head.run, dtype=dtype)
             head_plan.arena = self.head.arena   # per-lane head gradients (PipelineRuntime.set_lanes)
             if graphs and self.device.type == "cuda":

@@ -89,7 +89,7 @@ def test_bench_eight_ranks_gpt2_small_layout():
     out = json.loads(lines[0])
     c = out["config"]
     assert out["n_gpus"] == 8 and out["value"] > 0 and c["parallelism"] == "pp8" and c["microbatches"] == 32
-    assert c["model"] == "gpt2-small" and len(c["layer_split"]) == 8
+    assert c["model"] == "gpt2-small" and len(c["layer_split"]) == 8 * c["v"]
     assert sum(b - a for a, b in c["layer_split"]) == 12
     assert c["head"].startswith("distributed") and out["bubble_fraction"] is not None
 
@@ -134,7 +134,10 @@ def test_bench_four_ranks_measures_all_three_schedules():
     assert sch["Interleaved1F1B"]["v"] == 2 and sch["GPipe"]["v"] == 1
     assert sch["Interleaved1F1B"]["analytic_bubble"] < sch["1F1B"]["analytic_bubble"]
     assert sch["GPipe"]["speedup_vs_gpipe"] == 1.0
-    assert out["value"] == sch["1F1B"]["tok_s"] and out["config"]["schedule"] == "1F1B"
+    # --schedule auto: the headline is the best-planned schedule, and it is measured once
+    head = out["config"]["schedule"]
+    assert out["value"] == sch[head]["tok_s"] and set(out["config"]["schedule_choice"]["auto"]) == set(sch)
+    assert out["config"]["schedule_choice"]["auto"][head] == max(out["config"]["schedule_choice"]["auto"].values())
     assert out["p2p_bytes_per_step"] > 0 and "rccl_ranks" in out
     assert dt < 540, dt
 
