@@ -23,7 +23,8 @@ import torch.distributed as dist
 
 from . import ops
 from .models.config import NativeConfig
-from .models.native import HeadShard, NativeModel, ParamArena, balanced_layer_ranges, stage_cost_model
+from .models.native import (HeadShard, NativeModel, ParamArena, balanced_layer_ranges, comm_units,
+                            stage_cost_model)
 from .models.stage import NativeStage
 from .parallel.collectives import Collectives
 from .parallel.comm import P2P
@@ -218,10 +219,11 @@ def plan_head_pipeline(cfg: NativeConfig, pp: int, schedule: str, m: int, mbs: i
     base = generate(schedule, pp, m, v, style)
     regen = ((lambda lag: generate(schedule, pp, m, v, style, warmup_extra=lag)) if schedule in WARMUP_EXTRA
              else None)
-    orders, lag, makespan = plan_head_schedule(base, pp, v, style, head_costs, stage_costs, regen=regen)
+    comm = comm_units(cfg, seq_len, tokens=T)
+    orders, lag, makespan = plan_head_schedule(base, pp, v, style, head_costs, stage_costs, regen=regen, comm=comm)
     # no-bubble time in the same units (F = 1, B = 2 per stage-cost unit)
     ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * m / pp
-    return dict(schedule=schedule, v=v, style=style, layer_ranges=layer_ranges, stage_costs=stage_costs,
+    return dict(schedule=schedule, v=v, style=style, layer_ranges=layer_ranges, stage_costs=stage_costs, comm=comm,
                 chunks=chunks, head_costs=head_costs, orders=orders, lag=lag, makespan=makespan, ideal=ideal,
                 efficiency=ideal / makespan if makespan > 0 else 0.0)
 

@@ -737,6 +737,28 @@ def stage_cost_model(cfg: NativeConfig, seq_len: int = 1024) -> Tuple[float, flo
     return 1.0, head_units + 0.1, 0.1
 
 
+def comm_units(cfg: NativeConfig, seq_len: int = 1024, link_gbps: Optional[float] = None,
+               latency_us: float = 15.0, tokens: int = 32768) -> float:
+    """Transfer time of one microbatch's stage-boundary activation (bf16 [T, d]) in the
+    forward-layer units of :func:`stage_cost_model` -- the simulator's p2p latency for the
+    head-aware schedule planner.  ``link_gbps``: effective one-direction p2p bandwidth of an
+    xGMI link (MIPIPE_LINK_GBPS, default 60: MI355X's 153.6 GB/s link figure counts both
+    directions; RCCL p2p reaches ~80 % of a direction).  GPT-2 small: ~1.0 unit, i.e. a
+    hop costs about one layer forward."""
+    if link_gbps is None:
+        link_gbps = float(os.environ.get("MIPIPE_LINK_GBPS", "60"))
+    d = cfg.d_model
+    mm = d * cfg.qkv_dim + d * d + (3 if cfg.activation == "swiglu" else 2) * d * cfg.d_ff
+    attn = 2.0 * seq_len * d * (0.5 if cfg.causal else 1.0)
+    if cfg.cross_attn:
+        mm += 4 * d * d
+        attn *= 2
+    t_layer = _LAYER_OVERHEAD * (3 * 2 * mm / _E_GEMM + 2 * attn / _E_ATTN_F + 2.5 * 2 * attn / _E_ATTN_B)
+    unit = tokens * t_layer / 3.0                 # one layer forward of the microbatch
+    msg = tokens * d * 2 / (link_gbps * 1e9) + latency_us * 1e-6
+    return msg / unit
+
+
 def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 1024,
                           reference_rule: bool = False, head_on_last: bool = True) -> List[Tuple[int, int]]:
     """Layer ranges per stage.
