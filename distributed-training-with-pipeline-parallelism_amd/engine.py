@@ -229,10 +229,11 @@ def plan_head_pipeline(cfg: NativeConfig, pp: int, schedule: str, m: int, mbs: i
 
 
 def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
-                  candidates=("GPipe", "1F1B", "Interleaved1F1B")) -> Tuple[str, Dict[str, float]]:
-    """``schedule="auto"``: the candidate with the highest planned efficiency of the
-    head-aware plan (1F1B at PP = 1, where every schedule is bubble-free and 1F1B keeps one
-    stage per rank).  Returns (name, {name: planned efficiency})."""
+                  candidates=("GPipe", "1F1B", "Interleaved1F1B"), margin: float = 0.03) -> Tuple[str, Dict[str, float]]:
+    """``schedule="auto"``: 1F1B unless another candidate's head-aware plan is more
+    efficient by more than ``margin`` (relative) -- the plan's p2p model is an estimate, and
+    an interleaved rank sends twice the activations (1F1B at PP = 1, where every schedule is
+    bubble-free and 1F1B keeps one stage per rank).  Returns (name, {name: planned efficiency})."""
     if pp == 1:
         return "1F1B", {}
     eff = {}
@@ -242,6 +243,8 @@ def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
         except (ValueError, RuntimeError):
             continue
     best = max(eff, key=lambda k: (eff[k], k == "1F1B"))
+    if "1F1B" in eff and eff[best] < eff["1F1B"] * (1.0 + margin):
+        best = "1F1B"
     return best, eff
 
 

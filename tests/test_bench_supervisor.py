@@ -137,7 +137,8 @@ def test_bench_four_ranks_measures_all_three_schedules():
     # --schedule auto: the headline is the best-planned schedule, and it is measured once
     head = out["config"]["schedule"]
     assert out["value"] == sch[head]["tok_s"] and set(out["config"]["schedule_choice"]["auto"]) == set(sch)
-    assert out["config"]["schedule_choice"]["auto"][head] == max(out["config"]["schedule_choice"]["auto"].values())
+    eff = out["config"]["schedule_choice"]["auto"]
+    assert eff[head] == max(eff.values()) or (head == "1F1B" and max(eff.values()) < 1.03 * eff["1F1B"])
     assert out["p2p_bytes_per_step"] > 0 and "rccl_ranks" in out
     assert dt < 540, dt
 
