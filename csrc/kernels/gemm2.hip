@@ -249,12 +249,15 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
                                          uint64_t seed) {
   constexpr int RG = BM / WM;      // rows per group
   constexpr int CP = BN + 4;       // f32 pitch
+  // 8-column chunks per tile row; the store loop runs on the first NTE threads, a multiple
+  // of CH (all NTH threads for power-of-two widths; 504 of 512 for BN = 192)
+  constexpr int CH = BN / 8, NTE = (NTH / CH) * CH;
   float* ct = reinterpret_cast<float*>(smem);
   // bf16 outputs with WS != nullptr: also accumulate the column sums of the final values
   // into WS[N] (f32; the bias gradient of the next layer).  Every thread keeps the same 8
-  // columns over all its rows (NTH is a multiple of BN / 8), so the sums stay in registers
-  // until one LDS reduction and BN atomics per tile.
-  constexpr bool CS_OK = !ACC && (NTH % (BN / 8) == 0);
+  // columns over all its rows (its chunk idx % CH is fixed because the loop strides by NTE),
+  // so the sums stay in registers until one LDS reduction and BN atomics per tile.
+  constexpr bool CS_OK = !ACC;
   const bool cs = CS_OK && WS != nullptr;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll 1
@@ -291,8 +294,8 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
         continue;
       }
     }
-    for (int idx = threadIdx.x; idx < RG * BN / 8; idx += NTH) {
-      const int row = idx / (BN / 8), c8 = (idx % (BN / 8)) * 8;
+    for (int idx = threadIdx.x < NTE ? (int)threadIdx.x : RG * CH; idx < RG * CH; idx += NTE) {
+      const int row = idx / CH, c8 = (idx % CH) * 8;
       const int gr = rbase + row, gc = n0 + c8;
       if (gr >= M || gc >= N) continue;
       float v[8];
@@ -324,7 +327,7 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
 #pragma unroll
       for (int e = 0; e < 8; ++e) red[threadIdx.x * 8 + e] = csum[e];
       __syncthreads();
-      constexpr int CH = BN / 8, GRP = NTH / CH;   // column chunks; threads per chunk
+      constexpr int GRP = NTE / CH;   // threads per column chunk
       for (int c = threadIdx.x; c < BN; c += NTH) {
         float t = 0.f;
 #pragma unroll 4
@@ -898,6 +901,225 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
   const int nwg = ((M + 255) / 256) * ((N + 255) / 256);
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
                                           (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// gemm6: gemm3's ping-pong phase schedule (16x16x32 MFMAs, NT) on 256x192 tiles.
+//
+// Why: at the 32K-token microbatch of a PP > 1 rank the N = 768 GEMMs (fwd wo / fc2, dX of
+// qkv / wo / fc1) are 128 x 3 = 384 tiles of 256x256 = 1.5 rounds of 256 CUs: the second
+// round runs on half the chip (profiles/r3_gemm_tail_probe.txt: 0.83-0.92x hipBLASLt there,
+// 1.0x+ at M = 65536 where the grid is 3 whole rounds).  256x192 tiles make N = 768 four
+// tile columns (512 tiles = 2 whole rounds) and N = 2304 twelve (6 rounds instead of 4.5).
+// gemm2's 256x192 build (cfg 1) has the tile but not the schedule (2 stages, 4x slower
+// feed: 0.95x of gemm3 in the same probe).
+//
+// Layout: 8 waves as 4 (rows) x 2 (cols), 64 x 96 outputs each.  A K-tile (BK = 64) is four
+// LDS images, streamed one per phase exactly as in gemm3:
+//   A0 = rows {0..31, 64..95, 128..159, 192..223} (the first 32 rows of each wave row)
+//   A1 = the other 128 rows                                      (16 KiB each)
+//   B0 = cols {0..47, 96..143}   B1 = cols {48..95, 144..191}    (96 rows, 12 KiB each)
+// phase 1: A0 x B0, 2: A0 x B1, 3: A1 x B0, 4: A1 x B1 -- 2 x 3 blocks of 16x16, K = 64
+// in two 32-deep steps = 12 MFMAs per phase.  An A image is 16 one-KiB pieces (2 per
+// wave); a B image 12 (waves 0-3 issue 2, waves 4-7 one), so each wave's counted vmcnt
+// is 4 + 2 b (b = its B pieces per image): the wait retires exactly the image the next
+// phase reads, per issuing wave, and the barrier after it publishes it to all waves.
+// Waves 4-7 (one per SIMD, the partner of wave w - 4) run one barrier behind waves 0-3.
+// ---------------------------------------------------------------------------------------
+template <int EPI, bool ACC>
+__global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm6_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
+             const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+             float* __restrict__ WS, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr,
+             int64_t ldx, float alpha, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  constexpr int BM = 256, BN = 192, WM = 4, WN = 2;
+  constexpr int HA = 32, HB = 48;                 // a wave's rows / cols in one A / B image
+  constexpr int IMG_A = 128 * 128, IMG_B = 96 * 128;
+  constexpr int O_A1 = IMG_A, O_B0 = 2 * IMG_A, O_B1 = 2 * IMG_A + IMG_B;
+  constexpr int BUF = 2 * IMG_A + 2 * IMG_B;      // 56 KiB per K-tile, two buffers
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int wg = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GROUP = MP_G3_GROUP;
+  const int group = wg / (GROUP * gn);
+  const int first_m = group * GROUP;
+  const int gsz = min(gm - first_m, GROUP);
+  const int tm = first_m + (wg % (GROUP * gn)) % gsz;
+  const int tn = (wg % (GROUP * gn)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / WN, wc = wave % WN;
+  const int grp = wave >> 2;                      // ping-pong group (waves w, w + 4 share a SIMD)
+  const int wn = wc * (BN / WN);
+
+  const int nk = K / BK;
+
+  // staging: piece p = wave + 8 j holds image rows 8 p .. 8 p + 7 (lane row lr = lane >> 3,
+  // 16-byte chunk lane & 7); image row r & 15 = 8 (wave & 1) + lr for every piece
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ swzq(8 * (wave & 1) + lr);
+  const bool two_b = wave < 4;                    // B images: 12 pieces, waves 0-3 take the last 4
+  const bf16_t* pa0[2];
+  const bf16_t* pa1[2];
+  const bf16_t* pb0[2];
+  const bf16_t* pb1[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int r = 8 * (wave + 8 * j) + lr;        // image row
+    int a0 = m0 + (r / HA) * (BM / WM) + r % HA, a1 = a0 + HA;
+    a0 = a0 < M ? a0 : M - 1;                     // rows past the edge only feed masked outputs
+    a1 = a1 < M ? a1 : M - 1;
+    pa0[j] = A + (int64_t)a0 * lda + lc * 8;
+    pa1[j] = A + (int64_t)a1 * lda + lc * 8;
+    const int rb = r < 96 ? r : r - 64;           // waves 4-7, j = 1: no piece (never issued)
+    int b0 = n0 + (rb / HB) * (BN / WN) + rb % HB, b1 = b0 + HB;
+    b0 = b0 < N ? b0 : N - 1;
+    b1 = b1 < N ? b1 : N - 1;
+    pb0[j] = B + (int64_t)b0 * ldb + lc * 8;
+    pb1[j] = B + (int64_t)b1 * ldb + lc * 8;
+  }
+
+  // image h (0 = A0, 1 = B0, 2 = B1, 3 = A1: consumption order) of K-tile kt -> buffer kt & 1
+  auto issue = [&](int h, int kt) {
+    char* img = smem + (kt & 1) * BUF + (h == 0 ? 0 : h == 3 ? O_A1 : h == 1 ? O_B0 : O_B1);
+    const int64_t dk = (int64_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (j == 1 && (h == 1 || h == 2) && !two_b) continue;
+      const bf16_t* src = (h == 0 ? pa0[j] : h == 3 ? pa1[j] : h == 1 ? pb0[j] : pb1[j]) + dk;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(img + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+  // counted waits (derivation in the header): 4 + 2 b outstanding pieces, 2 + b for nk = 1
+  auto wait_steady = [&]() {
+    if (two_b) wait_vmcnt<8>(); else wait_vmcnt<6>();
+  };
+
+  f32x4 acc[4][6];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) acc[i][j] = f32x4{};
+
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  if (nk > 1) {
+    issue(0, 1);
+    issue(1, 1);
+    wait_steady();
+  } else {
+    if (two_b) wait_vmcnt<4>(); else wait_vmcnt<3>();
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (grp == 1) __builtin_amdgcn_s_barrier();  // stagger the two wave groups by one barrier
+  asm volatile("" ::: "memory");
+
+  bf16x8 af[2][2], b0[3][2], b1[3][2];
+  const int q = lane >> 4;
+  const int rA = wr * HA + (lane & 15);
+  const int rB = wc * HB + (lane & 15);
+  auto fq = [&](const char* img, int row, int st) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * ((4 * st + q) ^ swzq(row)));
+  };
+
+#define G6_MFMA(R0, BF, C0)                                                              \
+  __builtin_amdgcn_sched_barrier(0);                                                     \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                       \
+  _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                       \
+  _Pragma("unroll") for (int j_ = 0; j_ < 3; ++j_)                                       \
+    acc[R0 + i_][C0 + j_] = mfma16(af[i_][s_], BF[j_][s_], acc[R0 + i_][C0 + j_]);       \
+  __builtin_amdgcn_s_setprio(0);                                                         \
+  __builtin_amdgcn_sched_barrier(0);
+#define G6_BAR()                          \
+  asm volatile("" ::: "memory");          \
+  __builtin_amdgcn_s_barrier();           \
+  asm volatile("" ::: "memory");
+
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const bool steady = t + 2 < nk;
+    // ---- phase 1: A0 x B0
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i][s_] = fq(buf, rA + 16 * i, s_);
+#pragma unroll
+      for (int j = 0; j < 3; ++j) b0[j][s_] = fq(buf + O_B0, rB + 16 * j, s_);
+    }
+    if (t + 1 < nk) issue(2, t + 1);
+    if (steady) wait_steady(); else wait_vmcnt<0>();   // B1(t) landed
+    G6_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G6_MFMA(0, b0, 0);
+    G6_BAR();
+    // ---- phase 2: A0 x B1
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) b1[j][s_] = fq(buf + O_B1, rB + 16 * j, s_);
+    if (t + 1 < nk) issue(3, t + 1);
+    if (steady) wait_steady(); else wait_vmcnt<0>();   // A1(t) landed
+    G6_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G6_MFMA(0, b1, 3);
+    G6_BAR();
+    // ---- phase 3: A1 x B0; refill A0 of this buffer for K-tile t+2
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i][s_] = fq(buf + O_A1, rA + 16 * i, s_);
+    if (steady) issue(0, t + 2);
+    G6_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G6_MFMA(2, b0, 0);
+    G6_BAR();
+    // ---- phase 4: A1 x B1; refill B0; A0/B0 of K-tile t+1 retired for the next phase 1
+    if (steady) {
+      issue(1, t + 2);
+      wait_steady();
+    } else {
+      wait_vmcnt<0>();
+    }
+    G6_BAR();
+    G6_MFMA(2, b1, 3);
+    G6_BAR();
+  }
+#undef G6_MFMA
+#undef G6_BAR
+  if (grp == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered groups
+  __syncthreads();
+  epilogue<BM, BN, WM, WN, EPI, ACC>(Stage16<4, 6>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M, N, ldc,
+                                     ldr, ldx, alpha, 1, p_drop, seed);
+}
+
+template <int EPI, bool ACC>
+static int launch6(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
+                   int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
+                   float p_drop, uint64_t seed, hipStream_t st) {
+  constexpr int LDS_MAIN = 2 * (2 * 128 * 128 + 2 * 96 * 128);
+  constexpr int EPI_BYTES = 64 * (192 + 4) * 4;
+  constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
+  auto kern = gemm6_kernel<EPI, ACC>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int nwg = ((M + 255) / 256) * ((N + 191) / 192);
+  kern<<<dim3(nwg, 1), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (const bf16_t*)R,
+                                      (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
   return (int)hipGetLastError();
 }
 
@@ -1653,6 +1875,7 @@ static int dispatch(int cfg, const void* A, const void* B, void* C, const void* 
     if (cfg == 12) return launchs<32, 32, EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
+    if (cfg == 9) return launch6<EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
 #ifdef MP_PROBE_ENGINES
     if constexpr (!ACC) {
       if (cfg == 8) return launch5<EPI>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
@@ -1773,6 +1996,27 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
     const int t256 = ((M + 255) / 256) * ((N + 255) / 256);
     if (t256 >= 96) cfg = 5;
   }
+  // the 256x192 ping-pong engine (gemm6) where its grid fills whole rounds of 256 CUs
+  // better than 256x256 does on a multi-round grid: modelled time = rounds x tile area /
+  // tile efficiency, 0.84 measured (profiles/r4_gemm6_tail_probe.txt: N = 768 at 32K
+  // tokens 2 rounds x 0.89 vs 2 rounds with the second half empty, +3-7 %; 12 MFMAs per
+  // phase against gemm3's 16 under the same barriers cost 16 % per tile, so 4.5-round
+  // grids and one-round grids stay on gemm3).  Opt-in (MIPIPE_GEMM6=1; force_cfg 9 selects
+  // it): inside the step it lost -- 946K vs 973K tok/s with 2 lanes, 929K vs 933K with one,
+  // at the PP > 1 per-rank work (r4_gemm6_tail_probe.txt) -- the lanes already fill the
+  // half-empty round that it fixes, and it pays its lower per-tile rate everywhere
+  static const bool use6 = [] { const char* e = getenv("MIPIPE_GEMM6"); return e && e[0] == '1'; }();
+  if (!transA && !transB && use6 && force_cfg < 0 && split == 1 && cfg == 5) {
+    const int gm = (M + 255) / 256;
+    const int t256 = gm * ((N + 255) / 256);
+    const float r256 = (float)((t256 + 255) / 256);
+    const float r192 = (float)((gm * ((N + 191) / 192) + 255) / 256) * (0.75f / 0.84f);
+    if (t256 > 256 && r192 < 0.97f * r256) cfg = 9;
+  }
+  if (force_cfg == 9) {
+    cfg = (transA || transB) ? 0 : 9;
+    split = 1;
+  }
   // the TT (dW) build of the ping-pong engine: 256x256 tiles, split-K f32 accumulate
   // (MIPIPE_GEMM3T=0 keeps the 2-stage gemm2 TT engine)
   static const bool use3t = [] { const char* e = getenv("MIPIPE_GEMM3T"); return !(e && e[0] == '0'); }();
@@ -1829,9 +2073,9 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   int split = 1;
   const int cfg = mp_gemm2_plan(M, N, K, transA, transB, c_f32_accum, force_cfg, &split);
   if (colsum != nullptr) {
-    // fused output column sums: bf16 outputs, one pass (no split-K), tiles whose width
-    // divides the 512-thread epilogue (not 256x192); -3 tells the caller to sum separately
-    if (c_f32_accum || split > 1 || cfg == 1) return -3;
+    // fused output column sums: bf16 outputs, one pass (no split-K); -3 tells the caller
+    // to sum separately
+    if (c_f32_accum || split > 1) return -3;
     ws = colsum;
   }
   // plain / bias NT GEMMs of more 256x256 tiles than CUs: the persistent engine that

@@ -404,7 +404,7 @@ def test_default_build_has_no_probe_engines():
     assert not _probe_engines()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, pytest.param(8, marks=needs_probe_engines), 10, 11, 12])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, pytest.param(8, marks=needs_probe_engines), 9, 10, 11, 12])
 @pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, "bias_gelu"), (1000, 2304, 256, "bias"), (256, 384, 128, "res"),
                                        (520, 136, 64, "none"), (512, 768, 3072, "dgelu"), (1000, 1000, 640, "none"),
                                        (768, 512, 128, "bias")])
@@ -470,7 +470,7 @@ def test_gemm2_dw_splitk(cfg, M, N, K):
     close(g, base + dy.float().t() @ x.float(), atol=3e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 10])
+@pytest.mark.parametrize("cfg", [-1, 1, 4, 5, 9, 10])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 50304), (2048, 768, 8192), (300, 200, 4096)])
 def test_gemm2_nt_splitk_accumulate(cfg, M, N, K):
     """Both-K-contiguous operands into an f32 accumulator with split-K (distributed-head dX)."""
@@ -483,7 +483,7 @@ def test_gemm2_nt_splitk_accumulate(cfg, M, N, K):
     close(g, base + a.float() @ b.float().t(), atol=5e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize("cfg", [10, 11, 12, -1])
+@pytest.mark.parametrize("cfg", [10, 11, 12, 1, 9, -1])
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (1024, 2304, 768), (1000, 2048, 768), (1024, 768, 2048)])
 def test_gemm_small_engine_bias_relu_and_colsum(cfg, M, N, K):
     """Small-tile NT engine (reference-model 1024-token shapes): fused bias + ReLU with the

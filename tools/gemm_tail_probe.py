@@ -1,7 +1,9 @@
 """Tile-wave quantisation of the N = 768 GEMMs at 32K-token microbatches (the PP > 1 bench
 microbatch): 256x256 tiles are 384 = 1.5 waves of 256 CUs; 256x192 tiles are 512 = 2 waves.
-Times forced configs (gemm2 cfg 1 = 256x192, cfg 2 = 256x128, -1 = the planner's choice,
-i.e. the ping-pong 256x256 engine) and hipBLASLt, interleaved.  python tools/gemm_tail_probe.py"""
+Times forced configs (5 = the ping-pong 256x256 engine gemm3, 9 = the ping-pong 256x192
+engine gemm6, 1 = gemm2's 2-stage 256x192, -1 = the planner's choice) and hipBLASLt,
+interleaved.  python tools/gemm_tail_probe.py [--ms 8192,32768,65536] [--cfgs -1,5,9,1]"""
+import argparse
 import os
 import sys
 
@@ -25,14 +27,19 @@ def t(fn, it=20):
     return s.elapsed_time(e) / it * 1e3
 
 
-for M in (32768, 65536):
+ap = argparse.ArgumentParser()
+ap.add_argument("--ms", default="32768,65536")
+ap.add_argument("--cfgs", default="-1,5,9,1")
+a = ap.parse_args()
+CFGS = [int(c) for c in a.cfgs.split(",")]
+for M in [int(m) for m in a.ms.split(",")]:
     for N, K in ((768, 768), (768, 2304), (768, 3072), (2304, 768), (3072, 768)):
         x = torch.randn(M, K, device="cuda", dtype=torch.bfloat16)
         w = torch.randn(N, K, device="cuda", dtype=torch.bfloat16) * K ** -0.5
         y = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
         res = {}
         for rep in range(2):
-            for cfg in (-1, 1, 2):
+            for cfg in CFGS:
                 us = t(lambda: _k._gemm(x, w, y, cfg=cfg))
                 res[cfg] = min(res.get(cfg, 1e9), us)
             us = t(lambda: torch.mm(x, w.t(), out=y))
