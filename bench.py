@@ -42,8 +42,8 @@ supervisor.  The child arms a watchdog over init, warmup, every timed step and t
 step (on a stall it prints the program grid + all stacks and exits non-zero); the
 process-group timeout is 300 s.  If the headline fails on any rank, the supervisors retry
 it in a more conservative mode (the native engine with collectives deferred to the step
-end and one compute stream per rank, then torch p2p, then no HIP graphs) on a fresh
-rendezvous port; ``attempt`` / ``attempt_mode`` say which one produced the number, and
+end and one compute stream per rank, then torch p2p, then no HIP graphs, last every
+process group on gloo) on a fresh rendezvous port; ``attempt`` / ``attempt_mode`` say which one produced the number, and
 the other schedules run in that mode.  One global deadline
 (MIPIPE_BENCH_DEADLINE_S, default 540 s, under the driver's 600 s) bounds everything:
 each child gets at most what is left of it (and at most MIPIPE_BENCH_ATTEMPT_S, default
@@ -75,8 +75,11 @@ BASELINE_NOTE = ("no same-config reference number: BASELINE.md only has the refe
 
 # supervisor attempts of the headline: (p2p transport, HIP graphs + native tape).  "-safe":
 # the native engine with the round-4 concurrency features off -- collectives deferred to
-# the step end (serial-model proof) and one compute stream per pipeline rank
-ATTEMPTS = [("auto", 1), ("auto-safe", 1), ("torch", 1), ("torch", 0)]
+# the step end (serial-model proof) and one compute stream per pipeline rank.  "gloo": the
+# last resort when RCCL itself is unusable on the node -- every process group on gloo, p2p
+# and collectives staged through host memory (slow, but a measured, labelled number:
+# attempt_mode = "gloo", p2p = "gloo-staged")
+ATTEMPTS = [("auto", 1), ("auto-safe", 1), ("torch", 1), ("torch", 0), ("gloo", 1)]
 # the reference's three schedules (helper:215-220), measured back to back in one call
 SCHEDULES = ("GPipe", "1F1B", "Interleaved1F1B")
 # published L8 H8 rows of the reference (nb:703-708): (schedule, P) -> tok/s
@@ -209,6 +212,20 @@ def extra_budget(kind: str, left: float, cap: float, head_wall: float, ref_wall=
     return min(b, max(2.0 * est, 90.0)), est
 
 
+def child_env(base: dict, p2p: str, attempt: int, port: int, budget: float, res_path: str) -> dict:
+    """Environment of one supervised child: its attempt mode (ATTEMPTS), a fresh rendezvous
+    port, its time budget and where rank 0 writes the result."""
+    env = dict(base, MIPIPE_BENCH_CHILD="1", MIPIPE_P2P=p2p.split("-")[0], MIPIPE_BENCH_ATTEMPT=str(attempt),
+               MASTER_PORT=str(port), MIPIPE_BENCH_ATTEMPT_S=f"{budget:.0f}", MIPIPE_BENCH_RESULT=res_path,
+               MIPIPE_BENCH_MODE=p2p)
+    if p2p == "gloo":
+        env.update(MIPIPE_DIST_BACKEND="gloo", MIPIPE_P2P="auto")
+    if p2p.endswith("-safe"):
+        env.update(MIPIPE_COLL_OVERLAP="0", MIPIPE_PP_LANES="0")
+    env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # fresh rendezvous store per child
+    return env
+
+
 def plan_phases(a, argv) -> list:
     """The fixed, rank-independent list of child runs: (tag, kind, argv, schedule).  The
     headline's attempts first, then every other schedule of ``--schedules`` on the same
@@ -257,12 +274,7 @@ def supervise(a, argv) -> int:
 
     def run_child(j, tag, child_argv, p2p, graphs, attempt, budget):
         res_path = os.path.join(d, f"{tag}.json")
-        env = dict(os.environ, MIPIPE_BENCH_CHILD="1", MIPIPE_P2P=p2p.split("-")[0], MIPIPE_BENCH_ATTEMPT=str(attempt),
-                   MASTER_PORT=str(base_port + 1 + j), MIPIPE_BENCH_ATTEMPT_S=f"{budget:.0f}",
-                   MIPIPE_BENCH_RESULT=res_path, MIPIPE_BENCH_MODE=p2p)
-        if p2p.endswith("-safe"):
-            env.update(MIPIPE_COLL_OVERLAP="0", MIPIPE_PP_LANES="0")
-        env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # fresh rendezvous store per child
+        env = child_env(os.environ, p2p, attempt, base_port + 1 + j, budget, res_path)
         cmd = [sys.executable, os.path.abspath(__file__)] + child_argv + ["--graphs", str(graphs)]
         t0 = time.monotonic()
         proc = subprocess.Popen(cmd, env=env)

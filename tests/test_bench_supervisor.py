@@ -60,6 +60,25 @@ def test_default_budget_fits_the_driver_timeout():
     assert n >= 2 and t <= 560.0, (n, t)
 
 
+def test_attempt_modes_and_last_resort_gloo():
+    """The headline's attempts go from the full native path to ever more conservative ones;
+    the last moves every process group to gloo (RCCL unusable on the node), so a number --
+    labelled by attempt_mode / p2p -- still comes out."""
+    sys.path.insert(0, ROOT)
+    import bench
+    modes = [m for m, _ in bench.ATTEMPTS]
+    assert modes[0] == "auto" and modes[-1] == "gloo"
+    base = {"TORCHELASTIC_USE_AGENT_STORE": "1", "PATH": "/usr/bin"}
+    e = bench.child_env(base, "gloo", 4, 29600, 120.0, "/tmp/x.json")
+    assert e["MIPIPE_DIST_BACKEND"] == "gloo" and e["MIPIPE_P2P"] == "auto" and e["MIPIPE_BENCH_MODE"] == "gloo"
+    assert "TORCHELASTIC_USE_AGENT_STORE" not in e and e["MASTER_PORT"] == "29600"
+    e = bench.child_env(base, "auto-safe", 1, 29601, 120.0, "/tmp/x.json")
+    assert e["MIPIPE_P2P"] == "auto" and e["MIPIPE_COLL_OVERLAP"] == "0" and e["MIPIPE_PP_LANES"] == "0"
+    assert "MIPIPE_DIST_BACKEND" not in e
+    e = bench.child_env(base, "torch", 2, 29602, 120.0, "/tmp/x.json")
+    assert e["MIPIPE_P2P"] == "torch" and "MIPIPE_COLL_OVERLAP" not in e
+
+
 def test_two_stalled_attempts_end_nonzero_within_the_deadline():
     """Every attempt stalls: the supervisor gives up non-zero inside its global deadline
     (scaled down here to 80 s; the default is 540 s, test above)."""
