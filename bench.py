@@ -104,9 +104,10 @@ def parse(argv=None):
                          "the compat API on the native fp32 path, per schedule (auto: with a GPU)")
     ap.add_argument("--ref-args", default="8,8,32,128",
                     help="reference-config layers,heads,batch,seq (CPU tests shrink it)")
-    ap.add_argument("--phase", default="sched", choices=["sched", "ref"], help=argparse.SUPPRESS)
+    ap.add_argument("--phase", default="sched", choices=["sched", "ref", "plan"], help=argparse.SUPPRESS)
     ap.add_argument("--mbs", type=int, default=None,
-                    help="sequences per microbatch (default: 64 on one GPU, 32 with a pipeline)")
+                    help="sequences per microbatch (default: 64 on one GPU; with a pipeline the supervisor "
+                         "plans 32 or 16 -- engine.pick_microbatch -- and 32 without it)")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--microbatches", type=int, default=None)
     ap.add_argument("--dp", type=int, default=1)
@@ -303,7 +304,22 @@ def supervise(a, argv) -> int:
             _publish(done_path, "1")
         return rc, res, time.monotonic() - t0
 
+    # --mbs auto (no --mbs / --microbatches given, PP > 1): rank 0 plans the microbatch size
+    # in a CPU-only child (engine.pick_microbatch) and every rank's children get it
+    mbs_plan = None
+    pp = max(1, int(os.environ.get("WORLD_SIZE", "1")) // max(1, a.dp))
+    if a.mbs is None and a.microbatches is None and pp > 1 and os.environ.get("MIPIPE_BENCH_MBS", "auto") == "auto":
+        plan_path = os.path.join(d, "mbs.plan")
+        if rank == 0:
+            mbs_plan = plan_microbatch_child(argv, min(120.0, max(10.0, left() - 300.0)))
+            _publish(plan_path, json.dumps(mbs_plan))
+        else:
+            txt = _wait_file(plan_path, 180.0)
+            mbs_plan = json.loads(txt) if txt else None
+        if mbs_plan and mbs_plan.get("mbs"):
+            argv = list(argv) + ["--mbs", str(mbs_plan["mbs"]), "--microbatches", str(mbs_plan["microbatches"])]
     phases = plan_phases(a, argv)
+    walls = {"plan": round(time.monotonic() - t_start, 1)}
     results = {}
     headline = None
     head_wall = None
@@ -335,6 +351,7 @@ def supervise(a, argv) -> int:
             continue
         _, b, p2p, graphs, att = decision.split()
         rc, res, wall = run_child(j, tag, child_argv, p2p, int(graphs), int(att), float(b))
+        walls[tag] = round(wall, 1)
         if rank != 0:
             continue
         if kind == "headline":
@@ -357,8 +374,42 @@ def supervise(a, argv) -> int:
     _publish(final_path, "ok" if headline is not None else "fail")
     if headline is None:
         return 1
-    print(json.dumps(merge_results(headline, results, a)), flush=True)
+    out = merge_results(headline, results, a)
+    if mbs_plan is not None:
+        out.setdefault("config", {})["mbs_choice"] = mbs_plan
+    out["supervisor_walls_s"] = dict(walls, total=round(time.monotonic() - t_start, 1))
+    print(json.dumps(out), flush=True)
     return 0
+
+
+def plan_microbatch_child(argv, timeout_s: float) -> dict:
+    """Run ``bench.py --phase plan`` (pure planning, no GPU) and return its JSON, or
+    {"error": ...} -- the children then keep the fixed default (32 sequences)."""
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv) + ["--phase", "plan"]
+    env = dict(os.environ, MIPIPE_BENCH_CHILD="1")
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode == 0 and lines:
+            return json.loads(lines[-1])
+        return {"error": f"plan child rc={r.returncode}: {r.stderr[-300:]}"}
+    except subprocess.TimeoutExpired:
+        return {"error": f"plan child exceeded {timeout_s:.0f}s"}
+
+
+def run_plan(a) -> None:
+    """--phase plan: the microbatch size for the supervisor (never touches the GPU)."""
+    import mipipe  # noqa: F401
+    from mipipe.engine import pick_microbatch
+    from mipipe.models.config import NativeConfig
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    pp = max(1, world // max(1, a.dp))
+    kw = {"vocab_size": a.vocab} if a.vocab else {}
+    cfg = NativeConfig.by_name(a.model, **kw)
+    t0 = time.monotonic()
+    mbs, m, scores = pick_microbatch(cfg, pp, a.seq, 128 * pp)
+    print(json.dumps({"mbs": mbs, "microbatches": m, "scores": {str(k): v for k, v in scores.items()},
+                      "plan_s": round(time.monotonic() - t0, 1)}), flush=True)
 
 
 def _sched_entry(r: dict) -> dict:
@@ -741,6 +792,8 @@ def main():
         sys.exit(supervise(a, child_argv))
     if a.phase == "ref":
         run_ref(a)
+    elif a.phase == "plan":
+        run_plan(a)
     else:
         run(a)
 

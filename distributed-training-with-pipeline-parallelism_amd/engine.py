@@ -248,6 +248,55 @@ def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
     return best, eff
 
 
+# Per-GPU training throughput vs tokens per microbatch (GEMM M), relative to 32K tokens:
+# GPT-2 small, 128 x 1024 tokens per step, 2 microbatch lanes, one MI355X
+# (profiles/r4_bench_1gpu_mbs_sweep.json: 973K / 947K / 907K / 750K tok/s at 64K / 32K /
+# 16K / 8K tokens).  Smaller microbatches shrink the pipeline bubble but run each kernel
+# on fewer rows.
+MICROBATCH_RATE = ((65536, 1.027), (32768, 1.0), (16384, 0.958), (8192, 0.79))
+
+
+def microbatch_rate(tokens: int) -> float:
+    """MICROBATCH_RATE interpolated in log2(tokens), clamped at the ends."""
+    import math
+    pts = sorted(MICROBATCH_RATE)
+    if tokens <= pts[0][0]:
+        return pts[0][1]
+    if tokens >= pts[-1][0]:
+        return pts[-1][1]
+    for (t0, r0), (t1, r1) in zip(pts, pts[1:]):
+        if t0 <= tokens <= t1:
+            f = (math.log2(tokens) - math.log2(t0)) / (math.log2(t1) - math.log2(t0))
+            return r0 + f * (r1 - r0)
+    return 1.0
+
+
+def pick_microbatch(cfg: NativeConfig, pp: int, seq_len: int, seqs_per_replica: int,
+                    candidates=(32, 16), margin: float = 0.02) -> Tuple[int, int, Dict[int, dict]]:
+    """``--mbs auto`` at PP > 1 with a fixed batch per pipeline replica (weak scaling): for
+    each candidate microbatch size the schedule ``pick_schedule`` would run and its planned
+    efficiency (bubble + distributed head + p2p), times the measured per-microbatch kernel
+    rate (``microbatch_rate``).  The first candidate (the larger microbatch) is kept unless
+    another scores more than ``margin`` better.  Returns (mbs, microbatches, {mbs: detail})."""
+    scores = {}
+    for mbs in candidates:
+        if seqs_per_replica % mbs:
+            continue
+        m = seqs_per_replica // mbs
+        sched, eff = pick_schedule(cfg, pp, m, mbs, seq_len)
+        e = eff.get(sched, 1.0 if pp == 1 else 0.0)
+        rate = microbatch_rate(mbs * seq_len)
+        scores[mbs] = {"microbatches": m, "schedule": sched, "planned_efficiency": round(e, 4),
+                       "kernel_rate": round(rate, 4), "score": round(e * rate, 4)}
+    if not scores:
+        raise ValueError(f"no candidate microbatch size divides {seqs_per_replica} sequences")
+    first = next(iter(scores))
+    best = max(scores, key=lambda k: scores[k]["score"])
+    if scores[best]["score"] < scores[first]["score"] * (1.0 + margin):
+        best = first
+    return best, scores[best]["microbatches"], scores
+
+
 def auto_lanes(cfg: NativeConfig, pp: int, v: int, graphs: bool, device, m: int, tokens: int, params: int,
                layers: int, recompute: bool = False) -> int:
     """Microbatch lanes (PipelineRuntime.set_lanes) at PP = 1 with HIP graphs: up to 4 for

@@ -129,6 +129,25 @@ def test_bench_default_batch_is_128_sequences_per_gpu():
     assert out["scaling"] == "weak" and out["n_gpus"] == 1
 
 
+def test_bench_pipeline_plans_the_microbatch_size():
+    """No --mbs at PP > 1: rank 0's supervisor plans the microbatch size in a CPU-only child
+    (engine.pick_microbatch), every rank's children run it, the batch stays 128 sequences
+    per GPU, and the record carries the plan (config.mbs_choice)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_PORT=str(free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--model", "gpt2-tiny", "--vocab", "256",
+           "--seq", "8", "--steps", "1", "--warmup", "1", "--no-bubble", "--schedules", "none"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    c = out["config"]
+    plan = c["mbs_choice"]
+    assert plan["mbs"] in (16, 32) and set(plan["scores"]) == {"16", "32"}, plan
+    assert c["micro_batch"] == plan["mbs"] and c["microbatches"] == plan["microbatches"]
+    assert c["micro_batch"] * c["microbatches"] == 256 and c["global_batch"] == 256
+
+
 def test_bench_four_ranks_measures_all_three_schedules():
     """One ``bench.py --gpus 4`` call (CPU/gloo) measures the reference's comparison --
     GPipe, 1F1B and Interleaved1F1B on the same model/config, each with its measured and

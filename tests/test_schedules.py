@@ -302,3 +302,26 @@ def test_overlapped_programs_proven_with_and_without_lanes(name, v, P, dp):
         for lanes in (1, 2):
             check_lowered(prog, P * v, channels=ch, dp=dp, lanes=lanes)
     check_lowered(defer_collectives(prog), P * v, serial=True, dp=dp)
+
+
+def test_microbatch_rate_interpolates_the_measured_table():
+    from mipipe.engine import MICROBATCH_RATE, microbatch_rate
+    assert microbatch_rate(32768) == 1.0 and microbatch_rate(1 << 20) == MICROBATCH_RATE[0][1]
+    assert microbatch_rate(1024) == MICROBATCH_RATE[-1][1]
+    r = [microbatch_rate(t) for t in (8192, 12000, 16384, 24000, 32768, 65536)]
+    assert r == sorted(r), r          # more rows per kernel never plans slower
+
+
+def test_pick_microbatch_weak_scaling_gpt2_small():
+    """--mbs auto: at P = 4 the bubble saved by 32 microbatches of 16 outweighs their lower
+    kernel rate; at P = 2 it does not (within the 2 % margin) and 32-sequence microbatches
+    stay.  The batch per replica is fixed (128 P sequences)."""
+    from mipipe.engine import pick_microbatch
+    from mipipe.models.native import NativeConfig
+    cfg = NativeConfig.by_name("gpt2-small")
+    mbs, m, sc = pick_microbatch(cfg, 4, 1024, 512)
+    assert (mbs, m) == (16, 32) and set(sc) == {32, 16}
+    assert sc[16]["planned_efficiency"] > sc[32]["planned_efficiency"]
+    assert sc[16]["score"] > 1.02 * sc[32]["score"]
+    mbs, m, sc = pick_microbatch(cfg, 2, 1024, 256)
+    assert (mbs, m) == (32, 8)
