@@ -284,6 +284,115 @@ static int launch(Args p, int split, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Stream-K over the 64x64 engine.  The reference's 1024-token GEMMs are 192-576 tiles: at
+// split 1 a 192-tile grid leaves 64 of 256 CUs idle, and split-K cannot spread 192 tiles
+// evenly either (split 2 = 384 workgroups: half the CUs run two, the makespan is the same).
+// Here the grid is G workgroups (one or two per CU) and the tiles x K-pairs work units are
+// cut into G equal chunks of c <= 2 npairs consecutive units (k-fastest): a workgroup
+// computes the pieces of the (at most SK_SEG) tiles its chunk touches, each into its own
+// dense 64x64 partial ws[g][seg] (the same pipeline, kh halves and LDS combine as the tiled
+// kernel); one pass sums the partials of every tile in workgroup order (deterministic) and
+// applies the epilogue.
+// ---------------------------------------------------------------------------------------
+constexpr int SK_SEG = 3;
+
+template <bool A_KC, bool B_KC>
+__global__ void __launch_bounds__(NTH, 2) gemm_f32_sk_kernel(Args p, int npairs, int chunk) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * 2 * OPS];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, hl = lane >> 5;
+  const int wave = tid >> 6, kh = wave >> 2, wm = ((wave >> 1) & 1) * 32, wn = (wave & 1) * 32;
+  const int gn = (p.N + BT - 1) / BT;
+  const int tiles = ((p.M + BT - 1) / BT) * gn;
+  const int g = blockIdx.x;
+  const int units = tiles * npairs;
+  int u = g * chunk;
+  const int u_end = min(units, u + chunk);
+#pragma unroll 1
+  for (int seg = 0; seg < SK_SEG && u < u_end; ++seg) {
+    const int tile = u / npairs;
+    const int kp0 = u - tile * npairs, kp1 = min(npairs, u_end - tile * npairs);
+    const int m0 = (tile / gn) * BT, n0 = (tile % gn) * BT;
+    Stage<A_KC> sa0, sa1;
+    Stage<B_KC> sb0, sb1;
+    f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+    sa0.load(p.A, p.lda, m0, p.M, kp0 * 2 * BK, p.K);
+    sb0.load(p.B, p.ldb, n0, p.N, kp0 * 2 * BK, p.K);
+    sa1.load(p.A, p.lda, m0, p.M, (kp0 + 1) * 2 * BK, p.K);
+    sb1.load(p.B, p.ldb, n0, p.N, (kp0 + 1) * 2 * BK, p.K);
+    sa0.store(smem);
+    sb0.store(smem + OPS);
+    __syncthreads();
+    int kp = kp0;
+    for (; kp + 1 < kp1; kp += 2) {
+      pair_step<A_KC, B_KC>(p, smem, 0, kp, kp1, m0, n0, kh, wm, wn, l32, hl, acc0, acc1, sa0, sb0, sa1, sb1);
+      pair_step<A_KC, B_KC>(p, smem, 1, kp + 1, kp1, m0, n0, kh, wm, wn, l32, hl, acc0, acc1, sa1, sb1, sa0, sb0);
+    }
+    if (kp < kp1)
+      pair_step<A_KC, B_KC>(p, smem, 0, kp, kp1, m0, n0, kh, wm, wn, l32, hl, acc0, acc1, sa0, sb0, sa1, sb1);
+    f32x16 acc = acc0 + acc1;
+    float* red = smem;
+    if (kh == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((wave & 3) * 16 + r) * 64 + lane] = acc[r];
+    }
+    __syncthreads();
+    if (kh == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += red[(wave * 16 + r) * 64 + lane];
+      // dense partial tile: local row wm + (r & 3) + 8 (r >> 2) + 4 hl, local col wn + l32
+      float* part = p.ws + ((int64_t)g * SK_SEG + seg) * (BT * BT);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) part[(wm + (r & 3) + 8 * (r >> 2) + 4 * hl) * BT + wn + l32] = acc[r];
+    }
+    __syncthreads();   // red / the staging buffers are reused by the next segment
+    u = (tile + 1) * npairs;
+  }
+}
+
+// C = epi(sum of the partial tiles that cover each output, in workgroup order), 4 columns
+// per thread
+template <int EPI>
+__global__ void __launch_bounds__(256) reduce_sk_kernel(Args p, int npairs, int chunk) {
+  const int64_t i4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)p.M * p.N;
+  if (i4 * 4 >= total) return;
+  uint32_t thr = 0;
+  float inv = 1.f;
+  uint64_t seed = p.seed;
+  if ((EPI == E_BIAS_RELU || EPI == E_DRELU) && p.p_drop > 0.f) {
+    seed = step_seed(seed);
+    thr = drop_thr(p.p_drop);
+    inv = 1.f / (1.f - p.p_drop);
+  }
+  const int row = (int)((i4 * 4) / p.N), col = (int)((i4 * 4) % p.N);
+  const int gn = (p.N + BT - 1) / BT;
+  const int tile = (row / BT) * gn + col / BT;
+  const int off = (row % BT) * BT + col % BT;
+  const int u0 = tile * npairs, u1 = u0 + npairs;      // this tile's units
+  float4 s = float4{0.f, 0.f, 0.f, 0.f};
+  for (int g = u0 / chunk; g * chunk < u1; ++g) {
+    const int seg = tile - (g * chunk) / npairs;          // this tile's index among g's tiles
+    const float4 t = *reinterpret_cast<const float4*>(p.ws + ((int64_t)g * SK_SEG + seg) * (BT * BT) + off);
+    s.x += t.x;
+    s.y += t.y;
+    s.z += t.z;
+    s.w += t.w;
+  }
+  epi_store<EPI>(p, row, col, s.x, thr, inv, seed);
+  epi_store<EPI>(p, row, col + 1, s.y, thr, inv, seed);
+  epi_store<EPI>(p, row, col + 2, s.z, thr, inv, seed);
+  epi_store<EPI>(p, row, col + 3, s.w, thr, inv, seed);
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+static int launch_sk(Args p, int grid, int npairs, int chunk, hipStream_t st) {
+  gemm_f32_sk_kernel<A_KC, B_KC><<<grid, NTH, 0, st>>>(p, npairs, chunk);
+  const int64_t n4 = (int64_t)p.M * p.N / 4;
+  reduce_sk_kernel<EPI><<<(unsigned)((n4 + 255) / 256), 256, 0, st>>>(p, npairs, chunk);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // 128x128 engine (the guide's "128x128x32 block, 2x2 tiles of 32x32 per wave" shape, cdna
 // guide §3 'FP32-input MFMA': 122 TF untuned at 4096^3).  Per byte staged it does twice the
 // MFMA work of the 64x64 engine (32 vs 16 FLOP/B of operand), and each wave keeps FOUR
@@ -502,7 +611,44 @@ static int pick_split_big(int M, int N, int K, double* cost_out) {
 struct Plan {
   bool big;
   int split;
+  int sk_grid, sk_chunk;   // stream-K (64x64 engine): workgroups, units each; 0 = off
 };
+
+// stream-K instead of split-K when its busiest CU finishes earlier, in pick_split's units:
+// (workgroups per CU) x (chunk + ~3 pairs of pipeline fill per tile piece) + 1 for the
+// reduce pass, against rounds x (pairs / s + 3) (+ 1) of the best split.  Opt-in:
+// MIPIPE_F32_SK=auto plans it, =1 (or force_split = -2, the tests) forces it wherever the
+// chunk fits.  Off by default: +11 % on an isolated few-tile long-K GEMM (fwd linear2, 37.0
+// vs 41.5 us) but -1.4 % on the reference's fp32 step (182.6K vs 185.2K tok/s, 2 A/B
+// pairs, profiles/r4_f32_stream_k.txt) -- the microbatch lanes already fill the idle CUs
+// and the partial-tile pass is extra traffic.
+static void plan_sk(int M, int N, int K, Plan& pl, bool force) {
+  static const int mode = [] {   // 0 off (default), 1 forced, -1 planned ("auto")
+    const char* e = getenv("MIPIPE_F32_SK");
+    if (e && e[0] == 'a') return -1;
+    return e ? atoi(e) : 0;
+  }();
+  pl.sk_grid = pl.sk_chunk = 0;
+  if ((mode == 0 && !force) || pl.big) return;
+  const int tiles = ((M + BT - 1) / BT) * ((N + BT - 1) / BT);
+  const int npairs = (K + 2 * BK - 1) / (2 * BK);
+  const int units = tiles * npairs;
+  const int s = pl.split;
+  const double split_cost = (double)((tiles * s + 255) / 256) * ((double)npairs / s + 3.0) + (s > 1 ? 1.0 : 0.0);
+  double best = (mode == 1 || force) ? 1e30 : 0.97 * split_cost;
+  for (int per_cu = 1; per_cu <= 2; ++per_cu) {
+    const int G0 = 256 * per_cu;
+    const int c = (units + G0 - 1) / G0;
+    if (c < 4 || c > 2 * npairs) continue;
+    const double pieces = 1.0 + (double)(c - 1) / npairs;      // tiles a chunk touches, on average
+    const double cost = per_cu * (c + 3.0 * pieces) + 1.0;
+    if (cost < best) {
+      best = cost;
+      pl.sk_grid = (units + c - 1) / c;
+      pl.sk_chunk = c;
+    }
+  }
+}
 static Plan plan(int M, int N, int K, int force_split) {
   static const int mode = [] {
     const char* e = getenv("MIPIPE_F32_TILE");
@@ -516,18 +662,23 @@ static Plan plan(int M, int N, int K, int force_split) {
     const int rounds = (tiles + 511) / 512;
     big = tiles >= 448 && (double)tiles >= 0.85 * 512.0 * rounds;
   }
+  if (force_split == -2) big = false;   // forced stream-K (64x64 engine)
   int split = big ? pick_split_big(M, N, K, nullptr) : pick_split(M, N, K);
   if (big && mode == 0) split = 1;      // a full grid needs no split
   if (force_split > 0) split = force_split;
-  return Plan{big, split};
+  Plan pl{big, split, 0, 0};
+  if (force_split <= 0) plan_sk(M, N, K, pl, force_split == -2);
+  return pl;
 }
 
 }  // namespace gf32
 
 // floats of split-K workspace a problem needs (0: no split)
 extern "C" int64_t mp_gemm_f32_ws_elems(int M, int N, int K, int force_split) {
-  const int s = gf32::plan(M, N, K, force_split).split;
-  return (s > 1 && M % 4 == 0 && N % 4 == 0) ? (int64_t)s * M * N : 0;
+  const gf32::Plan pl = gf32::plan(M, N, K, force_split);
+  if (M % 4 || N % 4) return 0;
+  if (pl.sk_grid > 0) return (int64_t)pl.sk_grid * gf32::SK_SEG * gf32::BT * gf32::BT;
+  return pl.split > 1 ? (int64_t)pl.split * M * N : 0;
 }
 
 // epi: 0 none, 1 bias, 2 bias+ReLU (+dropout p_drop; pre-activation -> X), 3 residual,
@@ -546,10 +697,18 @@ extern "C" int mp_gemm_f32_ex(const float* A, const float* B, float* C, const fl
   const Plan pl = plan(M, N, K, force_split);
   int split = pl.split;
   if (ws == nullptr) split = 1;
-  Args p{A, B, C, bias, R, X, split > 1 ? ws : nullptr, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, accumulate,
+  const bool sk = pl.sk_grid > 0 && ws != nullptr;
+  Args p{A, B, C, bias, R, X, (split > 1 || sk) ? ws : nullptr, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, accumulate,
          p_drop, seed};
+  const int npairs = (K + 2 * BK - 1) / (2 * BK);
 #define MP_E(E)                                                                                      \
   case E:                                                                                            \
+    if (sk) {                                                                                        \
+      if (a_kc && b_kc) return launch_sk<true, true, E>(p, pl.sk_grid, npairs, pl.sk_chunk, st);     \
+      if (a_kc) return launch_sk<true, false, E>(p, pl.sk_grid, npairs, pl.sk_chunk, st);            \
+      if (b_kc) return launch_sk<false, true, E>(p, pl.sk_grid, npairs, pl.sk_chunk, st);            \
+      return launch_sk<false, false, E>(p, pl.sk_grid, npairs, pl.sk_chunk, st);                     \
+    }                                                                                                \
     if (pl.big) {                                                                                    \
       if (a_kc && b_kc) return launch_big<true, true, E>(p, split, st);                              \
       if (a_kc) return launch_big<true, false, E>(p, split, st);                                     \

@@ -90,6 +90,42 @@ def test_gemm_f32_epilogues(epi, p):
         close(y, 0.5 * lin + r.double())
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 2048), (1000, 776, 3000), (1024, 768, 768), (200, 136, 4096),
+                                   (1024, 2304, 768)])
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn"])
+@pytest.mark.parametrize("epi", ["none", "bias_relu", "accum"])
+def test_gemm_f32_stream_k(M, N, K, layout, epi):
+    """The stream-K schedule of the 64x64 engine (force_ks = -2): workgroup chunks that end
+    inside a tile and span up to three tiles, tails in M / N / K, every layout class and the
+    epilogues applied by the partial-tile reduce pass (ReLU + dropout with the forward mask
+    the backward regenerates, f32 accumulate with alpha)."""
+    torch.manual_seed(3)
+    a64, b64 = torch.randn(M, K, dtype=torch.float64), torch.randn(K, N, dtype=torch.float64) / math.sqrt(K)
+    A = a64.float().to(DEV) if layout[0] == "n" else a64.t().contiguous().float().to(DEV).t()
+    B = b64.t().contiguous().float().to(DEV).t() if layout[1] == "t" else b64.float().to(DEV)
+    ref = a64.float().double() @ b64.float().double()
+    e = ops.kernels._ext()
+    C = torch.full((M, N), float("nan"), device=DEV)
+    if epi == "none":
+        assert e.gemm_f32_ex(A, B, C, None, None, None, 0, 1.0, False, 0.0, 0, -2)
+        close(C, ref, atol=2e-4 * math.sqrt(K / 64), rtol=1e-5)
+    elif epi == "bias_relu":
+        bias = torch.randn(N, device=DEV)
+        X = torch.empty(M, N, device=DEV)
+        assert e.gemm_f32_ex(A, B, C, bias, None, X, 2, 1.0, False, 0.1, 11, -2)
+        pre = ref + bias.double().cpu()
+        close(X, pre, atol=2e-4 * math.sqrt(K / 64), rtol=1e-5)
+        C2 = torch.empty(M, N, device=DEV)     # the tiled engine: same dropout mask
+        assert e.gemm_f32_ex(A, B, C2, bias, None, torch.empty_like(X), 2, 1.0, False, 0.1, 11, 1)
+        assert torch.equal((C != 0), (C2 != 0))
+        close(C, C2, atol=2e-4 * math.sqrt(K / 64), rtol=1e-5)
+    else:
+        base = torch.randn(M, N, device=DEV)
+        C.copy_(base)
+        assert e.gemm_f32_ex(A, B, C, None, None, None, 0, 0.5, True, 0.0, 0, -2)
+        close(C, 0.5 * ref + base.double().cpu(), atol=2e-4 * math.sqrt(K / 64), rtol=1e-5)
+
+
 def test_linear_dw_f32_matches_torch():
     torch.manual_seed(2)
     T, N, K = 1024, 2304, 768
