@@ -87,6 +87,24 @@ NB_L8H8 = {("GPipe", 2): 1671.32, ("1F1B", 2): 1649.53, ("Interleaved1F1B", 2): 
            ("GPipe", 4): 1675.15, ("1F1B", 4): 1680.10, ("Interleaved1F1B", 4): 1739.43}
 
 
+# BASELINE.json's named multi-GPU configs (configs/*.yaml), measured after everything else
+# at the GPU count they name, each in its own child, only if the deadline leaves room:
+# (name, extra argv, estimated child seconds beyond the headline child's wall)
+BASE_CONFIGS = {
+    4: [("gpt2-small 1F1B PP=4 microbatches=8 (configs/gpt2_small_1f1b_pp4.yaml)",
+         ["--model", "gpt2-small", "--schedule", "1F1B", "--mbs", "16", "--microbatches", "8"], 0.0)],
+    8: [("gpt2-medium Interleaved1F1B PP=8 v=2 (configs/gpt2_medium_interleaved_pp8.yaml)",
+         ["--model", "gpt2-medium", "--schedule", "Interleaved1F1B", "--vstages", "2", "--mbs", "8",
+          "--microbatches", "16"], 30.0),
+        ("llama3-8b 1F1B PP=8 recompute (configs/llama3_8b_1f1b_pp8.yaml)",
+         ["--model", "llama3-8b", "--schedule", "1F1B", "--mbs", "1", "--microbatches", "16", "--seq", "8192",
+          "--recompute", "1"], 120.0),
+        ("llama3-8b DP=2 x PP=4 recompute (configs/llama3_8b_dp2_pp4.yaml)",
+         ["--model", "llama3-8b", "--dp", "2", "--schedule", "1F1B", "--mbs", "1", "--microbatches", "8", "--seq",
+          "8192", "--recompute", "1"], 120.0)],
+}
+
+
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None)
@@ -102,6 +120,9 @@ def parse(argv=None):
     ap.add_argument("--ref-fp32", default="auto", choices=["auto", "0", "1"],
                     help="also time the reference's own config (fp32 L8 H8, batch 32 x 128, m=4, fwd+bwd) through "
                          "the compat API on the native fp32 path, per schedule (auto: with a GPU)")
+    ap.add_argument("--base-configs", default="auto", choices=["auto", "0", "1"],
+                    help="at N = 4 / 8 also measure BASELINE.json's named configs (BASE_CONFIGS) last, if time "
+                         "allows (auto: on a GPU box only -- Llama-3 8B is not a CPU job)")
     ap.add_argument("--ref-args", default="8,8,32,128",
                     help="reference-config layers,heads,batch,seq (CPU tests shrink it)")
     ap.add_argument("--phase", default="sched", choices=["sched", "ref", "plan"], help=argparse.SUPPRESS)
@@ -207,6 +228,8 @@ def extra_budget(kind: str, left: float, cap: float, head_wall: float, ref_wall=
     later than 10 s before the global deadline -- so however the extras end, the whole
     run stays inside it."""
     est = ref_wall if (kind == "ref" and ref_wall) else (60.0 if kind == "ref" else head_wall * 1.25 + 10.0)
+    if kind.startswith("base"):     # "base:<extra seconds>"
+        est = head_wall * 1.25 + 10.0 + float(kind.split(":", 1)[1] if ":" in kind else 0.0)
     b = min(cap, left - 10.0)
     if b < max(MIN_ATTEMPT_S, est):
         return 0.0, est
@@ -238,6 +261,10 @@ def plan_phases(a, argv) -> list:
     if ref_fp32_on(a):
         for s in SCHEDULES:
             tags.append((f"r_{s}", "ref", list(argv) + ["--phase", "ref", "--schedule", s], s))
+    if (a.base_configs == "1") or (a.base_configs == "auto" and ref_fp32_on(argparse.Namespace(ref_fp32="auto"))):
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        for k, (name, extra, _) in enumerate(BASE_CONFIGS.get(world, [])):
+            tags.append((f"b{k}", "base", list(argv) + ["--dp", "1"] + extra, name))
     return tags
 
 
@@ -338,7 +365,11 @@ def supervise(a, argv) -> int:
             elif headline is not None and kind == "sched" and sched == headline["config"]["schedule"]:
                 pass        # the headline's own schedule: already measured
             elif headline is not None:
-                b, est = extra_budget(kind, left(), cap, head_wall, ref_wall)
+                kb = kind
+                if kind == "base":
+                    world = int(os.environ.get("WORLD_SIZE", "1"))
+                    kb = f"base:{BASE_CONFIGS[world][int(tag[1:])][2]}"
+                b, est = extra_budget(kb, left(), cap, head_wall, ref_wall)
                 if b > 0:
                     decision = f"go {b:.0f} {head_mode[0]} {head_mode[1]} {head_mode[2]}"
                 else:
@@ -464,6 +495,19 @@ def merge_results(headline: dict, results: dict, a) -> dict:
                       "dropout 0.1 (helper:23-55, :98-143, :214)".format(*a.ref_args.split(",")),
             "per_schedule": rb,
             "tok_s": max((v["tok_s"] for v in okr.values()), default=None)}
+    world = headline.get("n_gpus", 1)
+    base = {}
+    for tag, r in results.items():
+        if tag.startswith("b") and tag[1:].isdigit() and world in BASE_CONFIGS:
+            name = BASE_CONFIGS[world][int(tag[1:])][0]
+            e = _sched_entry(r)
+            if "tok_s" in e:
+                c = r.get("config", {})
+                e.update({k: c.get(k) for k in ("model", "schedule", "v", "parallelism", "micro_batch", "microbatches",
+                                                 "seq_len", "recompute", "global_batch")})
+            base[name] = e
+    if base:
+        out["baseline_configs"] = base
     return out
 
 

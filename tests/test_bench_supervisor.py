@@ -60,6 +60,51 @@ def test_default_budget_fits_the_driver_timeout():
     assert n >= 2 and t <= 560.0, (n, t)
 
 
+def test_baseline_configs_are_planned_last_at_their_gpu_count():
+    """BASELINE.json's named multi-GPU configs run after the headline, the other schedules
+    and the reference's fp32 config, at the GPU count they name (4: GPT-2 small 1F1B m=8;
+    8: GPT-2 medium interleaved, Llama-3 8B PP=8 and DP2 x PP4), and never by default off a
+    GPU box."""
+    sys.path.insert(0, ROOT)
+    import bench
+    old = os.environ.get("WORLD_SIZE")
+    try:
+        for world, n in ((4, 1), (8, 3), (2, 0)):
+            os.environ["WORLD_SIZE"] = str(world)
+            a = bench.parse(["--base-configs", "1", "--ref-fp32", "1"])
+            ph = bench.plan_phases(a, ["--steps", "3"])
+            kinds = [k for _, k, _, _ in ph]
+            assert kinds.count("base") == n
+            if n:
+                assert kinds[-n:] == ["base"] * n and kinds.index("base") > max(i for i, k in enumerate(kinds)
+                                                                                if k in ("ref", "sched"))
+                argv = ph[-n][2]
+                assert argv[:2] == ["--steps", "3"] and "--model" in argv
+            a = bench.parse(["--ref-fp32", "0"])
+            if not os.path.exists("/dev/kfd"):
+                assert not [p for p in bench.plan_phases(a, []) if p[1] == "base"]
+        os.environ["WORLD_SIZE"] = "8"
+        assert any("llama3-8b" in x for x in bench.plan_phases(bench.parse(["--base-configs", "1"]), [])[-1][2])
+    finally:
+        if old is None:
+            os.environ.pop("WORLD_SIZE", None)
+        else:
+            os.environ["WORLD_SIZE"] = old
+
+
+def test_merge_results_baseline_configs_block():
+    sys.path.insert(0, ROOT)
+    import bench
+    head = {"value": 10.0, "n_gpus": 4, "config": {"schedule": "1F1B"}}
+    res = {"b0": {"value": 7.0, "ms_per_step": 3.0, "config": {"model": "gpt2-small", "schedule": "1F1B",
+                                                               "microbatches": 8, "micro_batch": 16}}}
+    out = bench.merge_results(head, res, bench.parse(["--ref-fp32", "0"]))
+    (name, e), = out["baseline_configs"].items()
+    assert "gpt2-small" in name and e["tok_s"] == 7.0 and e["microbatches"] == 8 and e["model"] == "gpt2-small"
+    res = {"b0": {"skipped": "time"}}
+    assert bench.merge_results(head, res, bench.parse([]))["baseline_configs"][name] == {"skipped": "time"}
+
+
 def test_attempt_modes_and_last_resort_gloo():
     """The headline's attempts go from the full native path to ever more conservative ones;
     the last moves every process group to gloo (RCCL unusable on the node), so a number --
@@ -100,7 +145,7 @@ def test_bench_eight_ranks_gpt2_small_layout():
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1", "--mbs", "1",
-           "--seq", "32", "--vocab", "512"]
+           "--seq", "32", "--vocab", "512", "--base-configs", "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -156,7 +201,7 @@ def test_bench_four_ranks_measures_all_three_schedules():
     env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_PORT=str(free_port()))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4"] + ARGS[:-2]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--base-configs", "0"] + ARGS[:-2]
     t0 = time.monotonic()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
     dt = time.monotonic() - t0
