@@ -152,7 +152,7 @@ def max_inflight_microbatches(order, stages) -> int:
 
 def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, seq_len: int, device,
                    head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1,
-                   stage_shards: int = 1, dtype=torch.bfloat16) -> dict:
+                   stage_shards: int = 1, dtype=torch.bfloat16, graphs: bool = False) -> dict:
     """HBM plan of one pipeline rank and the recompute decision of ``recompute="auto"``:
     recompute only if the activation stash would not fit ``budget_frac`` of the device.
 
@@ -167,7 +167,11 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     f32 arenas (the reference's precision): the f32 weights ARE the master, so sharding
     leaves them whole and splits only the Adam moments -- 12 + 8 / shards bytes per
     parameter (head: 12 + 8 / head_shards).
-    Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute."""
+    Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute.
+    With HIP graphs every captured forward keeps its activations in the graph's private
+    pool (parallel/graphs.py), so the stash is held for every microbatch of the step, not
+    only the schedule's in-flight ones: ``graphs=True`` counts all of them (GPT-2 small,
+    32 x 16 sequences at P = 4: ~64 GB per rank measured, r4_INDEX.md)."""
     T = mbs * seq_len
     nlayers = sum(layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages)
     emb = cfg.vocab_padded * cfg.d_model
@@ -177,6 +181,9 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     head_opt = shard_b * emb / max(1, head_shards) if head_tokens else 0.0
     head_state = (fixed_b * emb if head_tokens else 0.0) + head_opt
     inflight = max_inflight_microbatches(order, set(my_stages))
+    if graphs:
+        inflight = max(inflight, len({a.mb for a in order if a is not None and a.stage in set(my_stages)
+                                      and a.op == Op.F}))
     from .models.native import _HEAD_CHUNK
     logit_rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
     logit_b = 4.0 if f32 else 2.0
@@ -389,7 +396,8 @@ class PipelineTrainer:
             self.memory_plan = plan_recompute(cfg, layer_ranges, my_stages, order, mbs, seq_len, self.device,
                                               head_tokens=head_tokens,
                                               head_shards=pp if (self.head_zero and pp > 1) else 1,
-                                              stage_shards=self.mesh.dp if self.dp_zero else 1, dtype=dtype)
+                                              stage_shards=self.mesh.dp if self.dp_zero else 1, dtype=dtype,
+                                              graphs=graphs and self.device.type == "cuda")
             recompute = self.memory_plan["recompute"]
         self.recompute = bool(recompute)
         # ZeRO-1 over DP replicas (MIPIPE_DP_ZERO=0: replicated master / moments, gradient

@@ -210,6 +210,11 @@ def test_recompute_auto_plan():
         dpz32 = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), stage_shards=2,
                                dtype=torch.float32)
         assert rep32["bytes_no_recompute"] - dpz32["bytes_no_recompute"] == pytest.approx(4.0 * nparams)
+        # HIP graphs keep every microbatch's stash in its graph pool: all 8 microbatches of
+        # rank 1's 1F1B order count, not its 3 in flight
+        g = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), graphs=True)
+        assert rep["inflight"] == 3 and g["inflight"] == 8
+        assert g["bytes_no_recompute"] > rep["bytes_no_recompute"]
         assert dpz32["bytes_no_recompute"] > dpz["bytes_no_recompute"]
         h32 = plan_recompute(cfg, l8, [7], o8, 1, 8192, torch.device("cuda", 0), head_tokens=1024, head_shards=8,
                              dtype=torch.float32)
