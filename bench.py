@@ -82,6 +82,8 @@ BASELINE_NOTE = ("no same-config reference number: BASELINE.md only has the refe
 ATTEMPTS = [("auto", 1), ("auto-safe", 1), ("torch", 1), ("torch", 0), ("gloo", 1)]
 # the reference's three schedules (helper:215-220), measured back to back in one call
 SCHEDULES = ("GPipe", "1F1B", "Interleaved1F1B")
+# ... and the ones measured next to them by --schedules all: the zero-bubble ZBH1 too
+ALL_SCHEDULES = SCHEDULES + ("ZBH1",)
 # published L8 H8 rows of the reference (nb:703-708): (schedule, P) -> tok/s
 NB_L8H8 = {("GPipe", 2): 1671.32, ("1F1B", 2): 1649.53, ("Interleaved1F1B", 2): 1796.30,
            ("GPipe", 4): 1675.15, ("1F1B", 4): 1680.10, ("Interleaved1F1B", 4): 1739.43}
@@ -116,7 +118,7 @@ def parse(argv=None):
                          "Interleaved1F1B (engine.pick_schedule; 1F1B at one GPU)")
     ap.add_argument("--schedules", default="all",
                     help="schedules also measured after the headline, each in a fresh child process group: "
-                         "'all' (GPipe,1F1B,Interleaved1F1B), 'none', or a comma list")
+                         "'all' (GPipe,1F1B,Interleaved1F1B,ZBH1), 'none', or a comma list")
     ap.add_argument("--ref-fp32", default="auto", choices=["auto", "0", "1"],
                     help="also time the reference's own config (fp32 L8 H8, batch 32 x 128, m=4, fwd+bwd) through "
                          "the compat API on the native fp32 path, per schedule (auto: with a GPU)")
@@ -158,7 +160,7 @@ def extra_schedules(a) -> list:
     if s.lower() in ("none", "0", ""):
         names = []
     elif s.lower() == "all":
-        names = list(SCHEDULES)
+        names = list(ALL_SCHEDULES)
     else:
         names = [_canon(x) for x in s.split(",") if x.strip()]
     return names
@@ -381,6 +383,9 @@ def supervise(a, argv) -> int:
         if not decision.startswith("go"):
             continue
         _, b, p2p, graphs, att = decision.split()
+        if kind == "headline" and int(att) >= 2 and _canon(a.schedule) == "auto":
+            # a planned schedule that failed twice is not retried: the later attempts run 1F1B
+            child_argv = list(child_argv) + ["--schedule", "1F1B"]
         rc, res, wall = run_child(j, tag, child_argv, p2p, int(graphs), int(att), float(b))
         walls[tag] = round(wall, 1)
         if rank != 0:

@@ -236,11 +236,17 @@ def plan_head_pipeline(cfg: NativeConfig, pp: int, schedule: str, m: int, mbs: i
 
 
 def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
-                  candidates=("GPipe", "1F1B", "Interleaved1F1B"), margin: float = 0.03) -> Tuple[str, Dict[str, float]]:
+                  candidates=("GPipe", "1F1B", "Interleaved1F1B", "ZBH1"),
+                  margin: float = 0.03) -> Tuple[str, Dict[str, float]]:
     """``schedule="auto"``: 1F1B unless another candidate's head-aware plan is more
     efficient by more than ``margin`` (relative) -- the plan's p2p model is an estimate, and
     an interleaved rank sends twice the activations (1F1B at PP = 1, where every schedule is
-    bubble-free and 1F1B keeps one stage per rank).  Returns (name, {name: planned efficiency})."""
+    bubble-free and 1F1B keeps one stage per rank).  ZBH1 (zero-bubble: the input-gradient
+    and weight-gradient halves of each backward scheduled apart) is a candidate: its I / W
+    split costs nothing per GPU (one GPU, 128 sequences: 969K vs 959K tok/s at 4 x 32,
+    931K vs 925K at 8 x 16, profiles/r4_zbh1_vs_1f1b_1gpu.json) and it fills the bubble
+    with W work -- GPT-2 small plans 0.959 vs 0.904 at P = 2.  Returns (name, {name: planned
+    efficiency})."""
     if pp == 1:
         return "1F1B", {}
     eff = {}

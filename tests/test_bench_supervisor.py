@@ -210,7 +210,7 @@ def test_bench_four_ranks_measures_all_three_schedules():
     assert len(lines) == 1
     out = json.loads(lines[0])
     sch = out["schedules"]
-    assert set(sch) == {"GPipe", "1F1B", "Interleaved1F1B"}, sch
+    assert set(sch) == {"GPipe", "1F1B", "Interleaved1F1B", "ZBH1"}, sch
     for name, e in sch.items():
         assert e["tok_s"] > 0 and e["bubble_fraction"] is not None and e["analytic_bubble"] is not None, (name, e)
         assert e["p2p_bytes_per_step"] > 0

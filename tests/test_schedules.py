@@ -313,15 +313,29 @@ def test_microbatch_rate_interpolates_the_measured_table():
 
 
 def test_pick_microbatch_weak_scaling_gpt2_small():
-    """--mbs auto: at P = 4 the bubble saved by 32 microbatches of 16 outweighs their lower
-    kernel rate; at P = 2 it does not (within the 2 % margin) and 32-sequence microbatches
-    stay.  The batch per replica is fixed (128 P sequences)."""
+    """--mbs auto: smaller microbatches shrink the bubble but run each kernel on fewer rows;
+    the larger candidate stays unless the smaller one scores > 2 % better (planned
+    efficiency x measured kernel rate).  The batch per replica is fixed (128 P sequences).
+    With the zero-bubble ZBH1 among the schedule candidates, GPT-2 small keeps
+    32-sequence microbatches and runs ZBH1 at P = 2 / 4."""
     from mipipe.engine import pick_microbatch
     from mipipe.models.native import NativeConfig
     cfg = NativeConfig.by_name("gpt2-small")
-    mbs, m, sc = pick_microbatch(cfg, 4, 1024, 512)
-    assert (mbs, m) == (16, 32) and set(sc) == {32, 16}
-    assert sc[16]["planned_efficiency"] > sc[32]["planned_efficiency"]
-    assert sc[16]["score"] > 1.02 * sc[32]["score"]
-    mbs, m, sc = pick_microbatch(cfg, 2, 1024, 256)
-    assert (mbs, m) == (32, 8)
+    for P in (2, 4):
+        mbs, m, sc = pick_microbatch(cfg, P, 1024, 128 * P)
+        assert set(sc) == {32, 16} and mbs * m == 128 * P
+        assert sc[16]["planned_efficiency"] > sc[32]["planned_efficiency"]      # the smaller bubble
+        if mbs == 32:
+            assert sc[16]["score"] <= 1.02 * sc[32]["score"]
+        else:
+            assert sc[16]["score"] > 1.02 * sc[32]["score"]
+        assert sc[mbs]["schedule"] == "ZBH1", sc
+    # without ZBH1's bubble filling, 16-sequence microbatches win at P = 4 (1F1B 0.92 vs 0.85)
+    import mipipe.engine as E
+    orig = E.pick_schedule
+    try:
+        E.pick_schedule = lambda *a, **k: orig(*a, candidates=("GPipe", "1F1B", "Interleaved1F1B"), **k)
+        mbs, m, sc = pick_microbatch(cfg, 4, 1024, 512)
+        assert (mbs, m) == (16, 32) and sc[16]["score"] > 1.02 * sc[32]["score"]
+    finally:
+        E.pick_schedule = orig
