@@ -10,22 +10,26 @@ N GPUs = N pipeline stages (PP=N, one process per GPU); for N>1 the driver launc
 with torch.distributed.run (if launched without it, this script re-launches itself under
 torch.distributed.run).  Work per GPU is fixed as N grows ("weak" scaling): every GPU
 runs 128 sequences of ``seq`` tokens through all of its layers per step, so the global
-batch is 128 N sequences.  A pipeline (N > 1) splits it into ``microbatches = 4*N`` of
-``mbs = 32`` sequences (1F1B bubble (P-1)/(5P-1)); at P = 8 the global batch is 1M tokens.
+batch is 128 N sequences.  A pipeline (N > 1) splits it into microbatches of 32 or 16
+sequences, planned by rank 0's supervisor (engine.pick_microbatch: planned pipeline
+efficiency x measured per-microbatch kernel rate; ``config.mbs_choice``); at P = 8 the
+global batch is 1M tokens.
 One GPU has no bubble to amortise and runs 2 microbatches of 64 (the two microbatch lanes
 overlap them; profiles/r3_bench_mbs64_ab.txt).  Each timed step is a full training step:
 all microbatch forwards/backwards through the lowered schedule, p2p of activations and
 gradients, grad-norm clip and the fused AdamW update.
 
 One call measures, each in a fresh child process group (so one can never cost another):
-  1. the headline (``value``, ``ms_per_step``, ``config``): ``--schedule`` (1F1B);
-  2. ``schedules``: GPipe, 1F1B and Interleaved1F1B (v=2) on the same model, batch and
+  1. the headline (``value``, ``ms_per_step``, ``config``): ``--schedule`` (auto: the best
+     planned of GPipe / 1F1B / Interleaved1F1B / ZBH1, ``config.schedule_choice``);
+  2. ``schedules``: GPipe, 1F1B, Interleaved1F1B (v=2) and ZBH1 on the same model, batch and
      microbatches -- tok/s, measured + analytic bubble, speedup vs GPipe, planned
      efficiency, head lag, HBM peak, p2p bytes per step (the reference's whole result,
      helper:215-220 / nb:402-433);
   3. ``reference_fp32`` (GPU default): the reference's own config -- fp32 L8 H8 d768, batch
      32 x 128, m = 4, fwd+bwd only -- through the compat API on the native fp32 kernels,
-     per schedule at P = N, next to the published row of BASELINE.md (``x_vs_nb``).
+     per schedule at P = N, next to the published row of BASELINE.md (``x_vs_nb``);
+  4. ``baseline_configs`` (GPU default, N = 4 / 8): BASELINE.json's named configs.
 Extras only start once the headline is in and only if the time left covers them (global
 deadline below); a skipped or failed extra is reported as such.
 
