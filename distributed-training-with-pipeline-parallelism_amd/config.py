@@ -25,7 +25,7 @@ class ModelSection:
 class ParallelSection:
     pp: int = 1
     dp: int = 1
-    schedule: str = "1F1B"              # GPipe | 1F1B | Interleaved1F1B | LoopedBFS | ZBH1
+    schedule: str = "1F1B"              # GPipe | 1F1B | Interleaved1F1B | LoopedBFS | ZBH1 | ZBV | auto (engine.pick_schedule)
     microbatches: Optional[int] = None  # default 2*pp
     v: Optional[int] = None             # virtual stages per rank (interleaved)
     style: str = "loop"                 # stage placement: loop | v

@@ -343,6 +343,10 @@ class PipelineTrainer:
                  split_head: Optional[bool] = None, head_align: Optional[int] = None, graphs: bool = False,
                  adam_eps: float = 1e-8):
         self.cfg = cfg
+        # schedule="auto": the best head-aware plan (pick_schedule; 1F1B at PP = 1)
+        self.schedule_choice = None
+        if str(schedule).lower() == "auto":
+            schedule, self.schedule_choice = pick_schedule(cfg, pp, n_microbatches, mbs, seq_len)
         self.schedule = canonical_name(schedule)
         style = REQUIRED_STYLE.get(self.schedule, style)
         self.style = style

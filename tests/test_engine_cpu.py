@@ -356,3 +356,15 @@ def _four_steps_worker(rank, world):
         x, y = _data(cfg, tr.mesh.dp_rank, step)
         tr.train_step(x, y)
     return {k: v.numpy().copy() for k, v in tr.state_dict().items()}
+
+
+def test_trainer_auto_schedule():
+    """PipelineTrainer(schedule="auto") (train.py's `parallel.schedule: auto`): the best
+    head-aware plan -- 1F1B on one stage; at PP > 1 the same choice as pick_schedule."""
+    from mipipe.engine import PipelineTrainer, pick_schedule
+    from mipipe.models.config import NativeConfig
+    cfg = NativeConfig.by_name("gpt2-tiny", vocab_size=256)
+    tr = PipelineTrainer(cfg, pp=1, schedule="auto", n_microbatches=2, mbs=2, seq_len=16, device="cpu")
+    assert tr.schedule == "1F1B" and tr.schedule_choice == {}
+    name, eff = pick_schedule(NativeConfig.by_name("gpt2-small"), 2, 8, 32, 1024)
+    assert name in eff and eff[name] == max(eff.values()) or (name == "1F1B" and max(eff.values()) < 1.03 * eff["1F1B"])
