@@ -1,0 +1,15 @@
+#!/bin/bash
+# PMC passes over tools/gemm_pmc_probe32k.py (one rocprofv3 run per counter group; each
+# group within the per-block limits: <= 8 SQ, 4 TCC, 4 TCP, 2 TA, 2 TD, 2 GRBM)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/gpmc32
+i=0
+for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INST_LEVEL_VMEM SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "TA_BUSY_avr TA_TA_BUSY_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_TCR_TCP_STALL_CYCLES_sum TCP_TD_TCP_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum" \
+           "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_DRAM_sum SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_RD SQ_INST_CYCLES_VMEM_WR"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-include-regex gemm --output-format csv -d gpurun_out/gpmc32/p$i -o run -- python3 tools/gemm_pmc_probe32k.py > gpurun_out/gpmc32/p$i.log 2>&1 || exit 1
+  find gpurun_out/gpmc32/p$i -name "*counter_collection.csv" -exec cp {} gpurun_out/gpmc32/p$i.csv \;
+done
+echo done
