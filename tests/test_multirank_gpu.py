@@ -41,6 +41,7 @@ def reference8():
 
 
 @pytest.mark.parametrize("n,schedule,graphs,split,dp", [(2, "1F1B", 0, 1, 1), (2, "ZBH1", 1, 1, 1),
+                                                        (4, "ZBH1", 1, 1, 1),
                                                         (4, "1F1B", 1, 1, 1), (4, "GPipe", 0, 0, 1),
                                                         (2, "ZBV", 0, 1, 1), (4, "1F1B", 1, 1, 2),
                                                         (2, "1F1B", 1, 1, 2)])
