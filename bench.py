@@ -344,10 +344,11 @@ def supervise(a, argv) -> int:
     if a.mbs is None and a.microbatches is None and pp > 1 and os.environ.get("MIPIPE_BENCH_MBS", "auto") == "auto":
         plan_path = os.path.join(d, "mbs.plan")
         if rank == 0:
-            mbs_plan = plan_microbatch_child(argv, min(120.0, max(10.0, left() - 300.0)))
+            # (the first `import torch` on a fresh box can take 1-2 minutes)
+            mbs_plan = plan_microbatch_child(argv, min(150.0, max(10.0, left() - 300.0)))
             _publish(plan_path, json.dumps(mbs_plan))
         else:
-            txt = _wait_file(plan_path, 180.0)
+            txt = _wait_file(plan_path, 210.0)
             mbs_plan = json.loads(txt) if txt else None
         if mbs_plan and mbs_plan.get("mbs"):
             argv = list(argv) + ["--mbs", str(mbs_plan["mbs"]), "--microbatches", str(mbs_plan["microbatches"])]
