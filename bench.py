@@ -88,9 +88,30 @@ ATTEMPTS = [("auto", 1), ("auto-safe", 1), ("torch", 1), ("torch", 0), ("gloo", 
 SCHEDULES = ("GPipe", "1F1B", "Interleaved1F1B")
 # ... and the ones measured next to them by --schedules all: the zero-bubble ZBH1 too
 ALL_SCHEDULES = SCHEDULES + ("ZBH1",)
-# published L8 H8 rows of the reference (nb:703-708): (schedule, P) -> tok/s
-NB_L8H8 = {("GPipe", 2): 1671.32, ("1F1B", 2): 1649.53, ("Interleaved1F1B", 2): 1796.30,
-           ("GPipe", 4): 1675.15, ("1F1B", 4): 1680.10, ("Interleaved1F1B", 4): 1739.43}
+# the reference's 9 (L, H) configs (nb:346-349), L8 H8 first; its published rows are
+# mipipe.bench.published (nb:679-732) -- imported lazily: the
+# supervisor itself imports nothing that could touch HIP
+REF_CONFIGS = ((8, 8), (4, 4), (4, 8), (4, 12), (8, 4), (8, 12), (12, 4), (12, 8), (12, 12))
+
+
+def ref_ps(world: int) -> list:
+    """Pipeline sizes of the fp32 reference phase: the P the reference published (2, 4),
+    on rank subsets 0..P-1 of this launch, then P = world -- so an N = 8 record compares
+    P = 2 with the P = 2 rows and P = 4 with the P = 4 rows, never P = 8 with either."""
+    return [p for p in (2, 4) if p < world] + [world]
+
+
+def ref_grid(a, P: int) -> list:
+    """(L, H) configs the fp32 reference child at pipeline size P runs."""
+    if a.ref_args != "8,8,32,128":
+        L, H = (int(x) for x in a.ref_args.split(",")[:2])
+        return [(L, H)]
+    g = a.ref_grid or ("all" if P in (2, 4) else "l8h8")
+    if g == "all":
+        return list(REF_CONFIGS)
+    if g == "l8h8":
+        return [(8, 8)]
+    return [tuple(int(x) for x in item.split(",")) for item in g.split(";") if item.strip()]
 
 
 # BASELINE.json's named multi-GPU configs (configs/*.yaml), measured after everything else
@@ -131,6 +152,10 @@ def parse(argv=None):
                          "allows (auto: on a GPU box only -- Llama-3 8B is not a CPU job)")
     ap.add_argument("--ref-args", default="8,8,32,128",
                     help="reference-config layers,heads,batch,seq (CPU tests shrink it)")
+    ap.add_argument("--ref-grid", default=None,
+                    help="reference (L,H) configs of the fp32 phase: 'l8h8', 'all' (the 9 of nb:346-349) or "
+                         "'L,H;L,H' (default: all at P = 2 / 4, where the reference published, else L8 H8)")
+    ap.add_argument("--ref-p", type=int, default=None, help=argparse.SUPPRESS)
     ap.add_argument("--phase", default="sched", choices=["sched", "ref", "plan"], help=argparse.SUPPRESS)
     ap.add_argument("--mbs", type=int, default=None,
                     help="sequences per microbatch (default: 64 on one GPU; with a pipeline the supervisor "
@@ -233,10 +258,21 @@ def extra_budget(kind: str, left: float, cap: float, head_wall: float, ref_wall=
     the last reference child's; the child is killed at twice that (>= 90 s), and never
     later than 10 s before the global deadline -- so however the extras end, the whole
     run stays inside it."""
-    est = ref_wall if (kind == "ref" and ref_wall) else (60.0 if kind == "ref" else head_wall * 1.25 + 10.0)
+    est = head_wall * 1.25 + 10.0
+    if kind.startswith("ref"):      # "ref:<runs>": one child runs <runs> (L, H, schedule) configs
+        runs = int(kind.split(":", 1)[1]) if ":" in kind else 3
+        # ~3 s per config on a GPU once a child has measured it (20 s for its start-up;
+        # MIPIPE_BENCH_REF_RUN_S: the per-config guess before any child measured one)
+        est = 20.0 + runs * (ref_wall if ref_wall else float(os.environ.get("MIPIPE_BENCH_REF_RUN_S", "3")))
     if kind.startswith("base"):     # "base:<extra seconds>"
         est = head_wall * 1.25 + 10.0 + float(kind.split(":", 1)[1] if ":" in kind else 0.0)
     b = min(cap, left - 10.0)
+    if kind.startswith("ref"):
+        # a reference child truncates its grid to its budget (run_ref): it only needs room
+        # for the first config's three schedules
+        if b < max(MIN_ATTEMPT_S, 20.0 + 3 * (ref_wall if ref_wall else 3.0)):
+            return 0.0, est
+        return min(b, max(2.0 * est, 90.0)), est
     if b < max(MIN_ATTEMPT_S, est):
         return 0.0, est
     return min(b, max(2.0 * est, 90.0)), est
@@ -265,8 +301,11 @@ def plan_phases(a, argv) -> list:
     for s in extra_schedules(a):
         tags.append((f"x_{s}", "sched", list(argv) + ["--schedule", s], s))
     if ref_fp32_on(a):
-        for s in SCHEDULES:
-            tags.append((f"r_{s}", "ref", list(argv) + ["--phase", "ref", "--schedule", s], s))
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        for P in ref_ps(world):
+            # one child per pipeline size runs every (L, H) config x schedule of its grid
+            # (one process group, one set of RCCL communicators), ranks >= P sit it out
+            tags.append((f"r{P}", "ref", list(argv) + ["--phase", "ref", "--ref-p", str(P)], f"P{P}"))
     if (a.base_configs == "1") or (a.base_configs == "auto" and ref_fp32_on(argparse.Namespace(ref_fp32="auto"))):
         world = int(os.environ.get("WORLD_SIZE", "1"))
         for k, (name, extra, _) in enumerate(BASE_CONFIGS.get(world, [])):
@@ -306,9 +345,12 @@ def supervise(a, argv) -> int:
     def left() -> float:
         return deadline - (time.monotonic() - t_start)
 
-    def run_child(j, tag, child_argv, p2p, graphs, attempt, budget):
+    def run_child(j, tag, child_argv, p2p, graphs, attempt, budget, sub_world=None):
         res_path = os.path.join(d, f"{tag}.json")
         env = child_env(os.environ, p2p, attempt, base_port + 1 + j, budget, res_path)
+        if sub_world is not None:
+            # a pipeline on ranks 0..sub_world-1 of this launch (one GPU each, LOCAL_RANK kept)
+            env.update(WORLD_SIZE=str(sub_world), LOCAL_WORLD_SIZE=str(sub_world))
         cmd = [sys.executable, os.path.abspath(__file__)] + child_argv + ["--graphs", str(graphs)]
         t0 = time.monotonic()
         proc = subprocess.Popen(cmd, env=env)
@@ -335,6 +377,10 @@ def supervise(a, argv) -> int:
             with open(res_path) as f:
                 res = json.loads(f.read())
             _publish(done_path, "1")
+        elif rank == 0 and os.path.exists(res_path + ".partial"):
+            with open(res_path + ".partial") as f:
+                res = json.loads(f.read())    # killed at its budget: what it finished
+            res["killed_at_budget_s"] = round(budget)
         return rc, res, time.monotonic() - t0
 
     # --mbs auto (no --mbs / --microbatches given, PP > 1): rank 0 plans the microbatch size
@@ -376,6 +422,8 @@ def supervise(a, argv) -> int:
                 if kind == "base":
                     world = int(os.environ.get("WORLD_SIZE", "1"))
                     kb = f"base:{BASE_CONFIGS[world][int(tag[1:])][2]}"
+                elif kind == "ref":
+                    kb = f"ref:{len(ref_grid(a, int(tag[1:]))) * len(SCHEDULES)}"
                 b, est = extra_budget(kb, left(), cap, head_wall, ref_wall)
                 if b > 0:
                     decision = f"go {b:.0f} {head_mode[0]} {head_mode[1]} {head_mode[2]}"
@@ -391,7 +439,13 @@ def supervise(a, argv) -> int:
         if kind == "headline" and int(att) >= 2 and _canon(a.schedule) == "auto":
             # a planned schedule that failed twice is not retried: the later attempts run 1F1B
             child_argv = list(child_argv) + ["--schedule", "1F1B"]
-        rc, res, wall = run_child(j, tag, child_argv, p2p, int(graphs), int(att), float(b))
+        sub = None
+        if kind == "ref":
+            sub = int(tag[1:])
+            if rank >= sub:
+                continue        # a pipeline on ranks 0..P-1: this rank sits it out
+            sub = sub if sub < int(os.environ.get("WORLD_SIZE", "1")) else None
+        rc, res, wall = run_child(j, tag, child_argv, p2p, int(graphs), int(att), float(b), sub)
         walls[tag] = round(wall, 1)
         if rank != 0:
             continue
@@ -406,7 +460,9 @@ def supervise(a, argv) -> int:
                                  f"({deadline - left():.0f}s of the {deadline:.0f}s deadline used)\n")
         else:
             if kind == "ref":
-                ref_wall = wall * 1.25 + 5
+                # per (L, H, schedule) run of the last reference child, for the next one's estimate
+                n_runs = len(ref_grid(a, int(tag[1:]))) * len(SCHEDULES)
+                ref_wall = (wall * 1.25 + 5) / max(1, n_runs)
             results[tag] = res if res is not None else {"error": f"child exited rc={rc} without a result "
                                                                  f"after {wall:.0f}s"}
     final_path = os.path.join(d, "final")
@@ -468,6 +524,45 @@ def _sched_entry(r: dict) -> dict:
     return out
 
 
+def merge_reference(refs: dict, world: int, a) -> dict:
+    """``reference_fp32``: every measured (L, H, P, schedule) row with its speedup vs GPipe at
+    the same (L, H, P), the published row of the SAME (L, H, P, schedule) where the
+    reference has one (P = 2 / 4: ``nb_row``, ``x_vs_nb``), the per-P summary, and --
+    for compatibility -- ``per_schedule``: L8 H8 at P = N."""
+    rows, status = [], {}
+    for tag, r in sorted(refs.items(), key=lambda kv: int(kv[0][1:])):
+        P = int(tag[1:])
+        if "rows" not in r:
+            status[f"P{P}"] = r           # error / skipped
+            continue
+        status[f"P{P}"] = {"complete": r.get("complete"), "configs": len(r["rows"]) // len(SCHEDULES),
+                           "wall_s": r.get("wall_s")}
+        rows.extend(r["rows"])
+    gp = {(x["L"], x["H"], x["P"]): x["tok_s"] for x in rows if x["schedule"] == "GPipe" and x.get("tok_s")}
+    for x in rows:
+        g = gp.get((x["L"], x["H"], x["P"]))
+        if g:
+            x["speedup_vs_gpipe"] = round(x["tok_s"] / g, 4)
+    summary = {}
+    for P in sorted({x["P"] for x in rows}):
+        xs = [x["x_vs_nb"] for x in rows if x["P"] == P and "x_vs_nb" in x]
+        e = {"rows": sum(1 for x in rows if x["P"] == P)}
+        if xs:
+            xs = sorted(xs)
+            e.update(x_vs_nb_min=xs[0], x_vs_nb_median=xs[len(xs) // 2], x_vs_nb_max=xs[-1], published_rows=len(xs))
+        else:
+            e["published_rows"] = 0
+            e["note"] = "the reference published P = 2 and 4 only (nb:679-732)"
+        summary[f"P{P}"] = e
+    per_schedule = {x["schedule"]: x for x in rows if (x["L"], x["H"], x["P"]) == (8, 8, world)}
+    okr = [x["tok_s"] for x in per_schedule.values() if x.get("tok_s")]
+    return {"config": "reference ModelArgs L x H d768 vocab 10000, batch {2} x seq {3}, m=4 (m=P for one stage "
+                      "per rank at P > 4), fp32, fwd+bwd only, dropout 0.1 (helper:23-55, :98-143, :214); "
+                      "P < N on ranks 0..P-1".format(*a.ref_args.split(",")),
+            "status": status, "summary": summary, "rows": rows, "per_schedule": per_schedule,
+            "tok_s": max(okr, default=None)}
+
+
 def merge_results(headline: dict, results: dict, a) -> dict:
     """The headline's JSON line + ``schedules`` (every measured schedule of the same
     model/config, the headline's own included) + ``reference_fp32``."""
@@ -481,30 +576,9 @@ def merge_results(headline: dict, results: dict, a) -> dict:
     if "GPipe" in ok:
         for k, v in ok.items():
             v["speedup_vs_gpipe"] = round(v["tok_s"] / ok["GPipe"]["tok_s"], 4)
-    refs = {tag[2:]: r for tag, r in results.items() if tag.startswith("r_")}
+    refs = {tag: r for tag, r in results.items() if tag.startswith("r") and tag[1:].isdigit()}
     if refs:
-        rb = {}
-        P = headline["n_gpus"]
-        for s, r in refs.items():
-            if "error" in r or "skipped" in r:
-                rb[s] = r
-                continue
-            e = dict(r)
-            nb_p = P if (s, P) in NB_L8H8 else 2
-            nb = NB_L8H8.get((s, nb_p)) if a.ref_args == "8,8,32,128" else None
-            if nb and e.get("tok_s"):
-                e["nb_row"] = {"tok_s": nb, "P": nb_p, "source": "BASELINE.md Table 1 (nb:703-708), 10-core CPU"}
-                e["x_vs_nb"] = round(e["tok_s"] / nb, 1)
-            rb[s] = e
-        okr = {k: v for k, v in rb.items() if v.get("tok_s")}
-        if "GPipe" in okr:
-            for k, v in okr.items():
-                v["speedup_vs_gpipe"] = round(v["tok_s"] / okr["GPipe"]["tok_s"], 4)
-        out["reference_fp32"] = {
-            "config": "reference ModelArgs L{0} H{1} d768 vocab 10000, batch {2} x seq {3}, m=4, fp32, fwd+bwd only, "
-                      "dropout 0.1 (helper:23-55, :98-143, :214)".format(*a.ref_args.split(",")),
-            "per_schedule": rb,
-            "tok_s": max((v["tok_s"] for v in okr.values()), default=None)}
+        out["reference_fp32"] = merge_reference(refs, headline["n_gpus"], a)
     world = headline.get("n_gpus", 1)
     base = {}
     for tag, r in results.items():
@@ -522,11 +596,15 @@ def merge_results(headline: dict, results: dict, a) -> dict:
 
 
 # ------------------------------------------------------------------------------ benchmark
-def emit(out: dict) -> None:
-    """Rank 0's result: into the supervisor's result file (MIPIPE_BENCH_RESULT), else stdout."""
+def emit(out: dict, partial: bool = False) -> None:
+    """Rank 0's result: into the supervisor's result file (MIPIPE_BENCH_RESULT), else stdout.
+    ``partial``: progress of a child that may still be killed at its budget (the supervisor
+    reads it only if the final result never came; it does not mark the child done)."""
     path = os.environ.get("MIPIPE_BENCH_RESULT")
+    if partial and not path:
+        return
     if path:
-        _publish(path, json.dumps(out))
+        _publish(path + (".partial" if partial else ""), json.dumps(out))
     else:
         print(json.dumps(out), flush=True)
 
@@ -753,61 +831,105 @@ def run(a) -> None:
 def run_ref(a) -> None:
     """The reference's own workload (helper:150-235 with nb:306's batch 32 x seq 128, m = 4,
     fwd+bwd only, no optimizer step) through the compat API on the native path at the
-    reference's precision (fp32 kernels), P = world size, one schedule.  Timing as the
-    reference (wall clock on the last rank over ``--steps`` steps after ``--warmup``) and
-    also max over ranks; plus the measured and analytic bubble."""
+    reference's precision (fp32 kernels), on a pipeline of P = ``--ref-p`` ranks (0..P-1 of
+    the launch), every schedule x every (L, H) config of ``ref_grid`` in ONE process group
+    (one set of RCCL communicators, reused by every schedule).  Timing as the reference
+    (wall clock over ``--steps`` steps after ``--warmup``; L8 H8 with the bench's step
+    counts, the other configs with the reference's own 2 warmup + 5 timed steps, nb:372)
+    and also max over ranks; plus the measured and analytic bubble.  Rank 0 re-publishes
+    the rows after every config, and stops starting new configs when 80 % of the child's
+    time budget is used (``complete`` says whether the whole grid ran)."""
+    import gc
     import torch
     import torch.distributed as dist
     import mipipe  # noqa: F401
     from mipipe.bench.compat import native_reference_schedule, run_train_iterations, stages_per_worker
+    from mipipe.bench.published import published, SOURCE_LINE
     from mipipe.models.ref_transformer import ModelArgs, Transformer, manual_model_split, tokenwise_loss_fn
     from mipipe.parallel.api import get_schedule_class
+    from mipipe.parallel.comm import P2P
     from mipipe.parallel.mesh import init_distributed
     from mipipe.utils.metrics import Watchdog
 
+    t_start = time.monotonic()
     budget = float(os.environ.get("MIPIPE_BENCH_ATTEMPT_S", "0") or 0)
-    wd = Watchdog(max(10.0, budget - 10.0) if budget > 0 else 180.0)
+    wd = Watchdog(max(10.0, budget - 10.0) if budget > 0 else 600.0)
+    rows = []
+    out = {"P": None, "rows": rows, "complete": False}
     with wd.step():
         rank, world, local_rank, device = init_distributed()
-        L, H, B, S = (int(x) for x in a.ref_args.split(","))
-        sched = _canon(a.schedule)
-        m = 4
-        if sched != "Interleaved1F1B" and m < world:
-            m = world      # torch needs m >= stages for one stage per rank (schedules.py:578-583)
-        torch.manual_seed(1234 + rank)
-        args = ModelArgs(n_layers=L, n_heads=H)
-        x = torch.randint(0, args.vocab_size, (B, S), dtype=torch.long, device=device)
-        y = torch.randint(0, args.vocab_size, (B, S), dtype=torch.long, device=device)
+        out["P"] = world
+        _, _, B, S = (int(x) for x in a.ref_args.split(","))
         gpu = device.type == "cuda"
-        if gpu:
-            schedule = native_reference_schedule(args, sched, rank, world, B, S, m, device, precision="fp32")
-            engine = "native fp32 kernels"
-        else:
-            spw = stages_per_worker(sched, L, world)
-            stages = [manual_model_split(Transformer(args), rank + world * i, world * spw, device) for i in range(spw)]
-            cls = get_schedule_class(sched)
-            schedule = cls(stages if spw > 1 or sched == "Interleaved1F1B" else stages[0], n_microbatches=m,
-                           loss_fn=tokenwise_loss_fn(args.vocab_size))
-            engine = "torch CPU (autograd)"
+        p2p = P2P(None, list(range(world)), device) if (gpu and world > 1) else None
+        grid = ref_grid(a, world)
+    for gi, (L, H) in enumerate(grid):
+        # every rank runs the same configs: rank 0 decides (time) and broadcasts
+        go = torch.tensor([1.0 if (budget <= 0 or time.monotonic() - t_start < 0.8 * budget) else 0.0],
+                          dtype=torch.float64, device=device)
         if world > 1:
-            dist.barrier()
-        met = run_train_iterations(schedule, x, y, rank, world, num_iterations=a.steps, warmup=a.warmup,
-                                   device=device)
-        el = torch.tensor([met["elapsed_time"]], dtype=torch.float64, device=device)
-        if world > 1:
-            dist.all_reduce(el, op=dist.ReduceOp.MAX)
-        rt = schedule.runtime
-        last = torch.tensor([met["throughput"] if rank == world - 1 else 0.0], dtype=torch.float64, device=device)
-        if world > 1:
-            dist.all_reduce(last, op=dist.ReduceOp.SUM)
-    out = {"tok_s": round(met["tokens_processed"] / float(el.item()), 1),
-           "tok_s_last_rank_timer": round(float(last.item()), 1),
-           "ms_per_step": round(float(el.item()) / a.steps * 1e3, 3),
-           "steps": a.steps, "warmup": a.warmup, "P": world, "v": rt.v, "microbatches": rt.m,
-           "bubble_fraction": None if met.get("bubble_fraction") is None else round(met["bubble_fraction"], 4),
-           "analytic_bubble": None if met.get("analytic_bubble") is None else round(met["analytic_bubble"], 4),
-           "precision": met.get("precision", "fp32"), "engine": engine,
-           "native_runner": met.get("native_runner"), "lanes": met.get("lanes"), "p2p": rt.p2p.kind}
+            dist.broadcast(go, src=0)
+        if float(go.item()) < 0.5:
+            break
+        steps, warmup = (a.steps, a.warmup) if gi == 0 else (5, 2)
+        for sched in SCHEDULES:
+            with wd.step():
+                m = 4
+                if sched != "Interleaved1F1B" and m < world:
+                    m = world      # torch needs m >= stages for one stage per rank (schedules.py:578-583)
+                torch.manual_seed(1234 + rank)
+                args = ModelArgs(n_layers=L, n_heads=H)
+                x = torch.randint(0, args.vocab_size, (B, S), dtype=torch.long, device=device)
+                y = torch.randint(0, args.vocab_size, (B, S), dtype=torch.long, device=device)
+                if gpu:
+                    schedule = native_reference_schedule(args, sched, rank, world, B, S, m, device,
+                                                         precision="fp32", p2p=p2p)
+                    engine = "native fp32 kernels"
+                else:
+                    spw = stages_per_worker(sched, L, world)
+                    stages = [manual_model_split(Transformer(args), rank + world * i, world * spw, device)
+                              for i in range(spw)]
+                    cls = get_schedule_class(sched)
+                    schedule = cls(stages if spw > 1 or sched == "Interleaved1F1B" else stages[0], n_microbatches=m,
+                                   loss_fn=tokenwise_loss_fn(args.vocab_size))
+                    engine = "torch CPU (autograd)"
+                if world > 1:
+                    dist.barrier()
+                met = run_train_iterations(schedule, x, y, rank, world, num_iterations=steps, warmup=warmup,
+                                           device=device, measure_bubble=not a.no_bubble)
+                el = torch.tensor([met["elapsed_time"]], dtype=torch.float64, device=device)
+                if world > 1:
+                    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+                rt = schedule.runtime
+                last = torch.tensor([met["throughput"] if rank == world - 1 else 0.0], dtype=torch.float64,
+                                    device=device)
+                if world > 1:
+                    dist.all_reduce(last, op=dist.ReduceOp.SUM)
+                row = {"L": L, "H": H, "P": world, "schedule": sched, "v": rt.v, "microbatches": rt.m,
+                       "tok_s": round(met["tokens_processed"] / float(el.item()), 1),
+                       "tok_s_last_rank_timer": round(float(last.item()), 1),
+                       "ms_per_step": round(float(el.item()) / steps * 1e3, 3), "steps": steps, "warmup": warmup,
+                       "bubble_fraction": None if met.get("bubble_fraction") is None else
+                       round(met["bubble_fraction"], 4),
+                       "analytic_bubble": None if met.get("analytic_bubble") is None else
+                       round(met["analytic_bubble"], 4),
+                       "precision": met.get("precision", "fp32"), "engine": engine,
+                       "native_runner": met.get("native_runner"), "lanes": met.get("lanes"), "p2p": rt.p2p.kind}
+                nb = published(L, H, world, sched) if a.ref_args.split(",")[2:] == ["32", "128"] else None
+                if nb:
+                    row["nb_row"] = {"tok_s": nb, "P": world, "source": f"BASELINE.md Table 1 "
+                                                                       f"(nb:{SOURCE_LINE[(L, H, world, sched)]}), "
+                                                                       "10-core CPU"}
+                    row["x_vs_nb"] = round(row["tok_s"] / nb, 1)
+                rows.append(row)
+                if rank == 0:
+                    emit(out, partial=True)   # a budget kill still leaves the runs done so far
+                del schedule, rt
+                gc.collect()
+                if gpu:
+                    torch.cuda.empty_cache()
+    out["complete"] = len(rows) == len(grid) * len(SCHEDULES)
+    out["wall_s"] = round(time.monotonic() - t_start, 1)
     if rank == 0:
         emit(out)
     with wd.step():
@@ -828,7 +950,8 @@ def main():
                "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", "29533"),
                os.path.abspath(__file__)] + argv
         sys.exit(subprocess.call(cmd))
-    if n != world_env and world_env > 1:
+    if n != world_env and world_env > 1 and not (a.phase == "ref" and a.ref_p == world_env):
+        # (a reference child on ranks 0..P-1 of the launch runs with WORLD_SIZE = P)
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world_env}")
     if os.environ.get("MIPIPE_BENCH_CHILD") != "1" and not a.no_supervise:
         # drop a --graphs the supervisor will set per attempt

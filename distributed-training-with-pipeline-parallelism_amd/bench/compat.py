@@ -80,8 +80,11 @@ def run_train_iterations(schedule, x: torch.Tensor, y: torch.Tensor, rank: int, 
     if rt is not None:
         st0 = next(iter(rt.stages.values()))
         arena = getattr(st0, "arena", None)
-        out["precision"] = ("fp32" if arena.dtype == torch.float32 else "bf16") if arena is not None else \
-            str(next(st0.submod.parameters()).dtype).replace("torch.", "")
+        if arena is not None:
+            out["precision"] = "fp32" if arena.dtype == torch.float32 else "bf16"
+        else:   # (a stage the reference's split left without layers has no parameters)
+            p0 = next(iter(st0.submod.parameters()), None)
+            out["precision"] = str(p0.dtype).replace("torch.", "") if p0 is not None else str(x.dtype)
         out["native_runner"] = rt.native_runner is not None
         out["native_reason"] = rt.native_reason
         out["lanes"] = rt.lanes
@@ -115,7 +118,7 @@ def stages_per_worker(schedule_type: str, n_layers: int, world_size: int) -> int
 
 def native_reference_schedule(args: ModelArgs, schedule_type: str, rank: int, world_size: int, batch_size: int,
                               seq_length: int, num_microbatches: int, device, precision: str = "fp32",
-                              lanes: Optional[int] = None):
+                              lanes: Optional[int] = None, p2p=None):
     """The reference's per-rank setup (helper:180-220: interleave rule, loop placement
     ``stage = rank + world*i``, schedule factory) on the native path: build_reference_stage
     per local stage (f32 or bf16 kernels, HIP graphs on GPUs), the schedule class, and --
@@ -129,7 +132,7 @@ def native_reference_schedule(args: ModelArgs, schedule_type: str, rank: int, wo
                                     mbs=batch_size // num_microbatches, seq_len=seq_length) for i in range(spw)]
     cls = get_schedule_class(schedule_type)
     schedule = cls(stages if spw > 1 or schedule_type == "Interleaved1F1B" else stages[0],
-                   n_microbatches=num_microbatches, loss_fn=tokenwise_loss_fn(args.vocab_size))
+                   n_microbatches=num_microbatches, loss_fn=tokenwise_loss_fn(args.vocab_size), p2p=p2p)
     if dev.type == "cuda":
         from ..engine import auto_lanes
         st = stages[0]

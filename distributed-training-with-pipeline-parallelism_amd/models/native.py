@@ -760,14 +760,22 @@ def comm_units(cfg: NativeConfig, seq_len: int = 1024, link_gbps: Optional[float
 
 
 def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 1024,
-                          reference_rule: bool = False, head_on_last: bool = True) -> List[Tuple[int, int]]:
+                          reference_rule: bool = False, head_on_last: bool = True,
+                          ranks: Optional[int] = None) -> List[Tuple[int, int]]:
     """Layer ranges per stage.
 
     ``reference_rule``: ``L // num_stages`` per stage, remainder on the last stage
     (reference helper:70-75).  Otherwise a cost-balanced split: the embedding and the
     LM head (+ loss) are priced in layer-equivalents from their FLOPs and the layers are
     distributed so the max stage cost is minimal (the head of a 50k-vocab GPT-2 costs
-    ~4.5 layers; leaving it out of the balance is what makes naive PP=8 splits slow)."""
+    ~4.5 layers; leaving it out of the balance is what makes naive PP=8 splits slow).
+
+    ``ranks`` (virtual stages, ``num_stages = ranks x v`` in loop placement, stage s on
+    rank s % ranks): what bounds the pipeline is a RANK's summed work, so the one-layer
+    remainders go to the stages of the least-loaded ranks and the split minimises the
+    max rank load first, then the max stage cost, and prefers no empty stage (GPT-2
+    small, P = 4, v = 2: [1,1,1,2,2,2,2,1] -- every rank 3 layers -- instead of
+    [1,1,2,2,2,2,2,0], which leaves one rank 2 and another 4)."""
     L = cfg.n_layers
     if reference_rule or num_stages == 1:
         per = L // num_stages
@@ -776,15 +784,32 @@ def balanced_layer_ranges(cfg: NativeConfig, num_stages: int, seq_len: int = 102
     if not head_on_last:  # distributed head (parallel/headsplit.py): only the final norm stays
         head_cost = 0.1
     P = num_stages
+    multi = ranks is not None and 1 < ranks < P
     best = None
     for k_last in range(0, L + 1):
         rest = L - k_last
         base, extra = divmod(rest, P - 1)
-        # give the remainder to the later non-head stages (stage 0 also holds the embedding)
-        counts = [base + (1 if s >= P - 1 - extra else 0) for s in range(P - 1)] + [k_last]
+        if not multi:
+            # give the remainder to the later non-head stages (stage 0 also holds the embedding)
+            counts = [base + (1 if s >= P - 1 - extra else 0) for s in range(P - 1)] + [k_last]
+        else:
+            counts = [base] * (P - 1) + [k_last]
+            load = [0.0] * ranks
+            for s, c in enumerate(counts):
+                load[s % ranks] += c + (emb_cost if s == 0 else 0.0) + (head_cost if s == P - 1 else 0.0)
+            for _ in range(extra):
+                # the +1 goes to the least-loaded rank's latest stage without one yet
+                cand = [s for s in range(P - 1) if counts[s] == base]
+                s = min(cand, key=lambda t: (load[t % ranks], -t))
+                counts[s] += 1
+                load[s % ranks] += 1
         costs = [c + (emb_cost if s == 0 else 0.0) + (head_cost if s == P - 1 else 0.0)
                  for s, c in enumerate(counts)]
-        key = (round(max(costs), 6), -min(counts[:-1]) if P > 1 else 0)
+        if multi:
+            rload = [sum(costs[s] for s in range(P) if s % ranks == r) for r in range(ranks)]
+            key = (round(max(rload), 6), round(max(costs), 6), -min(counts))
+        else:
+            key = (round(max(costs), 6), -min(counts[:-1]) if P > 1 else 0)
         if best is None or key < best[0]:
             best = (key, counts)
     out, start = [], 0

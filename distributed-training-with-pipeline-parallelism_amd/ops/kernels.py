@@ -1,11 +1,9 @@
 """Op wrappers: GPU -> HIP kernels in ``_C.so``; CPU -> PyTorch f32 reference math."""
 from __future__ import annotations
 
-import contextlib
 import importlib.util
 import math
 import os
-import threading
 from typing import Optional, Tuple
 
 import torch
@@ -542,43 +540,88 @@ def linear_f32(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = Non
     return _LinearF32.apply(x, w, b)
 
 
-# f32_linears: ONE process-wide dispatcher is installed over torch.nn.functional.linear the
-# first time the block is entered (and never removed); it routes to the f32 MFMA GEMM only
-# while the CALLING THREAD is inside an f32_linears() block (a thread-local depth), so
-# other threads and modules outside the block keep ATen, and nested / concurrent blocks
-# never restore a stale function over each other.
-_F32_TLS = threading.local()
-_F32_LOCK = threading.Lock()
-_F32_ORIG = None
+class F32Linear(torch.nn.Linear):
+    """``nn.Linear`` whose f32 GPU forward/backward run on :func:`linear_f32` (other dtypes
+    and CPU: ATen).  Installed by class swap (:func:`use_f32_kernels`): same parameters,
+    same state_dict keys."""
+
+    def forward(self, x):
+        if x.is_cuda and x.dtype == torch.float32 and self.weight.dtype == torch.float32:
+            return _LinearF32.apply(x, self.weight, self.bias)
+        return super().forward(x)
 
 
-def _f32_linear_dispatch(input, weight, bias=None):
-    if (getattr(_F32_TLS, "depth", 0) > 0 and input.is_cuda and input.dtype == torch.float32 and
-            weight.dtype == torch.float32 and (bias is None or bias.dtype == torch.float32)):
-        return _LinearF32.apply(input, weight, bias)
-    return _F32_ORIG(input, weight, bias)
+def _mha_projected(mod: torch.nn.MultiheadAttention, query, key, value, is_causal: bool, linear):
+    """``nn.MultiheadAttention`` forward without attention weights: packed / k-v-shared /
+    separate input projections through ``linear``, SDPA core, output projection."""
+    same_qkv, same_kv = query is key and key is value, key is value
+    if not mod.batch_first:
+        query, key, value = (t.transpose(0, 1) for t in (query, key, value))
+    B, L, E = query.shape
+    H = mod.num_heads
+    w, b = mod.in_proj_weight, mod.in_proj_bias
+
+    def part(lo, hi):
+        return w[lo:hi], (b[lo:hi] if b is not None else None)
+    if same_qkv:
+        q, k, v = linear(query, w, b).chunk(3, dim=-1)
+    elif same_kv:
+        q = linear(query, *part(0, E))
+        k, v = linear(key, *part(E, 3 * E)).chunk(2, dim=-1)
+    else:
+        q = linear(query, *part(0, E))
+        k = linear(key, *part(E, 2 * E))
+        v = linear(value, *part(2 * E, 3 * E))
+
+    def heads(t):
+        return t.reshape(B, t.shape[1], H, E // H).transpose(1, 2)
+    o = torch.nn.functional.scaled_dot_product_attention(
+        heads(q), heads(k), heads(v), dropout_p=mod.dropout if mod.training else 0.0, is_causal=is_causal)
+    o = o.transpose(1, 2).reshape(B, L, E)
+    o = linear(o, mod.out_proj.weight, mod.out_proj.bias)
+    return o.transpose(0, 1) if not mod.batch_first else o
 
 
-@contextlib.contextmanager
-def f32_linears():
-    """Within the block, ``torch.nn.functional.linear`` on f32 GPU tensors called from this
-    thread runs on :func:`linear_f32`: every nn.Linear and every nn.MultiheadAttention
-    projection (torch's multi_head_attention_forward calls the module-level ``linear``) of
-    an f32 module, forward and backward.  Other dtypes / CPU / other threads keep ATen."""
-    global _F32_ORIG
-    if not ext_available():
-        yield
-        return
-    import torch.nn.functional as F
-    with _F32_LOCK:
-        if _F32_ORIG is None:
-            _F32_ORIG = F.linear
-            F.linear = _f32_linear_dispatch
-    _F32_TLS.depth = getattr(_F32_TLS, "depth", 0) + 1
-    try:
-        yield
-    finally:
-        _F32_TLS.depth -= 1
+class F32MultiheadAttention(torch.nn.MultiheadAttention):
+    """``nn.MultiheadAttention`` whose input / output projections run on :func:`linear_f32`
+    and whose core is SDPA -- the path torch's own ``multi_head_attention_forward`` takes
+    with ``need_weights=False`` (what ``nn.TransformerDecoderLayer`` passes, helper:40-44).
+    Anything else (weights requested, masks, separate k/v dims, bias_k, add_zero_attn, CPU,
+    non-f32) runs the stock module."""
+
+    def forward(self, query, key, value, key_padding_mask=None, need_weights=True, attn_mask=None,
+                average_attn_weights=True, is_causal=False):
+        stock = (need_weights or key_padding_mask is not None or attn_mask is not None or not query.is_cuda
+                 or query.dtype != torch.float32 or not self._qkv_same_embed_dim or self.bias_k is not None
+                 or self.add_zero_attn or query.dim() != 3)
+        if stock:
+            return super().forward(query, key, value, key_padding_mask=key_padding_mask, need_weights=need_weights,
+                                   attn_mask=attn_mask, average_attn_weights=average_attn_weights, is_causal=is_causal)
+        return _mha_projected(self, query, key, value, is_causal, _LinearF32.apply), None
+
+
+_F32_SWAP = {torch.nn.Linear: F32Linear, torch.nn.modules.linear.NonDynamicallyQuantizableLinear: F32Linear,
+             torch.nn.MultiheadAttention: F32MultiheadAttention}
+
+
+def use_f32_kernels(module: torch.nn.Module, on: bool = True) -> int:
+    """Route an f32 module's linears and attention projections to the f32 MFMA GEMM by
+    swapping the class of its ``nn.Linear`` / ``nn.MultiheadAttention`` submodules (and back
+    with ``on=False``).  Parameters, buffers and state_dict keys are untouched, and nothing
+    outside ``module`` changes (no global patch of ``torch.nn.functional``).  Returns the
+    number of submodules switched."""
+    n = 0
+    for mod in module.modules():
+        if on:
+            cls = _F32_SWAP.get(type(mod))
+            if cls is not None:
+                mod._mipipe_f32_orig_cls = type(mod)
+                mod.__class__ = cls
+                n += 1
+        elif type(mod) in (F32Linear, F32MultiheadAttention):
+            mod.__class__ = mod.__dict__.pop("_mipipe_f32_orig_cls")
+            n += 1
+    return n
 
 
 # MIPIPE_WGRAD_GROUP=0: every weight-gradient GEMM of a job list in its own launch

@@ -40,8 +40,9 @@ class _PipelineSchedule:
     def __init__(self, stages: Union[StageBase, Sequence[StageBase]], n_microbatches: int,
                  loss_fn: Optional[Callable] = None, scale_grads: bool = True, group=None,
                  pipe_ranks: Optional[Sequence[int]] = None, style: str = "loop", profile: bool = False,
-                 copy_outputs: bool = True):
-        """``copy_outputs`` (default, the reference's semantics): the last rank's ``step()``
+                 copy_outputs: bool = True, p2p: Optional[P2P] = None):
+        """``p2p``: an existing transport over the same group (a sweep building many schedules
+        in one process group reuses one set of RCCL communicators).  ``copy_outputs`` (default, the reference's semantics): the last rank's ``step()``
         returns a fresh tensor, as the dependency's ``torch.cat`` merge does.  False: a
         zero-copy view of the native stage's persistent logits buffer -- valid only until the
         next ``step()``, which rewrites it in place (eager copy or graph replay)."""
@@ -68,7 +69,10 @@ class _PipelineSchedule:
             raise ValueError(f"{self._name} requires n_microbatches ({n_microbatches}) >= num_stages ({num_stages})")
         if self._name == "Interleaved1F1B":
             interleave_params(pp, n_microbatches)
-        p2p = P2P(group, pipe_ranks, stages[0].device)
+        if p2p is None:
+            p2p = P2P(group, pipe_ranks, stages[0].device)
+        else:
+            p2p.reset_channels()
         self._runtime = PipelineRuntime(stages, self._name, n_microbatches, rank, pp, p2p, loss_fn=loss_fn,
                                         scale_grads=scale_grads, style=style, profile=profile)
         self.pipeline_order = self._runtime.orders
@@ -168,8 +172,9 @@ class ScheduleZBVZeroBubble(_PipelineSchedule):
     _name = "ZBV"
 
     def __init__(self, stages, n_microbatches, loss_fn=None, scale_grads=True, group=None, pipe_ranks=None,
-                 style: str = "v", profile: bool = False, copy_outputs: bool = True):
-        super().__init__(stages, n_microbatches, loss_fn, scale_grads, group, pipe_ranks, "v", profile, copy_outputs)
+                 style: str = "v", profile: bool = False, copy_outputs: bool = True, p2p=None):
+        super().__init__(stages, n_microbatches, loss_fn, scale_grads, group, pipe_ranks, "v", profile, copy_outputs,
+                         p2p)
 
 
 _CLASSES = {"GPipe": ScheduleGPipe, "1F1B": Schedule1F1B, "Interleaved1F1B": ScheduleInterleaved1F1B,

@@ -238,6 +238,12 @@ class P2P:
             w.release()
         self._live.clear()
 
+    def reset_channels(self) -> None:
+        """Back to the engine's two direction channels (a transport reused by a new runtime
+        whose program may be proven on both; see use_single_channel)."""
+        if self.engine is not None:
+            self.channels = min(2, int(self.engine.channels))
+
     def use_single_channel(self) -> None:
         """Post both directions on channel 0 (the lowered program's two-channel order was
         not proven deadlock-free, see simulate.check_lowered)."""

@@ -53,7 +53,10 @@ _CAPTURE_STREAMS: Dict[int, torch.cuda.Stream] = {}
 def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any]) -> Any:
     """Capture ``fn()`` into ``g`` without a device-wide synchronisation (module docstring):
     on a per-device capture stream that first waits for the current stream, thread-local
-    capture mode, a private memory pool."""
+    capture mode, a private memory pool.  If ``fn`` raises (an allocation failing inside the
+    capture, say), the capture is ended and discarded and THAT exception propagates -- not
+    the ``hipErrorStreamCaptureUnjoined`` that ending a half-built capture reports when the
+    failure left a forked side stream unjoined."""
     cur = torch.cuda.current_stream()
     idx = cur.device.index if cur.device.index is not None else torch.cuda.current_device()
     cs = _CAPTURE_STREAMS.get(idx)
@@ -64,8 +67,17 @@ def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any]) -> Any:
         g.capture_begin(capture_error_mode="thread_local")
         try:
             out = fn()
-        finally:
-            g.capture_end()
+        except BaseException:
+            try:
+                g.capture_end()     # leaves capture mode; the half-built graph is invalid
+            except Exception:       # noqa: BLE001 - secondary to the error being raised
+                pass
+            try:
+                g.reset()
+            except Exception:       # noqa: BLE001
+                pass
+            raise
+        g.capture_end()
     cur.wait_stream(cs)
     return out
 

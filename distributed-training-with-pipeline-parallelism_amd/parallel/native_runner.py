@@ -37,6 +37,22 @@ def active() -> Optional["TapeRecorder"]:
     return _ACTIVE
 
 
+class paused:
+    """Run a block outside the active recording: its device work and collectives are NOT
+    put on the tape.  For per-step work the runtime issues itself on every step, replayed
+    or not (``StageBase.post_step``): recording it too would run it twice per replay."""
+
+    def __enter__(self):
+        global _ACTIVE
+        self._saved, _ACTIVE = _ACTIVE, None
+        return self
+
+    def __exit__(self, *exc):
+        global _ACTIVE
+        _ACTIVE = self._saved
+        return False
+
+
 class TapeRecorder:
     def __init__(self, device: torch.device):
         from ..ops.kernels import load_ext

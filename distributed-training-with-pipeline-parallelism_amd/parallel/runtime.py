@@ -824,6 +824,8 @@ class PipelineRuntime:
                         self.timer.add(a, ready[0] if ready[0] is not None else t_s, self.timer.mark())
             except Exception:
                 self._report_failure(idx)
+                if hasattr(self.p2p, "release_works"):
+                    self.p2p.release_works()    # no handle outlives a failed step
                 raise
         self._join_lanes(rec)
         if deps is not None:
@@ -835,8 +837,12 @@ class PipelineRuntime:
             w.wait()
         if hasattr(self.p2p, "release_works"):
             self.p2p.release_works()
-        for st in self.stages.values():
-            st.post_step()
+        # post_step (the tied-embedding gradient sum) runs outside the recording: a replayed
+        # step issues it after the tape (_step_native), so recording it would sum twice
+        from .native_runner import paused
+        with paused():
+            for st in self.stages.values():
+                st.post_step()
         if self.profile:
             self.last_timeline, self.last_step_ms = self.timer.finish()
             self.last_timeline_source = "python executor"

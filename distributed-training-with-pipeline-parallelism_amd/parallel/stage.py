@@ -127,10 +127,23 @@ class PipelineStage(StageBase):
         if self.graphs and dist.is_initialized() and dist.get_world_size() > 1 and dist.get_backend() == "nccl":
             self.graphs = False
         self._graph_fns: Dict[int, Callable] = {}
-        # f32 modules on GPU: every linear / attention projection on the f32 MFMA GEMM
-        # (ops.f32_linears); off: ATen (hipBLASLt)
-        self.f32_kernels = False
+        self._f32_kernels = False
         self._orig_forward: Optional[Callable] = None
+
+    @property
+    def f32_kernels(self) -> bool:
+        """f32 modules on GPU: every linear / attention projection of the submodule on the
+        f32 MFMA GEMM (ops.use_f32_kernels swaps the submodules' classes; nothing global is
+        patched); off: ATen (hipBLASLt)."""
+        return self._f32_kernels
+
+    @f32_kernels.setter
+    def f32_kernels(self, on: bool) -> None:
+        on = bool(on)
+        if on != self._f32_kernels:
+            from ..ops.kernels import use_f32_kernels
+            use_f32_kernels(self.submod, on)
+            self._f32_kernels = on
 
     # reference-visible attributes
     @property
@@ -150,23 +163,15 @@ class PipelineStage(StageBase):
                 a = a.detach().requires_grad_(True)
             inputs.append(a)
         inputs = tuple(inputs)
-        with self._kernels_ctx():
-            fwd = self._graphed_fn(mb, inputs) if self.graphs and self.device.type == "cuda" else self.submod
-            with torch.enable_grad():
-                out = _as_tuple(fwd(*inputs))
-            loss = None
-            if self.is_last and loss_fn is not None:
-                loss = loss_fn(out[0] if len(out) == 1 else out, target)
-                self._loss_cache[mb] = loss * loss_scale if loss_scale != 1.0 else loss
+        fwd = self._graphed_fn(mb, inputs) if self.graphs and self.device.type == "cuda" else self.submod
+        with torch.enable_grad():
+            out = _as_tuple(fwd(*inputs))
+        loss = None
+        if self.is_last and loss_fn is not None:
+            loss = loss_fn(out[0] if len(out) == 1 else out, target)
+            self._loss_cache[mb] = loss * loss_scale if loss_scale != 1.0 else loss
         self._fwd_cache[mb] = (inputs, out)
         return tuple(o.detach() for o in out), loss
-
-    def _kernels_ctx(self):
-        if self.f32_kernels and self.device.type == "cuda":
-            from ..ops.kernels import f32_linears
-            return f32_linears()
-        import contextlib
-        return contextlib.nullcontext()
 
     def _graphed_fn(self, mb: int, inputs: Tuple[torch.Tensor, ...]) -> Callable:
         fn = self._graph_fns.get(mb)

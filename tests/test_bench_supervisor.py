@@ -235,39 +235,84 @@ def test_extra_phases_never_push_past_the_deadline():
     for head_wall in (20.0, 60.0, 150.0, 230.0):
         t = head_wall + 1.0                 # headline attempt 0 succeeded
         ref_wall = None
-        for kind in ["sched"] * 2 + ["ref"] * 3:
+        # N = 8: four other schedules, then the reference grid at P = 2, 4 (27 runs each) and 8
+        for kind in ["sched"] * 4 + ["ref:27", "ref:27", "ref:3"]:
             b, est = bench.extra_budget(kind, bench.DEADLINE_S - t, bench.ATTEMPT_CAP_S, head_wall, ref_wall)
             if b <= 0:
                 continue
             assert b <= bench.DEADLINE_S - t - 10.0
             t += b + 5.0                    # hangs to its limit; the kill takes <= 5 s
-            if kind == "ref":
-                ref_wall = b * 1.25 + 5
+            if kind.startswith("ref"):
+                ref_wall = (b * 1.25 + 5) / int(kind.split(":")[1])
         assert t <= 560.0, (head_wall, t)
 
 
 def test_merge_results_reference_block_and_speedups():
     """bench.merge_results: the headline line + every schedule (the headline's own included)
-    with speedup vs GPipe, and the reference fp32 block next to the published row of the
-    same (schedule, P) -- P = 2's row at N = 1, where the reference published none."""
+    with speedup vs GPipe, and the reference fp32 rows, each next to the published row of the
+    SAME (L, H, P, schedule) -- P = 2 / 4 only; P = 1 and P = 8 rows carry none (VERDICT r4:
+    never P = 8 against the P = 2 row)."""
     sys.path.insert(0, ROOT)
     import argparse
     import bench
-    head = {"value": 100.0, "n_gpus": 1, "ms_per_step": 10.0, "bubble_fraction": 0.0, "analytic_bubble": 0.0,
+    head = {"value": 100.0, "n_gpus": 8, "ms_per_step": 10.0, "bubble_fraction": 0.0, "analytic_bubble": 0.0,
             "config": {"schedule": "1F1B", "v": 1, "microbatches": 2}}
+
+    def row(L, H, P, s, t):
+        from mipipe.bench.published import published, SOURCE_LINE
+        r = {"L": L, "H": H, "P": P, "schedule": s, "tok_s": t}
+        nb = published(L, H, P, s)
+        if nb:
+            r["nb_row"] = {"tok_s": nb, "P": P, "source": f"nb:{SOURCE_LINE[(L, H, P, s)]}"}
+            r["x_vs_nb"] = round(t / nb, 1)
+        return r
     res = {"x_GPipe": {"value": 80.0, "config": {"schedule": "GPipe", "v": 1}},
            "x_Interleaved1F1B": {"error": "child exited rc=17 without a result after 50s"},
-           "r_GPipe": {"tok_s": 167132.0, "P": 1}, "r_1F1B": {"tok_s": 184000.0, "P": 1},
-           "r_Interleaved1F1B": {"skipped": "time"}}
+           "r2": {"P": 2, "complete": True, "rows": [row(8, 8, 2, "GPipe", 167132.0), row(8, 8, 2, "1F1B", 164953.0),
+                                                     row(8, 8, 2, "Interleaved1F1B", 179630.0)]},
+           "r4": {"P": 4, "complete": False, "rows": [row(8, 8, 4, "GPipe", 167515.0)]},
+           "r8": {"P": 8, "complete": True, "rows": [row(8, 8, 8, "GPipe", 100.0), row(8, 8, 8, "1F1B", 120.0)]}}
     a = argparse.Namespace(ref_args="8,8,32,128")
     out = bench.merge_results(head, res, a)
     s = out["schedules"]
     assert s["1F1B"]["tok_s"] == 100.0 and s["GPipe"]["speedup_vs_gpipe"] == 1.0
     assert s["1F1B"]["speedup_vs_gpipe"] == 1.25 and "error" in s["Interleaved1F1B"]
     r = out["reference_fp32"]
-    assert r["per_schedule"]["1F1B"]["nb_row"]["tok_s"] == 1649.53 and r["per_schedule"]["1F1B"]["nb_row"]["P"] == 2
-    assert r["per_schedule"]["GPipe"]["x_vs_nb"] == 100.0 and r["tok_s"] == 184000.0
-    assert "skipped" in r["per_schedule"]["Interleaved1F1B"]
-    # a shrunken reference config gets no published row to compare with
-    out2 = bench.merge_results(head, res, argparse.Namespace(ref_args="2,2,8,16"))
-    assert "nb_row" not in out2["reference_fp32"]["per_schedule"]["1F1B"]
+    for x in r["rows"]:
+        assert "nb_row" not in x or x["nb_row"]["P"] == x["P"], x
+        assert ("nb_row" in x) == (x["P"] in (2, 4)), x
+    p2 = {x["schedule"]: x for x in r["rows"] if x["P"] == 2}
+    assert p2["GPipe"]["x_vs_nb"] == 100.0 and p2["1F1B"]["speedup_vs_gpipe"] == round(164953 / 167132, 4)
+    assert r["summary"]["P2"]["published_rows"] == 3 and r["summary"]["P8"]["published_rows"] == 0
+    assert r["status"]["P4"]["complete"] is False and r["status"]["P2"]["configs"] == 1
+    # per_schedule: L8 H8 at P = N (8)
+    assert set(r["per_schedule"]) == {"GPipe", "1F1B"} and r["tok_s"] == 120.0
+    res["r2"] = {"skipped": "time"}
+    assert bench.merge_results(head, res, a)["reference_fp32"]["status"]["P2"] == {"skipped": "time"}
+
+
+def test_bench_eight_ranks_reference_at_published_pipeline_sizes():
+    """an N = 8 call runs the reference's fp32 config at P = 2 and P = 4 on rank
+    subsets (ranks 0..P-1) as well as at P = 8, and every row's published comparison is the
+    row of the same P (here L4 H4, the cheapest published config, on CPU/gloo)."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MIPIPE_BENCH_ATTEMPT_S="240", MASTER_PORT=str(free_port()),
+               MIPIPE_BENCH_REF_RUN_S="40")    # a d768 model on one CPU thread per rank
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1", "--mbs",
+           "1", "--seq", "32", "--vocab", "512", "--model", "gpt2-tiny", "--base-configs", "0", "--schedules", "none",
+           "--ref-fp32", "1", "--ref-grid", "4,4", "--no-bubble"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=540, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    ref = out["reference_fp32"]
+    assert set(ref["status"]) == {"P2", "P4", "P8"}, ref["status"]
+    by_p = {}
+    for x in ref["rows"]:
+        by_p.setdefault(x["P"], set()).add(x["schedule"])
+        assert (x["L"], x["H"]) == (4, 4) and x["tok_s"] > 0
+        if x["P"] in (2, 4):
+            assert x["nb_row"]["P"] == x["P"] and x["x_vs_nb"] > 0, x
+        else:
+            assert "nb_row" not in x
+    assert by_p == {P: {"GPipe", "1F1B", "Interleaved1F1B"} for P in (2, 4, 8)}, by_p

@@ -15,8 +15,8 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(n, *args, port, backend="gloo"):
-    env = dict(os.environ, MIPIPE_DIST_BACKEND=backend, OMP_NUM_THREADS="2")
+def _run(n, *args, port, backend="gloo", extra_env=None):
+    env = dict(os.environ, MIPIPE_DIST_BACKEND=backend, OMP_NUM_THREADS="2", **(extra_env or {}))
     if backend != "gloo":
         env.pop("MIPIPE_DIST_BACKEND")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}", "--master-addr",
@@ -60,6 +60,29 @@ def test_multirank_gpu_matches_single(reference, n, schedule, graphs, split, dp)
     # per-lane stage + head gradients, sends ordered after their lane
     if graphs and schedule in ("1F1B", "GPipe"):
         assert res["lanes"] >= 2, res
+
+
+@pytest.fixture(scope="module")
+def reference_5steps():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return _run(1, "--steps", "5", port=29769)["losses"]
+
+
+@pytest.mark.parametrize("split,env", [(0, {}), (1, {"MIPIPE_HEAD_ZERO": "0"})])
+def test_multirank_gpu_replayed_steps_reduce_once(reference_5steps, split, env):
+    """steps replayed from the native tape must not repeat per-step work the
+    runtime issues itself.  split=0: GPT-2's tied embedding lives on the first and the last
+    stage and its two gradients are summed once per step (post_step, outside the tape; it
+    was also recorded, so every replayed step summed it twice).  split=1 with a replicated
+    head (MIPIPE_HEAD_ZERO=0): the head gradient is all-reduced over the pipeline after the
+    lane merge, so the clip norm must come from the reduced gradient, not the merge's
+    sum of squares.  Five steps: two replayed after the capture and the recording step."""
+    res = _run(2, "--schedule", "1F1B", "--graphs", "1", "--split-head", str(split), "--steps", "5",
+               port=29930 + split, extra_env=env)
+    assert res["native_runner"], res["native_reason"]
+    assert res["lanes"] >= 2, res
+    assert res["losses"] == pytest.approx(reference_5steps, rel=2e-3)
 
 
 @pytest.mark.parametrize("n,graphs,split", [(2, 1, 1), (4, 1, 1), (4, 0, 0)])

@@ -167,3 +167,29 @@ def test_microbatch_lanes_match_single_lane(name, lanes, monkeypatch):
     for a in tr2.optimizer.arenas:
         for extra in a.grad_lanes[1:]:
             assert float(extra.abs().max()) == 0.0     # merged and cleared at the join
+
+
+def test_capture_failure_reraises_the_original_error_and_capture_recovers():
+    """VERDICT r4 #6a: an exception inside a capture (e.g. an allocation failing) must
+    surface as itself, not as the hipErrorStreamCaptureUnjoined that ending the half-built
+    capture reports when the failure left a forked side stream unjoined; the next capture on
+    the same capture stream must work."""
+    from mipipe.parallel.graphs import capture
+    x = torch.ones(4096, device="cuda")
+    side = torch.cuda.Stream()
+    torch.cuda.synchronize()
+
+    def bad():
+        y = x * 2.0
+        side.wait_stream(torch.cuda.current_stream())     # forked into the capture ...
+        with torch.cuda.stream(side):
+            y.add_(1.0)
+        raise ValueError("injected failure inside the capture")   # ... and never joined
+
+    with pytest.raises(ValueError, match="injected failure"):
+        capture(torch.cuda.CUDAGraph(), bad)
+    g = torch.cuda.CUDAGraph()
+    out = capture(g, lambda: x * 3.0)
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.full_like(x, 3.0))

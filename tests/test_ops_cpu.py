@@ -140,24 +140,32 @@ def test_swiglu_rope_embedding_adamw():
     torch.testing.assert_close(pf, p.detach(), atol=1e-6, rtol=1e-6)
 
 
-def test_f32_linears_is_thread_local():
-    """ops.f32_linears() installs one dispatcher over F.linear and routes only the calling
-    thread's f32 GPU linears while inside the block (nested blocks count depth; other
-    threads and CPU tensors keep ATen)."""
-    import threading
+def test_use_f32_kernels_swaps_module_classes_only():
+    """ops.use_f32_kernels() routes the reference layer's linears and attention projections
+    to the f32 GEMM by swapping submodule classes (no global F.linear patch):
+    parameters, state_dict keys and CPU outputs are unchanged, torch.nn.functional is never
+    touched, and switching off restores the stock classes."""
     from mipipe.ops import kernels as K
-    if not K.ext_available():
-        pytest.skip("extension not built")
-    seen = {}
-    with K.f32_linears():
-        seen["main"] = K._F32_TLS.depth
-        t = threading.Thread(target=lambda: seen.__setitem__("other", getattr(K._F32_TLS, "depth", 0)))
-        t.start()
-        t.join()
-        with K.f32_linears():
-            seen["nested"] = K._F32_TLS.depth
-        x, w, b = torch.randn(4, 8), torch.randn(3, 8), torch.randn(3)
-        torch.testing.assert_close(F.linear(x, w, b), x @ w.t() + b)   # CPU: ATen
-    seen["after"] = K._F32_TLS.depth
-    assert seen == {"main": 1, "other": 0, "nested": 2, "after": 0}
-    assert F.linear is K._f32_linear_dispatch   # installed once, never swapped back and forth
+    orig_linear = F.linear
+    torch.manual_seed(0)
+    layer = torch.nn.TransformerDecoderLayer(32, 4, dim_feedforward=64, dropout=0.0, batch_first=True)
+    keys = list(layer.state_dict())
+    x = torch.randn(2, 5, 32)
+    ref = layer(x, x)
+    n = K.use_f32_kernels(layer, True)
+    assert n == 6   # self_attn + out_proj, multihead_attn + out_proj, linear1, linear2
+    assert type(layer.self_attn) is K.F32MultiheadAttention and type(layer.linear1) is K.F32Linear
+    assert list(layer.state_dict()) == keys
+    torch.testing.assert_close(layer(x, x), ref)          # CPU: the stock path
+    # the f32 attention path itself (projections + SDPA; on GPUs the projections are the
+    # f32 GEMM) with ATen linears on CPU, vs the stock module: self, k-v-shared, separate
+    mha = layer.multihead_attn
+    q, kv, v2 = torch.randn(2, 5, 32), torch.randn(2, 7, 32), torch.randn(2, 7, 32)
+    for args in ((q, q, q), (q, kv, kv), (q, kv, v2)):
+        want = torch.nn.MultiheadAttention.forward(mha, *args, need_weights=False)[0]
+        torch.testing.assert_close(K._mha_projected(mha, *args, False, F.linear), want, atol=1e-5, rtol=1e-5)
+    assert K.use_f32_kernels(layer, False) == 6
+    assert type(layer.self_attn) is torch.nn.MultiheadAttention
+    assert type(layer.self_attn.out_proj) is torch.nn.modules.linear.NonDynamicallyQuantizableLinear
+    torch.testing.assert_close(layer(x, x), ref)
+    assert F.linear is orig_linear

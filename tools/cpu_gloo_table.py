@@ -27,30 +27,7 @@ sys.path.insert(0, ROOT)
 REF = "/root/reference/LLMsDistributedTrainingHelper.py"
 
 # published throughput: (L, H, P, schedule) -> tok/s
-PUB = {}
-_rows = """4 4 2 3154.76 3238.24 3278.79
-4 4 4 3606.48 3722.89 3545.62
-4 8 2 3051.49 2995.72 3219.27
-4 8 4 3333.58 3541.49 3409.60
-4 12 2 2899.89 2966.34 3023.31
-4 12 4 3249.43 3323.24 3235.95
-8 4 2 1769.51 1773.75 1895.92
-8 4 4 1928.99 2019.28 2169.55
-8 8 2 1671.32 1649.53 1796.30
-8 8 4 1675.15 1680.10 1739.43
-8 12 2 1371.54 1511.65 1252.73
-8 12 4 1608.81 1714.38 1751.59
-12 4 2 1095.58 1168.28 1228.10
-12 4 4 1259.14 1276.17 1265.39
-12 8 2 1036.03 1097.85 1157.26
-12 8 4 1165.24 1234.93 1173.06
-12 12 2 915.56 986.30 1072.16
-12 12 4 1063.27 1210.86 1147.74"""
-SCHEDS = ("GPipe", "1F1B", "Interleaved1F1B")
-for line in _rows.splitlines():
-    L, H, P, *v = line.split()
-    for s, x in zip(SCHEDS, v):
-        PUB[(int(L), int(H), int(P), s)] = float(x)
+from mipipe.bench.published import PUBLISHED as PUB, SCHEDULES as SCHEDS  # noqa: E402
 
 
 def _ref_worker(rank, world, L, H, sched, B, S, iters, q, port):
