@@ -346,6 +346,8 @@ class WGradOverlap:
                 side = torch.cuda.ExternalStream(ops.load_ext().create_stream(idx, 0),
                                                  device=torch.device("cuda", idx))
             _WGRAD_SIDE[idx] = side
+            from ..parallel.graphs import register_side_stream
+            register_side_stream(side)     # joined back if a capture fails mid-fork
         self.side = side
         self.main = torch.cuda.current_stream(idx)
         if self.side.cuda_stream == self.main.cuda_stream:

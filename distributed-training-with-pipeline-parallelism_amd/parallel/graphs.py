@@ -48,6 +48,35 @@ def _tensors(obj, out: List[torch.Tensor]) -> List[torch.Tensor]:
 
 
 _CAPTURE_STREAMS: Dict[int, torch.cuda.Stream] = {}
+# streams that code running inside a capture may fork off the capture stream (the
+# weight-gradient side stream, models/native.py WGradOverlap): on a failed capture they are
+# joined back before the capture is ended, so ending it succeeds and leaves every stream
+# out of capture mode
+_SIDE_STREAMS: List[torch.cuda.Stream] = []
+
+
+def register_side_stream(s: "torch.cuda.Stream") -> None:
+    if all(x.cuda_stream != s.cuda_stream for x in _SIDE_STREAMS):
+        _SIDE_STREAMS.append(s)
+
+
+def _capturing(s: "torch.cuda.Stream") -> bool:
+    with torch.cuda.stream(s):
+        return torch.cuda.is_current_stream_capturing()
+
+
+def _abort_capture(g: "torch.cuda.CUDAGraph", cs: "torch.cuda.Stream") -> None:
+    """End a capture whose function raised: join every registered side stream still in
+    capture mode (a fork the failure left open) into the capture stream, end the capture
+    (a partial, discarded graph) and drop it.  Secondary errors are swallowed: the caller
+    re-raises the original one."""
+    try:
+        for s in _SIDE_STREAMS:
+            if s.cuda_stream != cs.cuda_stream and _capturing(s):
+                cs.wait_stream(s)
+        g.capture_end()
+    except Exception:       # noqa: BLE001 - secondary to the error being raised
+        pass
 
 
 def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any]) -> Any:
@@ -68,14 +97,7 @@ def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any]) -> Any:
         try:
             out = fn()
         except BaseException:
-            try:
-                g.capture_end()     # leaves capture mode; the half-built graph is invalid
-            except Exception:       # noqa: BLE001 - secondary to the error being raised
-                pass
-            try:
-                g.reset()
-            except Exception:       # noqa: BLE001
-                pass
+            _abort_capture(g, cs)
             raise
         g.capture_end()
     cur.wait_stream(cs)

@@ -174,9 +174,10 @@ def test_capture_failure_reraises_the_original_error_and_capture_recovers():
     surface as itself, not as the hipErrorStreamCaptureUnjoined that ending the half-built
     capture reports when the failure left a forked side stream unjoined; the next capture on
     the same capture stream must work."""
-    from mipipe.parallel.graphs import capture
+    from mipipe.parallel.graphs import capture, register_side_stream
     x = torch.ones(4096, device="cuda")
     side = torch.cuda.Stream()
+    register_side_stream(side)   # as WGradOverlap registers its stream
     torch.cuda.synchronize()
 
     def bad():
@@ -188,6 +189,9 @@ def test_capture_failure_reraises_the_original_error_and_capture_recovers():
 
     with pytest.raises(ValueError, match="injected failure"):
         capture(torch.cuda.CUDAGraph(), bad)
+    assert not torch.cuda.is_current_stream_capturing()
+    with torch.cuda.stream(side):
+        assert not torch.cuda.is_current_stream_capturing()
     g = torch.cuda.CUDAGraph()
     out = capture(g, lambda: x * 3.0)
     g.replay()
