@@ -70,6 +70,7 @@ int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void
              int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, float* colsum, float p_drop,
              uint64_t seed, hipStream_t st);
 int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg, int* split_out);
+int64_t mp_gemm2_ws_floats(int cfg, int split, int M, int N);
 int mp_gemm2_has_probe_engines();
 int mp_gemm_tt_grouped(int n, const void* const* A, const void* const* B, float* const* C, const int* M, const int* N,
                        const int* K, const int64_t* lda, const int64_t* ldb, const int64_t* ldc, float alpha,
@@ -402,10 +403,14 @@ int64_t gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<t
                                       colsum->numel() >= N),
               "gemm2: colsum must be a contiguous f32 [N] tensor");
   // split-K slabs (plain stores + one reduce pass instead of f32 atomics)
+  // split-K slabs (plain stores + one reduce pass instead of f32 atomics), or the stream-K
+  // engine's flags + partial tiles: from the caching allocator on the current stream (graph
+  // captures take it from their private pool), so concurrent streams never share one
   int split = 1;
-  mp_gemm2_plan(M, N, K, transA, transB, accum, (int)force_cfg, &split);
+  const int cfg = mp_gemm2_plan(M, N, K, transA, transB, accum, (int)force_cfg, &split);
   torch::Tensor ws;
-  if (split > 1) ws = torch::empty({(int64_t)split * M * N}, C.options().dtype(torch::kFloat32));
+  const int64_t ws_n = mp_gemm2_ws_floats(cfg, split, M, N);
+  if (ws_n > 0) ws = torch::empty({ws_n}, C.options().dtype(torch::kFloat32));
   const int rc = mp_gemm2(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual),
                           mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),
                           residual.has_value() ? residual->stride(0) : 0, aux.has_value() ? aux->stride(0) : 0,
@@ -659,5 +664,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("result"), pybind11::arg("waiter") = 0);
   m.def("probe_set", &probe_set, pybind11::arg("flag"), pybind11::arg("value"), pybind11::arg("setter") = 0);
   m.def("probe_clock_khz", []() { return mp_probe_clock_khz(); });
+  m.def("gemm2_plan", [](int64_t M, int64_t N, int64_t K, bool transA, bool transB, bool accum, int64_t force_cfg) {
+    int split = 1;
+    const int cfg = mp_gemm2_plan((int)M, (int)N, (int)K, transA, transB, accum, (int)force_cfg, &split);
+    return std::make_tuple(cfg, split);
+  }, "engine config + split-K factor the v2 GEMM picks (14: stream-K gemm7)");
   m.def("gemm2_has_probe_engines", []() { return mp_gemm2_has_probe_engines() != 0; });
 }

@@ -1123,6 +1123,319 @@ static int launch6(const void* A, const void* B, void* C, const void* bias, cons
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------------------
+// gemm7: stream-K 256x256 NT GEMM on gemm3's 16x16x32 ping-pong main loop, for grids that
+// are not whole rounds of 256 CUs (a pipeline rank's 8K-32K-token microbatches: N = 768 is
+// 96-384 tiles = 0.4-1.5 rounds, profiles/r5_*gemm*).
+//
+// One persistent workgroup per CU (G = gridDim.x).  Tiles [0, dp) are data-parallel, dp a
+// multiple of G: workgroup b runs tiles b, b + G, ...  The remaining sk tiles are split
+// into 8 XCD groups (consecutive tile ids, so a group's A panels stay in its L2), and a
+// group's K iterations (sk_x tiles x K/64) are cut into q = G/8 equal contiguous ranges,
+// one per workgroup of that XCD in dispatch order (b = x, x + 8, x + 16, ...; the
+// dispatcher places block b on XCD b % 8).  A tile cut between workgroups is OWNED by the
+// one holding its last K iteration; the others (lower in dispatch order) are contributors,
+// and a workgroup contributes to at most one tile -- the last of its range.  Order inside a
+// workgroup: the contributed segment FIRST (its f32 partial goes to the workgroup's slot
+// and a flag is raised), then its own whole tiles, then the tile whose head lower
+// workgroups computed, LAST: by then those partials are long published.  A workgroup
+// waits only for workgroups dispatched before it, which hold a CU or are done, so the
+// protocol cannot deadlock even when other kernels occupy CUs (microbatch lanes).
+//
+// Hand-off (cdna guide §6 Guideline 16, R1): partial stored with sc1 (write-through)
+// 16-byte buffer stores in register order (thread-linear, coalesced), every wave drains
+// vmcnt, workgroup barrier, one agent-scope flag store; the owner's thread 0 polls the
+// flag (bounded: a lost hand-off sets an error word instead of hanging), barrier, and every
+// wave reads the partial with sc1 buffer loads (no L1 copy can be stale).  The flags are
+// the first 1088 B of the workspace, zeroed by a memset node before every launch.
+// ---------------------------------------------------------------------------------------
+constexpr int SK_SLOT = 256 * 256;          // floats per partial tile
+constexpr int SK_FLAGS = 272;               // flag words + error word (first 1088 B of the workspace)
+constexpr int SK_ERR = 256;                 // index of the error word
+constexpr int SK_MAX_G = 256;
+
+__device__ __forceinline__ void g7_mainloop(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, int M, int N,
+                                            int64_t lda, int64_t ldb, int m0, int n0, int kt0, int nk, char* smem,
+                                            f32x4 (&acc)[8][4]) {
+  constexpr int HALF = 128 * 128;
+  constexpr int BUF = 4 * HALF;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / 4, wc = wave % 4;
+  const int lr = lane >> 3;
+  const int lc = (lane & 7) ^ swzq(8 * (wave & 1) + lr);
+  const bf16_t* pa[2];
+  const bf16_t* pb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    int ra = m0 + 128 * j + 8 * wave + lr;
+    ra = ra < M ? ra : M - 1;
+    int rb = n0 + 64 * ((wave >> 2) + 2 * j) + 8 * (wave & 3) + lr;
+    rb = rb < N ? rb : N - 1;
+    pa[j] = A + (int64_t)ra * lda + (int64_t)kt0 * BK + lc * 8;
+    pb[j] = B + (int64_t)rb * ldb + (int64_t)kt0 * BK + lc * 8;
+  }
+  const bool a1_ok0 = m0 + 64 + 8 * wave + lr < M, a1_ok1 = m0 + 192 + 8 * wave + lr < M;
+  const bool b1_ok0 = n0 + 64 * (wave >> 2) + 32 + 8 * (wave & 3) + lr < N;
+  const bool b1_ok1 = n0 + 64 * ((wave >> 2) + 2) + 32 + 8 * (wave & 3) + lr < N;
+  const int64_t a1_off0 = a1_ok0 ? 64 * lda : 0, a1_off1 = a1_ok1 ? 64 * lda : 0;
+  const int64_t b1_off0 = b1_ok0 ? 32 * ldb : 0, b1_off1 = b1_ok1 ? 32 * ldb : 0;
+  auto issue = [&](int h, int kt) {
+    char* img = smem + (kt & 1) * BUF + (h == 0 ? 0 : h == 3 ? HALF : h == 1 ? 2 * HALF : 3 * HALF);
+    const int64_t dk = (int64_t)kt * BK;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16_t* src;
+      if (h == 0) src = pa[j] + dk;
+      else if (h == 3) src = pa[j] + dk + (j ? a1_off1 : a1_off0);
+      else if (h == 1) src = pb[j] + dk;
+      else src = pb[j] + dk + (j ? b1_off1 : b1_off0);
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(img + (wave + 8 * j) * 1024), 16, 0,
+                                       0);
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{};
+  issue(0, 0);
+  issue(1, 0);
+  issue(2, 0);
+  issue(3, 0);
+  if (nk > 1) {
+    issue(0, 1);
+    issue(1, 1);
+    wait_vmcnt<8>();
+  } else {
+    wait_vmcnt<4>();
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (wr == 1) __builtin_amdgcn_s_barrier();  // stagger the wave rows by one barrier
+  asm volatile("" ::: "memory");
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  const int q = lane >> 4;
+  const int rA = wr * 64 + (lane & 15);
+  const int rB = wc * 32 + (lane & 15);
+  auto fq = [&](const char* img, int row, int st) -> bf16x8 {
+    return *reinterpret_cast<const bf16x8*>(img + row * 128 + 16 * ((4 * st + q) ^ swzq(row)));
+  };
+#define G7_MFMA(R0, BF, C0)                                                              \
+  __builtin_amdgcn_sched_barrier(0);                                                     \
+  __builtin_amdgcn_s_setprio(1);                                                         \
+  _Pragma("unroll") for (int s_ = 0; s_ < 2; ++s_)                                       \
+  _Pragma("unroll") for (int i_ = 0; i_ < 4; ++i_)                                       \
+  _Pragma("unroll") for (int j_ = 0; j_ < 2; ++j_)                                       \
+    acc[R0 + i_][C0 + j_] = mfma16(af[i_][s_], BF[j_][s_], acc[R0 + i_][C0 + j_]);       \
+  __builtin_amdgcn_s_setprio(0);                                                         \
+  __builtin_amdgcn_sched_barrier(0);
+#define G7_BAR()                          \
+  asm volatile("" ::: "memory");          \
+  __builtin_amdgcn_s_barrier();           \
+  asm volatile("" ::: "memory");
+  for (int t = 0; t < nk; ++t) {
+    const char* buf = smem + (t & 1) * BUF;
+    const bool steady = t + 2 < nk;
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][s_] = fq(buf, rA + 16 * i, s_);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b0[j][s_] = fq(buf + 2 * HALF, rB + 16 * j, s_);
+    }
+    if (t + 1 < nk) issue(2, t + 1);
+    if (steady) wait_vmcnt<8>(); else wait_vmcnt<0>();
+    G7_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G7_MFMA(0, b0, 0);
+    G7_BAR();
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b1[j][s_] = fq(buf + 3 * HALF, rB + 16 * j, s_);
+    if (t + 1 < nk) issue(3, t + 1);
+    if (steady) wait_vmcnt<8>(); else wait_vmcnt<0>();
+    G7_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G7_MFMA(0, b1, 2);
+    G7_BAR();
+#pragma unroll
+    for (int s_ = 0; s_ < 2; ++s_)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i][s_] = fq(buf + HALF, rA + 16 * i, s_);
+    if (steady) issue(0, t + 2);
+    G7_BAR();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G7_MFMA(4, b0, 0);
+    G7_BAR();
+    if (steady) {
+      issue(1, t + 2);
+      wait_vmcnt<8>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    G7_BAR();
+    G7_MFMA(4, b1, 2);
+    G7_BAR();
+  }
+#undef G7_MFMA
+#undef G7_BAR
+  if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
+  __syncthreads();
+}
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+
+// a contributor's partial tile -> its slot (sc1, register order), then its flag
+__device__ __forceinline__ void g7_publish(const f32x4 (&acc)[8][4], float* slot, unsigned* flag) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(slot, 0, SK_SLOT * 4, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), r, (int)threadIdx.x * 16,
+                                             (i * 4 + j) * NT * 16, 16 /* sc1 */);   // lane part in voffset
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its stores
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the owner adds a contributor's partial once its flag is up (bounded poll)
+__device__ __forceinline__ void g7_absorb(f32x4 (&acc)[8][4], const float* slot, unsigned* flag, unsigned* err) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > (1u << 24)) {     // ~0.5 s: a lost hand-off ends the kernel, flagged
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the poll
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(slot), 0, SK_SLOT * 4,
+                                                                     0x00020000);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, (i * 4 + j) * NT * 16,
+                                                              16 /* sc1 */);
+      acc[i][j] += __builtin_bit_cast(f32x4, v);
+    }
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm7_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, bf16_t* __restrict__ C,
+             const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+             float* __restrict__ colsum, float* __restrict__ ws, int M, int N, int K, int64_t lda, int64_t ldb,
+             int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop, uint64_t seed, int dp_tiles,
+             int sk_tiles) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int G = gridDim.x, b = blockIdx.x;
+  const int gn = (N + 255) / 256;
+  const int kt = K / BK;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave / 4, wn = (wave % 4) * 64;
+  unsigned* flags = reinterpret_cast<unsigned*>(ws);
+  float* part = ws + SK_FLAGS;
+  f32x4 acc[8][4];
+  auto finish = [&](int m0, int n0) {
+    epilogue<256, 256, 2, 4, EPI, false>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, C, bias, R, AUX, colsum,
+                                         M, N, ldc, ldr, ldx, alpha, 1, p_drop, seed);
+  };
+  // data-parallel tiles (whole rounds): each XCD walks a contiguous block of tile rows
+  for (int t = b; t < dp_tiles; t += G) {
+    const int tile = xcd_remap(t, dp_tiles);
+    const int m0 = (tile / gn) * 256, n0 = (tile % gn) * 256;
+    g7_mainloop(A, B, M, N, lda, ldb, m0, n0, 0, kt, smem, acc);
+    finish(m0, n0);
+  }
+  if (sk_tiles <= 0) return;
+  // stream-K tiles: XCD group x = b % 8 owns tiles [t0, t1) and splits their iterations
+  const int x = b & 7, q = G >> 3, L = b >> 3;
+  const int t0 = dp_tiles + (int)((int64_t)x * sk_tiles / 8), t1 = dp_tiles + (int)((int64_t)(x + 1) * sk_tiles / 8);
+  const int64_t iters = (int64_t)(t1 - t0) * kt;
+  auto lo_of = [&](int l) { return (int)(iters * l / q); };   // first iteration of workgroup l
+  const int s = lo_of(L), e = lo_of(L + 1);
+  if (s >= e) return;
+  const int tf = s / kt, tl = (e - 1) / kt;    // group-relative first / last tile
+  int hi = tl;
+  if (e % kt != 0) {
+    // contributor of tile tl: its head segment goes to this workgroup's slot
+    const int k0 = (s > tl * kt ? s : tl * kt) - tl * kt;
+    const int tile = t0 + tl;
+    g7_mainloop(A, B, M, N, lda, ldb, (tile / gn) * 256, (tile % gn) * 256, k0, e - tl * kt - k0, smem, acc);
+    g7_publish(acc, part + (int64_t)b * SK_SLOT, flags + b);
+    hi = tl - 1;
+  }
+  // own tiles, the one whose head lower workgroups computed last
+  for (int tr = hi; tr >= tf; --tr) {
+    const int k0 = (s > tr * kt ? s : tr * kt) - tr * kt;
+    const int tile = t0 + tr;
+    const int m0 = (tile / gn) * 256, n0 = (tile % gn) * 256;
+    g7_mainloop(A, B, M, N, lda, ldb, m0, n0, k0, kt - k0, smem, acc);
+    if (k0 > 0) {
+      for (int l = L - 1; l >= 0; --l) {
+        if (lo_of(l) == lo_of(l + 1)) continue;    // an empty range published nothing
+        const int bl = x + 8 * l;
+        g7_absorb(acc, part + (int64_t)bl * SK_SLOT, flags + bl, flags + SK_ERR);
+        if (lo_of(l) <= tr * kt) break;
+      }
+    }
+    finish(m0, n0);
+  }
+}
+
+// plan of the stream-K engine: 0 if it should not be used for this grid, else the grid
+// size G (dp / sk tile counts out)
+static int plan7(int M, int N, int K, int* dp_out, int* sk_out) {
+  const int G = SK_MAX_G;
+  const int T = ((M + 255) / 256) * ((N + 255) / 256);
+  const int kt = K / BK;
+  if (T < 64 || T % G == 0 || kt < 4) return 0;
+  int sk = T < G ? T : T % G + G, dp = T - sk;
+  // modelled k-iteration units: a tile costs kt + 3 (prologue fill, C write); the
+  // stream-K part costs its even share of iterations + 3 + 4 for the partial hand-off
+  const float plain = (float)((T + G - 1) / G) * (kt + 3);
+  const float skt = (float)(dp / G) * (kt + 3) + (float)(((int64_t)sk * kt + G - 1) / G) + 7.f;
+  if (skt > 0.97f * plain) return 0;
+  *dp_out = dp;
+  *sk_out = sk;
+  return G;
+}
+
+template <int EPI>
+static int launch7(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* colsum,
+                   float* ws, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx,
+                   float alpha, float p_drop, uint64_t seed, hipStream_t st) {
+  int dp = 0, sk = 0;
+  const int G = plan7(M, N, K, &dp, &sk);
+  if (G == 0 || ws == nullptr) return -1;
+  constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
+  constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
+  constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
+  auto kern = gemm7_kernel<EPI>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  // the flag words: zeroed before every launch (a memset node under graph capture)
+  hipError_t e = hipMemsetAsync(ws, 0, SK_FLAGS * sizeof(unsigned), st);
+  if (e != hipSuccess) return (int)e;
+  kern<<<dim3(G), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, (const bf16_t*)bias,
+                                 (const bf16_t*)R, (bf16_t*)X, colsum, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha,
+                                 p_drop, seed, dp, sk);
+  return (int)hipGetLastError();
+}
+
 // gemm4 / gemm5: probe engines with recorded null results (profiles/r2_probes.md), built only
 // into the A/B variant (tools/build_ext.py --variant probes -D MP_PROBE_ENGINES), not _C.so.
 #ifdef MP_PROBE_ENGINES
@@ -1957,6 +2270,13 @@ extern "C" int mp_gemm2_has_probe_engines() {
 #endif
 }
 
+// f32 workspace elements the planned engine needs (split-K slabs, or the stream-K flags +
+// partial-tile slots)
+extern "C" int64_t mp_gemm2_ws_floats(int cfg, int split, int M, int N) {
+  if (cfg == 14) return (int64_t)SK_FLAGS + (int64_t)SK_MAX_G * SK_SLOT;
+  return split > 1 ? (int64_t)split * M * N : 0;
+}
+
 extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg,
                              int* split_out) {
   int split = 1;
@@ -2058,6 +2378,19 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
     }
   }
   if (use5 && cfg == 5 && split == 1 && !c_f32_accum && force_cfg < 0) cfg = 8;
+  // the stream-K engine (gemm7) where the 256x256 grid is not whole rounds of 256 CUs
+  // (MIPIPE_GEMM_SK=0 disables; force_cfg 14 selects it wherever plan7 accepts the grid)
+  static const bool use_sk = [] { const char* e = getenv("MIPIPE_GEMM_SK"); return !(e && e[0] == '0'); }();
+  // replaces the ping-pong engine's partial rounds and the bf16-output split-K slabs (f32
+  // slab round trip through HBM + a reduce pass) of the gemm2 tiles alike
+  if (!transA && !transB && !c_f32_accum && (force_cfg == 14 || (use_sk && force_cfg < 0 && cfg != 10 &&
+                                                                 cfg != 11 && cfg != 12 && cfg != 8))) {
+    int dp = 0, sk = 0;
+    if (plan7(M, N, K, &dp, &sk) > 0) {
+      cfg = 14;
+      split = 1;
+    }
+  }
   *split_out = split;
   return cfg;
 }
@@ -2072,6 +2405,16 @@ extern "C" int mp_gemm2(const void* A, const void* B, void* C, const void* bias,
   if (K % BK != 0 || N % 8 != 0 || M % 8 != 0) return -1;
   int split = 1;
   const int cfg = mp_gemm2_plan(M, N, K, transA, transB, c_f32_accum, force_cfg, &split);
+  if (cfg == 14) {
+    if (ws == nullptr) return -1;
+    switch (epilogue) {
+#define MP_G7(E_) case E_: return launch7<E_>(A, B, C, bias, residual, aux, colsum, ws, M, N, K, lda, ldb, ldc, ld_res, ld_aux, alpha, p_drop, seed, st);
+      MP_G7(EPI_NONE) MP_G7(EPI_BIAS) MP_G7(EPI_BIAS_GELU) MP_G7(EPI_BIAS_RELU) MP_G7(EPI_BIAS_RES) MP_G7(EPI_RES)
+      MP_G7(EPI_DGELU) MP_G7(EPI_DRELU)
+#undef MP_G7
+      default: return -2;
+    }
+  }
   if (colsum != nullptr) {
     // fused output column sums: bf16 outputs, one pass (no split-K); -3 tells the caller
     // to sum separately

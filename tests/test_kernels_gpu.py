@@ -435,6 +435,52 @@ def test_gemm2_configs(cfg, M, N, K, epi):
 
 
 @needs_probe_engines
+@pytest.mark.parametrize("M,N,K,epi", [(8192, 768, 768, "bias"), (4000, 1000, 640, "none"), (9000, 2304, 768, "bias_gelu"),
+                                       (24576, 768, 3072, "res"), (8192, 768, 2304, "dgelu"),
+                                       (16384, 2304, 768, "colsum")])
+def test_gemm7_stream_k(M, N, K, epi):
+    """gemm7 (stream-K over 256 persistent workgroups, XCD-grouped K ranges, sc1 partial
+    hand-off): grids of 64-324 tiles incl. ragged M / N edges, every fused epilogue class,
+    the fused column sums; also bit-for-bit stable across repeated launches (each tile's
+    partials are summed in a fixed order)."""
+    from mipipe.ops import kernels as _k
+    e = _k.load_ext()
+    assert e.gemm2_plan(M, N, K, False, False, False, -1)[0] == 14, "planner should pick stream-K here"
+    torch.manual_seed(0)
+    x, w, b, r = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1), rnd(M, N)
+    xg, wg, bg, rg = (t.to(DEV) for t in (x, w, b, r))
+    y = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    aux = rnd(M, N).to(DEV)
+    epi_id = dict(none=0, bias=1, bias_gelu=2, res=5, dgelu=6, colsum=0)[epi]
+    cs = torch.zeros(N, device=DEV) if epi == "colsum" else None
+    run = lambda out: _k._gemm(xg, wg, out, bias=bg if "bias" in epi else None,  # noqa: E731
+                               residual=rg if epi == "res" else None, aux=aux if "gelu" in epi else None,
+                               epi=epi_id, colsum=cs)
+    run(y)
+    ref = x.float() @ w.float().t()
+    if "bias" in epi:
+        ref = ref + b.float()
+    if epi == "bias_gelu":
+        close(aux, ref.to(torch.bfloat16))
+        ref = torch.nn.functional.gelu(ref.to(torch.bfloat16).float(), approximate="tanh")
+    if epi == "res":
+        ref = ref + r.float()
+    if epi == "dgelu":
+        a = aux.float().cpu()
+        k0, k1 = 0.7978845608028654, 0.044715
+        t = torch.tanh(k0 * (a + k1 * a ** 3))
+        ref = ref * (0.5 * (1 + t) + 0.5 * a * (1 - t * t) * k0 * (1 + 3 * k1 * a * a))
+    close(y, ref)
+    if cs is not None:
+        torch.testing.assert_close(cs.cpu(), y.float().sum(0).cpu(), rtol=2e-2, atol=2e-1 * M ** 0.5 * 1e-1)
+    if epi in ("none", "bias", "res"):
+        y2 = torch.empty_like(y)
+        for _ in range(3):
+            run(y2)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y2)
+
+
 @pytest.mark.parametrize("cfg", [7, 108, 103])
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (1000, 776, 512), (520, 264, 64), (1536, 1280, 128),
                                    (2048, 512, 1344)])

@@ -169,3 +169,22 @@ def test_use_f32_kernels_swaps_module_classes_only():
     assert type(layer.self_attn.out_proj) is torch.nn.modules.linear.NonDynamicallyQuantizableLinear
     torch.testing.assert_close(layer(x, x), ref)
     assert F.linear is orig_linear
+
+
+def test_gemm_planner_picks_stream_k_only_for_partial_rounds():
+    """gemm2.hip mp_gemm2_plan (host code, runs without a GPU): the stream-K engine (cfg 14)
+    for NT grids that are not whole rounds of 256 CUs -- a pipeline rank's 8K-32K-token
+    microbatches -- and the ping-pong engine (5) for whole rounds (64K tokens, N = 768:
+    768 tiles = 3 rounds); never for dW (TT, f32 accumulate) or short-token grids."""
+    from mipipe.ops import kernels as K
+    e = K.load_ext()
+    if e is None or not hasattr(e, "gemm2_plan"):
+        pytest.skip("extension not built")
+    plan = lambda M, N, Kd, ta=False, tb=False, acc=False: e.gemm2_plan(M, N, Kd, ta, tb, acc, -1)[0]  # noqa: E731
+    for M, N, Kd in ((8192, 768, 768), (8192, 768, 3072), (32768, 768, 3072), (32768, 768, 2304),
+                     (16384, 2304, 768), (32768, 2304, 768)):
+        assert plan(M, N, Kd) == 14, (M, N, Kd)
+    for M, N, Kd in ((65536, 768, 768), (65536, 768, 3072), (65536, 3072, 768)):
+        assert plan(M, N, Kd) != 14, (M, N, Kd)
+    assert plan(2048, 768, 768) != 14                       # 24 tiles: the small-tile engine
+    assert plan(768, 3072, 32768, True, True, True) != 14    # dW
