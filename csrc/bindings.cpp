@@ -70,7 +70,7 @@ int mp_gemm2(const void* A, const void* B, void* C, const void* bias, const void
              int epilogue, int c_f32_accum, float alpha, int force_cfg, float* ws, float* colsum, float p_drop,
              uint64_t seed, hipStream_t st);
 int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_f32_accum, int force_cfg, int* split_out);
-int64_t mp_gemm2_ws_floats(int cfg, int split, int M, int N);
+int64_t mp_gemm2_ws_floats(int cfg, int split, int M, int N, int K);
 int mp_gemm2_has_probe_engines();
 int mp_gemm_tt_grouped(int n, const void* const* A, const void* const* B, float* const* C, const int* M, const int* N,
                        const int* K, const int64_t* lda, const int64_t* ldb, const int64_t* ldc, float alpha,
@@ -409,7 +409,7 @@ int64_t gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<t
   int split = 1;
   const int cfg = mp_gemm2_plan(M, N, K, transA, transB, accum, (int)force_cfg, &split);
   torch::Tensor ws;
-  const int64_t ws_n = mp_gemm2_ws_floats(cfg, split, M, N);
+  const int64_t ws_n = mp_gemm2_ws_floats(cfg, split, M, N, K);
   if (ws_n > 0) ws = torch::empty({ws_n}, C.options().dtype(torch::kFloat32));
   const int rc = mp_gemm2(A.data_ptr(), B.data_ptr(), C.data_ptr(), ptr_or_null(bias), ptr_or_null(residual),
                           mptr_or_null(aux), M, N, K, A.stride(0), B.stride(0), C.stride(0),

@@ -1124,23 +1124,21 @@ static int launch6(const void* A, const void* B, void* C, const void* bias, cons
 }
 
 // ---------------------------------------------------------------------------------------
-// gemm7: stream-K 256x256 NT GEMM on gemm3's 16x16x32 ping-pong main loop, for grids that
-// are not whole rounds of 256 CUs (a pipeline rank's 8K-32K-token microbatches: N = 768 is
-// 96-384 tiles = 0.4-1.5 rounds, profiles/r5_*gemm*).
+// gemm7: 256x256 NT GEMM (gemm3's 16x16x32 ping-pong main loop) that splits the PARTIAL
+// round of a grid over all CUs -- a pipeline rank's 8K-32K-token microbatches are 96-384
+// tiles of 256x256 for N = 768, i.e. 0.4-1.5 rounds of 256 CUs (profiles/r5_gemm7_*).
 //
-// One persistent workgroup per CU (G = gridDim.x).  Tiles [0, dp) are data-parallel, dp a
-// multiple of G: workgroup b runs tiles b, b + G, ...  The remaining sk tiles are split
-// into 8 XCD groups (consecutive tile ids, so a group's A panels stay in its L2), and a
-// group's K iterations (sk_x tiles x K/64) are cut into q = G/8 equal contiguous ranges,
-// one per workgroup of that XCD in dispatch order (b = x, x + 8, x + 16, ...; the
-// dispatcher places block b on XCD b % 8).  A tile cut between workgroups is OWNED by the
-// one holding its last K iteration; the others (lower in dispatch order) are contributors,
-// and a workgroup contributes to at most one tile -- the last of its range.  Order inside a
-// workgroup: the contributed segment FIRST (its f32 partial goes to the workgroup's slot
-// and a flag is raised), then its own whole tiles, then the tile whose head lower
-// workgroups computed, LAST: by then those partials are long published.  A workgroup
-// waits only for workgroups dispatched before it, which hold a CU or are done, so the
-// protocol cannot deadlock even when other kernels occupy CUs (microbatch lanes).
+// One persistent workgroup per CU (G = gridDim.x = 256).  The whole rounds (dp tiles, a
+// multiple of G) run data-parallel: workgroup b takes tiles b, b + G, ...  The remaining
+// tail tiles are split into 8 XCD groups (consecutive tile ids; block b runs on XCD b % 8)
+// and each of a group's c tiles into S K-chunks: the group's workgroup l (b = x + 8 l, in
+// dispatch order) computes chunk j = l / c of tile l % c.  Workgroups of one chunk index
+// walk the same K range of neighbouring tiles at the same time, so A panels are shared in
+// the XCD's L2 (a stream-K walk that staggers K offsets across the tiles of one row band
+// measured 2.4x slower: the A panel is re-read from HBM per tile).  Chunks 0..S-2 publish
+// f32 partials; the last chunk's workgroup owns the tile: it absorbs the others (they were
+// dispatched before it, hold a CU or are done -- no deadlock even when other kernels occupy
+// CUs) and runs the fused epilogue.
 //
 // Hand-off (cdna guide §6 Guideline 16, R1): partial stored with sc1 (write-through)
 // 16-byte buffer stores in register order (thread-linear, coalesced), every wave drains
@@ -1318,14 +1316,22 @@ __device__ __forceinline__ void g7_absorb(f32x4 (&acc)[8][4], const float* slot,
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the poll
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(slot), 0, SK_SLOT * 4,
                                                                      0x00020000);
+  // 8 loads in flight at a time (all 32 at once would need 128 more VGPRs beside acc)
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 8; i += 2) {
+    u32x4_t v[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, (i * 4 + j) * NT * 16,
-                                                              16 /* sc1 */);
-      acc[i][j] += __builtin_bit_cast(f32x4, v);
-    }
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        v[ii][j] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, ((i + ii) * 4 + j) * NT * 16,
+                                                         16 /* sc1 */);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i + ii][j] += __builtin_bit_cast(f32x4, v[ii][j]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 }
 
 template <int EPI>
@@ -1334,7 +1340,7 @@ gemm7_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, bf16_t*
              const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
              float* __restrict__ colsum, float* __restrict__ ws, int M, int N, int K, int64_t lda, int64_t ldb,
              int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop, uint64_t seed, int dp_tiles,
-             int sk_tiles) {
+             int sk_tiles, int S) {
   if (p_drop > 0.f) seed = step_seed(seed);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int G = gridDim.x, b = blockIdx.x;
@@ -1358,56 +1364,57 @@ gemm7_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, bf16_t*
     finish(m0, n0);
   }
   if (sk_tiles <= 0) return;
-  // stream-K tiles: XCD group x = b % 8 owns tiles [t0, t1) and splits their iterations
-  const int x = b & 7, q = G >> 3, L = b >> 3;
+  // the partial round: XCD group x = b % 8 owns tiles [t0, t1) (c of them); its q = G / 8
+  // workgroups split each into S chunks, workgroup l taking chunk l / c of tile l % c, so
+  // the workgroups of one chunk index walk the same K range of neighbouring tiles at once
+  // (their A panels are shared through the XCD's L2)
+  const int x = b & 7, q = G >> 3, l = b >> 3;
   const int t0 = dp_tiles + (int)((int64_t)x * sk_tiles / 8), t1 = dp_tiles + (int)((int64_t)(x + 1) * sk_tiles / 8);
-  const int64_t iters = (int64_t)(t1 - t0) * kt;
-  auto lo_of = [&](int l) { return (int)(iters * l / q); };   // first iteration of workgroup l
-  const int s = lo_of(L), e = lo_of(L + 1);
-  if (s >= e) return;
-  const int tf = s / kt, tl = (e - 1) / kt;    // group-relative first / last tile
-  int hi = tl;
-  if (e % kt != 0) {
-    // contributor of tile tl: its head segment goes to this workgroup's slot
-    const int k0 = (s > tl * kt ? s : tl * kt) - tl * kt;
-    const int tile = t0 + tl;
-    g7_mainloop(A, B, M, N, lda, ldb, (tile / gn) * 256, (tile % gn) * 256, k0, e - tl * kt - k0, smem, acc);
-    g7_publish(acc, part + (int64_t)b * SK_SLOT, flags + b);
-    hi = tl - 1;
+  const int c = t1 - t0;
+  if (c <= 0 || l >= c * S) return;
+  const int ti = l % c, j = l / c;
+  const int k0 = (int)((int64_t)j * kt / S), k1 = (int)((int64_t)(j + 1) * kt / S);
+  const int tile = t0 + ti;
+  const int m0 = (tile / gn) * 256, n0 = (tile % gn) * 256;
+  g7_mainloop(A, B, M, N, lda, ldb, m0, n0, k0, k1 - k0, smem, acc);
+  if (j < S - 1) {
+    g7_publish(acc, part + (int64_t)b * SK_SLOT, flags + b);   // contributor: partial + flag
+    return;
   }
-  // own tiles, the one whose head lower workgroups computed last
-  for (int tr = hi; tr >= tf; --tr) {
-    const int k0 = (s > tr * kt ? s : tr * kt) - tr * kt;
-    const int tile = t0 + tr;
-    const int m0 = (tile / gn) * 256, n0 = (tile % gn) * 256;
-    g7_mainloop(A, B, M, N, lda, ldb, m0, n0, k0, kt - k0, smem, acc);
-    if (k0 > 0) {
-      for (int l = L - 1; l >= 0; --l) {
-        if (lo_of(l) == lo_of(l + 1)) continue;    // an empty range published nothing
-        const int bl = x + 8 * l;
-        g7_absorb(acc, part + (int64_t)bl * SK_SLOT, flags + bl, flags + SK_ERR);
-        if (lo_of(l) <= tr * kt) break;
-      }
-    }
-    finish(m0, n0);
+  // owner (the last chunk): the lower chunks of this tile were dispatched before it
+  for (int jj = 0; jj < S - 1; ++jj) {
+    const int bl = x + 8 * (ti + jj * c);
+    g7_absorb(acc, part + (int64_t)bl * SK_SLOT, flags + bl, flags + SK_ERR);
   }
+  finish(m0, n0);
 }
 
-// plan of the stream-K engine: 0 if it should not be used for this grid, else the grid
-// size G (dp / sk tile counts out)
-static int plan7(int M, int N, int K, int* dp_out, int* sk_out) {
-  const int G = SK_MAX_G;
+// plan of the split-tail engine: 0 if it should not be used for this grid, else the grid
+// size G (data-parallel tiles, tail tiles and chunks per tail tile out)
+static int plan7(int M, int N, int K, int* dp_out, int* sk_out, int* S_out) {
+  const int G = SK_MAX_G, q = G / 8;
   const int T = ((M + 255) / 256) * ((N + 255) / 256);
   const int kt = K / BK;
   if (T < 64 || T % G == 0 || kt < 4) return 0;
-  int sk = T < G ? T : T % G + G, dp = T - sk;
-  // modelled k-iteration units: a tile costs kt + 3 (prologue fill, C write); the
-  // stream-K part costs its even share of iterations + 3 + 4 for the partial hand-off
+  const int sk = T % G, dp = T - sk;
+  const int cmax = (sk + 7) / 8;                   // tail tiles of the fullest XCD group
+  // modelled k-iteration units: a tile costs kt + 3 (prologue fill, C write); a chunked
+  // tail tile ceil(kt / S) + 3, plus 2 per partial its owner reads (256 KiB at the
+  // cross-XCD rate) and 1 for the contributors' publish
   const float plain = (float)((T + G - 1) / G) * (kt + 3);
-  const float skt = (float)(dp / G) * (kt + 3) + (float)(((int64_t)sk * kt + G - 1) / G) + 7.f;
-  if (skt > 0.97f * plain) return 0;
+  float best = 3.0e38f;
+  int bestS = 0;
+  for (int S = 2; S * cmax <= q && S <= 8; ++S) {
+    const float t = (float)(dp / G) * (kt + 3) + (float)((kt + S - 1) / S) + 3.f + 2.f * (S - 1) + 1.f;
+    if (t < best) {
+      best = t;
+      bestS = S;
+    }
+  }
+  if (bestS == 0 || best > 0.95f * plain) return 0;
   *dp_out = dp;
   *sk_out = sk;
+  *S_out = bestS;
   return G;
 }
 
@@ -1415,8 +1422,8 @@ template <int EPI>
 static int launch7(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* colsum,
                    float* ws, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx,
                    float alpha, float p_drop, uint64_t seed, hipStream_t st) {
-  int dp = 0, sk = 0;
-  const int G = plan7(M, N, K, &dp, &sk);
+  int dp = 0, sk = 0, S = 0;
+  const int G = plan7(M, N, K, &dp, &sk, &S);
   if (G == 0 || ws == nullptr) return -1;
   constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
   constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
@@ -1432,7 +1439,7 @@ static int launch7(const void* A, const void* B, void* C, const void* bias, cons
   if (e != hipSuccess) return (int)e;
   kern<<<dim3(G), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, (const bf16_t*)bias,
                                  (const bf16_t*)R, (bf16_t*)X, colsum, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha,
-                                 p_drop, seed, dp, sk);
+                                 p_drop, seed, dp, sk, S);
   return (int)hipGetLastError();
 }
 
@@ -2272,8 +2279,16 @@ extern "C" int mp_gemm2_has_probe_engines() {
 
 // f32 workspace elements the planned engine needs (split-K slabs, or the stream-K flags +
 // partial-tile slots)
-extern "C" int64_t mp_gemm2_ws_floats(int cfg, int split, int M, int N) {
-  if (cfg == 14) return (int64_t)SK_FLAGS + (int64_t)SK_MAX_G * SK_SLOT;
+extern "C" int64_t mp_gemm2_ws_floats(int cfg, int split, int M, int N, int K) {
+  if (cfg == 14) {
+    // partial slots are indexed by block id; contributors are blocks x + 8 l with
+    // l < c (S - 1) for the fullest XCD group's c tail tiles
+    int dp = 0, sk = 0, S = 0;
+    if (plan7(M, N, K, &dp, &sk, &S) == 0) return (int64_t)SK_FLAGS + (int64_t)SK_MAX_G * SK_SLOT;
+    const int cmax = (sk + 7) / 8;
+    const int64_t slots = (int64_t)8 * cmax * (S - 1);
+    return (int64_t)SK_FLAGS + slots * SK_SLOT;
+  }
   return split > 1 ? (int64_t)split * M * N : 0;
 }
 
@@ -2385,8 +2400,8 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   // slab round trip through HBM + a reduce pass) of the gemm2 tiles alike
   if (!transA && !transB && !c_f32_accum && (force_cfg == 14 || (use_sk && force_cfg < 0 && cfg != 10 &&
                                                                  cfg != 11 && cfg != 12 && cfg != 8))) {
-    int dp = 0, sk = 0;
-    if (plan7(M, N, K, &dp, &sk) > 0) {
+    int dp = 0, sk = 0, S = 0;
+    if (plan7(M, N, K, &dp, &sk, &S) > 0) {
       cfg = 14;
       split = 1;
     }

@@ -157,7 +157,7 @@ def max_inflight_microbatches(order, stages) -> int:
 
 def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, seq_len: int, device,
                    head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1,
-                   stage_shards: int = 1, dtype=torch.bfloat16, graphs: bool = False) -> dict:
+                   stage_shards: int = 1, dtype=torch.bfloat16, graphs: bool = False, lanes: int = 1) -> dict:
     """HBM plan of one pipeline rank and the recompute decision of ``recompute="auto"``:
     recompute only if the activation stash would not fit ``budget_frac`` of the device.
 
@@ -173,32 +173,37 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     leaves them whole and splits only the Adam moments -- 12 + 8 / shards bytes per
     parameter (head: 12 + 8 / head_shards).
     Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute.
-    With HIP graphs every captured forward keeps its activations in the graph's private
-    pool (parallel/graphs.py), so the stash is held for every microbatch of the step, not
-    only the schedule's in-flight ones: ``graphs=True`` counts all of them (GPT-2 small,
-    32 x 16 sequences at P = 4: ~64 GB per rank measured, r4_INDEX.md)."""
+    The stash is counted per stage from the slot plan of the rank's order
+    (parallel/stash.py): the in-flight microbatches of each stage -- also with HIP graphs,
+    whose captures share one pool per stash slot (``lanes``: slots are per microbatch lane;
+    MIPIPE_STASH_RING=0 restores one private pool per graph, i.e. all m stashes)."""
     T = mbs * seq_len
-    nlayers = sum(layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages)
+    from .parallel.stash import stash_slots_per_stage
+    layers_of = {s: layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages}
+    nlayers = sum(layers_of.values())
     emb = cfg.vocab_padded * cfg.d_model
     nparams = cfg.layer_params() * nlayers + (emb if 0 in my_stages else 0)
     f32 = dtype == torch.float32
     fixed_b, shard_b = (12.0, 8.0) if f32 else (8.0, 12.0)
     head_opt = shard_b * emb / max(1, head_shards) if head_tokens else 0.0
     head_state = (fixed_b * emb if head_tokens else 0.0) + head_opt
-    inflight = max_inflight_microbatches(order, set(my_stages))
-    if graphs:
-        inflight = max(inflight, len({a.mb for a in order if a is not None and a.stage in set(my_stages)
-                                      and a.op == Op.F}))
+    slots = stash_slots_per_stage(order, my_stages, lanes if graphs else 1)
+    if graphs and os.environ.get("MIPIPE_STASH_RING", "1") == "0":
+        n_mb = len({a.mb for a in order if a is not None and a.stage in set(my_stages) and a.op == Op.F})
+        slots = {s: n_mb for s in my_stages}
+    stash_layers = sum(slots.get(s, 1) * layers_of[s] for s in my_stages)   # stash-layer units
+    inflight = max(slots.values(), default=1)
     from .models.native import _HEAD_CHUNK
     logit_rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
     logit_b = 4.0 if f32 else 2.0
     fixed = (fixed_b + shard_b / max(1, stage_shards)) * nparams + head_state + logit_b * logit_rows * \
         cfg.vocab_padded + 4e9
-    full = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=False)
-    rec = fixed + inflight * nlayers * cfg.stash_bytes_per_layer(T, recompute=True) + \
+    full = fixed + stash_layers * cfg.stash_bytes_per_layer(T, recompute=False)
+    rec = fixed + stash_layers * cfg.stash_bytes_per_layer(T, recompute=True) + \
         cfg.stash_bytes_per_layer(T, recompute=False)
     total = torch.cuda.get_device_properties(device).total_memory if device.type == "cuda" else float("inf")
-    return dict(inflight=inflight, layers=nlayers, bytes_no_recompute=full, bytes_recompute=rec, hbm=total,
+    return dict(inflight=inflight, stash_slots=slots, layers=nlayers, bytes_no_recompute=full, bytes_recompute=rec,
+                hbm=total,
                 recompute=bool(full > budget_frac * total), head_state_bytes=head_state,
                 head_optimizer_bytes=head_opt)
 
@@ -445,7 +450,9 @@ class PipelineTrainer:
                                               head_tokens=head_tokens,
                                               head_shards=pp if (self.head_zero and pp > 1) else 1,
                                               stage_shards=self.mesh.dp if self.dp_zero else 1, dtype=dtype,
-                                              graphs=graphs and self.device.type == "cuda")
+                                              graphs=graphs and self.device.type == "cuda",
+                                              lanes=2 if (graphs and self.device.type == "cuda" and
+                                                          n_microbatches >= 2) else 1)
             recompute = self.memory_plan["recompute"]
         self.recompute = bool(recompute)
         # ZeRO-1 over DP replicas (MIPIPE_DP_ZERO=0: replicated master / moments, gradient

@@ -1,7 +1,7 @@
 """Adapter between :class:`~mipipe.models.native.NativeModel` and the pipeline runtime."""
 from __future__ import annotations
 
-from typing import Optional
+from typing import Dict, Optional
 
 import torch
 import torch.distributed as dist
@@ -61,6 +61,38 @@ class NativeStage(StageBase):
         # so the schedule hands back the merged [B, S, vocab] as a view (no concatenation)
         self._merged_logits: Optional[torch.Tensor] = None
         self._gctx = {}
+        # activation-stash slot ring under HIP graphs (parallel/stash.py, set by the runtime):
+        # mb -> (lane, slot); the graphs of a slot's microbatches share one memory pool
+        self._slot_of: Dict[int, tuple] = {}
+        self._last_reader: Dict[int, str] = {}
+        self._pools: Dict[tuple, object] = {}
+        self._released: set = set()
+
+    def set_stash_plan(self, slot_of: Dict[int, tuple], last_reader: Dict[int, str]) -> None:
+        """Slot of each microbatch's stash and the op that reads it last (B, or W after I)."""
+        self._slot_of, self._last_reader = dict(slot_of), dict(last_reader)
+
+    def stash_slots(self) -> int:
+        return len(set(self._slot_of.values())) if self._slot_of else 0
+
+    def _pool(self, mb: int):
+        c = self._slot_of.get(mb)
+        if c is None:
+            return None
+        p = self._pools.get(c)
+        if p is None:
+            p = self._pools[c] = torch.cuda.graph_pool_handle()
+        return p
+
+    def _release_stash(self, mb: int, op: str) -> None:
+        """After the capture of the stash's last reader: unpin it, so the slot's next
+        forward capture reuses its blocks (replay order on the slot's lane = capture order)."""
+        if self._last_reader.get(mb) != op or mb in self._released or mb not in self._slot_of:
+            return
+        self._released.add(mb)
+        for key in (("F", mb), ("FL", mb), ("I", mb)):
+            self.graphs.release(key)
+        self._gctx.pop(mb, None)
 
     def _graphed(self) -> bool:
         return self.graphs is not None and self.step_id > 1
@@ -136,7 +168,8 @@ class NativeStage(StageBase):
 
     def backward_weight_mb(self, mb):
         if self._graphed():
-            self.graphs.run(("W", mb), (), lambda ins: self.model.backward_weight(mb))
+            self.graphs.run(("W", mb), (), lambda ins: self.model.backward_weight(mb), pool=self._pool(mb))
+            self._release_stash(mb, "W")
             return
         self.model.backward_weight(mb)
 
@@ -159,7 +192,7 @@ class NativeStage(StageBase):
 
         # the logits-returning forward (compat step(return_outputs=True)) is its own graph
         key = ("FL", mb) if want_logits else ("F", mb)
-        out = self.graphs.run(key, ins, fn, keep=lambda: self._gctx[mb])
+        out = self.graphs.run(key, ins, fn, keep=lambda: self._gctx[mb], pool=self._pool(mb))
         if want_logits:
             loss, logits = out
             return (logits,), loss
@@ -178,7 +211,8 @@ class NativeStage(StageBase):
             return self.model.backward(ins[0] if ins else None, self._gctx[mb], self.mbs, self.S,
                                        weight_grads=weight_grads)
 
-        dx = self.graphs.run((op, mb), ins, fn, keep=lambda: self.model.defer_w.get(mb))
+        dx = self.graphs.run((op, mb), ins, fn, keep=lambda: self.model.defer_w.get(mb), pool=self._pool(mb))
+        self._release_stash(mb, op)
         return (dx,) if dx is not None else ()
 
     def infer_output_specs(self, args):

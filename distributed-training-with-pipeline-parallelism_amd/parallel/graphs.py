@@ -79,10 +79,11 @@ def _abort_capture(g: "torch.cuda.CUDAGraph", cs: "torch.cuda.Stream") -> None:
         pass
 
 
-def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any]) -> Any:
+def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any], pool=None) -> Any:
     """Capture ``fn()`` into ``g`` without a device-wide synchronisation (module docstring):
     on a per-device capture stream that first waits for the current stream, thread-local
-    capture mode, a private memory pool.  If ``fn`` raises (an allocation failing inside the
+    capture mode, a private memory pool (``pool``: the pool of earlier captures to share --
+    parallel/stash.py slot rings).  If ``fn`` raises (an allocation failing inside the
     capture, say), the capture is ended and discarded and THAT exception propagates -- not
     the ``hipErrorStreamCaptureUnjoined`` that ending a half-built capture reports when the
     failure left a forked side stream unjoined."""
@@ -93,7 +94,10 @@ def capture(g: "torch.cuda.CUDAGraph", fn: Callable[[], Any]) -> Any:
         cs = _CAPTURE_STREAMS[idx] = torch.cuda.Stream(device=idx)
     cs.wait_stream(cur)
     with torch.cuda.stream(cs):
-        g.capture_begin(capture_error_mode="thread_local")
+        if pool is not None:
+            g.capture_begin(pool=pool, capture_error_mode="thread_local")
+        else:
+            g.capture_begin(capture_error_mode="thread_local")
         try:
             out = fn()
         except BaseException:
@@ -122,9 +126,11 @@ class GraphCache:
         return key in self.graphs
 
     def run(self, key: Hashable, inputs: Sequence[torch.Tensor], fn: Callable[[Sequence[torch.Tensor]], Any],
-            keep: Callable[[], Any] = None) -> Any:
+            keep: Callable[[], Any] = None, pool=None) -> Any:
         """Replay the graph captured for ``key`` (capturing it on first use).  ``keep``
-        returns objects whose tensors must outlive the capture (saved activations)."""
+        returns objects whose tensors must outlive the capture (saved activations) -- until
+        :meth:`release`.  ``pool``: capture into this shared memory pool (a stash slot's,
+        parallel/stash.py) instead of a private one."""
         from . import native_runner
         rec = native_runner.active()
         entry = self.graphs.get(key)
@@ -132,7 +138,7 @@ class GraphCache:
             if rec is not None:
                 rec.invalidate(f"graph {key!r} captured during the recording step")
             g = torch.cuda.CUDAGraph()
-            out = capture(g, lambda: fn(inputs))
+            out = capture(g, lambda: fn(inputs), pool=pool)
             kept = _tensors(keep(), []) if keep is not None else []
             entry = (g, list(inputs), out, kept)
             self.graphs[key] = entry
@@ -149,6 +155,14 @@ class GraphCache:
         if rec is not None:
             rec.graph(entry[0], self.label(key))
         return entry[2]
+
+    def release(self, key: Hashable) -> None:
+        """Drop the tensors ``keep`` pinned for ``key`` (its graph and outputs stay): once the
+        last graph reading them is captured, their blocks return to the capture's pool, where
+        the next capture into that pool (the slot's next occupant) reuses them."""
+        entry = self.graphs.get(key)
+        if entry is not None and entry[3]:
+            self.graphs[key] = (entry[0], entry[1], entry[2], [])
 
     def clear(self) -> None:
         self.graphs.clear()

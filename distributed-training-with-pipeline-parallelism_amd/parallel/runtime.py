@@ -190,6 +190,21 @@ class PipelineRuntime:
         self._in_bufs: Dict[int, Tuple[torch.Tensor, ...]] = {}
         self._tgt_bufs: Dict[int, torch.Tensor] = {}
         self._loss_bufs: Dict[tuple, torch.Tensor] = {}
+        self._install_stash_plan()
+
+    def _install_stash_plan(self) -> None:
+        """Activation-stash slots of this rank's stages under its compute order and lanes
+        (parallel/stash.py): graphed stages capture each slot's microbatches into one pool,
+        so a rank holds the schedule's in-flight stashes, not all m (MIPIPE_STASH_RING=0:
+        one private pool per graph, the pre-round-5 behaviour)."""
+        if os.environ.get("MIPIPE_STASH_RING", "1") == "0":
+            return
+        from .stash import plan_stash_slots
+        slot, last, _ = plan_stash_slots(self.orders.get(self.rank, []), list(self.stages), self.lanes)
+        for s, st in self.stages.items():
+            if hasattr(st, "set_stash_plan"):
+                st.set_stash_plan({mb: v for (ss, mb), v in slot.items() if ss == s},
+                                  {mb: v for (ss, mb), v in last.items() if ss == s})
 
     # ------------------------------------------------------------------ hang-freedom
     def _prove(self, program: Dict[int, List[Entry]], p2p) -> Dict[int, List[Entry]]:
@@ -343,6 +358,7 @@ class PipelineRuntime:
             ha.set_lanes(n)
         self.native_runner = None   # a recorded tape does not know about lanes
         self._tapes.clear()
+        self._install_stash_plan()  # slots never shared across lanes
         return n
 
     def _head_arena(self):

@@ -210,11 +210,19 @@ def test_recompute_auto_plan():
         dpz32 = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), stage_shards=2,
                                dtype=torch.float32)
         assert rep32["bytes_no_recompute"] - dpz32["bytes_no_recompute"] == pytest.approx(4.0 * nparams)
-        # HIP graphs keep every microbatch's stash in its graph pool: all 8 microbatches of
-        # rank 1's 1F1B order count, not its 3 in flight
+        # HIP graphs: the captures of a stash slot share one pool (parallel/stash.py), so a
+        # rank holds its schedule's in-flight stashes (rank 1 of 1F1B PP = 4: 3 = P - s) per
+        # microbatch lane; MIPIPE_STASH_RING=0 (one private pool per graph): all 8
         g = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), graphs=True)
-        assert rep["inflight"] == 3 and g["inflight"] == 8
-        assert g["bytes_no_recompute"] > rep["bytes_no_recompute"]
+        g2 = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), graphs=True, lanes=2)
+        assert rep["inflight"] == 3 and g["inflight"] == 3 and 3 <= g2["inflight"] <= 4
+        import os
+        os.environ["MIPIPE_STASH_RING"] = "0"
+        try:
+            g0 = plan_recompute(cfg, l4, [1], o4, 1, 8192, torch.device("cuda", 0), graphs=True)
+        finally:
+            del os.environ["MIPIPE_STASH_RING"]
+        assert g0["inflight"] == 8 and g0["bytes_no_recompute"] > g2["bytes_no_recompute"]
         assert dpz32["bytes_no_recompute"] > dpz["bytes_no_recompute"]
         h32 = plan_recompute(cfg, l8, [7], o8, 1, 8192, torch.device("cuda", 0), head_tokens=1024, head_shards=8,
                              dtype=torch.float32)

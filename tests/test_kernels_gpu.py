@@ -434,7 +434,6 @@ def test_gemm2_configs(cfg, M, N, K, epi):
     close(y, ref)
 
 
-@needs_probe_engines
 @pytest.mark.parametrize("M,N,K,epi", [(8192, 768, 768, "bias"), (4000, 1000, 640, "none"), (9000, 2304, 768, "bias_gelu"),
                                        (24576, 768, 3072, "res"), (8192, 768, 2304, "dgelu"),
                                        (16384, 2304, 768, "colsum")])
@@ -481,6 +480,7 @@ def test_gemm7_stream_k(M, N, K, epi):
         assert torch.equal(y, y2)
 
 
+@needs_probe_engines
 @pytest.mark.parametrize("cfg", [7, 108, 103])
 @pytest.mark.parametrize("M,N,K", [(1024, 768, 768), (1000, 776, 512), (520, 264, 64), (1536, 1280, 128),
                                    (2048, 512, 1344)])

@@ -197,3 +197,49 @@ def test_capture_failure_reraises_the_original_error_and_capture_recovers():
     g.replay()
     torch.cuda.synchronize()
     assert torch.equal(out, torch.full_like(x, 3.0))
+
+
+def _train_mem(schedule, ring, m=8, steps=4):
+    import os
+    old = os.environ.get("MIPIPE_STASH_RING")
+    os.environ["MIPIPE_STASH_RING"] = "1" if ring else "0"
+    try:
+        cfg = CFGS["gpt2"]
+        dev = torch.device("cuda", 0)
+        torch.cuda.empty_cache()
+        torch.cuda.reset_peak_memory_stats(dev)
+        base = torch.cuda.memory_allocated(dev)
+        tr = PipelineTrainer(cfg, pp=1, schedule=schedule, n_microbatches=m, mbs=4, seq_len=256, device=dev,
+                             seed=3, graphs=True)
+        g = torch.Generator(device="cuda").manual_seed(7)
+        x = torch.randint(0, cfg.vocab_size, (m * 4, 256), device=dev, generator=g)
+        y = torch.randint(0, cfg.vocab_size, (m * 4, 256), device=dev, generator=g)
+        tr.capture_graphs(x, y)
+        losses = [float(tr.train_step(x, y)) for _ in range(steps)]
+        torch.cuda.synchronize()
+        peak = torch.cuda.max_memory_allocated(dev) - base
+        slots = [st.stash_slots() for st in tr.stages]
+        del tr
+        torch.cuda.empty_cache()
+        return losses, peak, slots
+    finally:
+        if old is None:
+            os.environ.pop("MIPIPE_STASH_RING", None)
+        else:
+            os.environ["MIPIPE_STASH_RING"] = old
+
+
+def test_stash_ring_follows_the_schedule_under_graphs():
+    """with HIP graphs the captures of a stash slot share one pool, so a
+    rank's HBM follows its schedule's in-flight microbatches: 1F1B at P = 1 holds one stash
+    per microbatch lane, GPipe all m = 8 -- and training is unchanged (bitwise: same kernels,
+    same order; only where the stash lives differs)."""
+    l_on, p_1f1b, s_1f1b = _train_mem("1F1B", True)
+    l_off, p_1f1b_off, _ = _train_mem("1F1B", False)
+    l_g, p_gpipe, s_gpipe = _train_mem("GPipe", True)
+    assert l_on == l_off
+    assert l_g == pytest.approx(l_on, rel=1e-4)
+    assert s_gpipe[0] == 8 and s_1f1b[0] <= 2, (s_gpipe, s_1f1b)
+    # the stash difference: GPipe holds 8 stashes, 1F1B 1 per lane
+    assert p_1f1b < 0.75 * p_gpipe, (p_1f1b, p_gpipe)
+    assert p_1f1b < 0.75 * p_1f1b_off, (p_1f1b, p_1f1b_off)

@@ -344,3 +344,40 @@ def test_pick_microbatch_weak_scaling_gpt2_small():
         assert (mbs, m) == (16, 32) and sc[16]["score"] > 1.02 * sc[32]["score"]
     finally:
         E.pick_schedule = orig
+
+
+def test_stash_slot_plan_follows_the_schedule():
+    """parallel/stash.py: the slots a stage's forwards occupy = the schedule's in-flight
+    stashes -- 1F1B P - s (torch Schedule1F1B warmup, schedules.py:873-876), GPipe m, ZBH1
+    until each W; never shared across microbatch lanes; a slot is reused only after its
+    previous occupant's last reader."""
+    from mipipe.parallel.ir import Op
+    from mipipe.parallel.stash import plan_stash_slots, stash_slots_per_stage
+    P, m = 4, 16
+    for name, v in (("1F1B", 1), ("GPipe", 1), ("ZBH1", 1), ("Interleaved1F1B", 2)):
+        orders = generate(name, P, m, v)
+        for r in range(P):
+            stages = [s for s in range(P * v) if s % P == r]
+            for lanes in (1, 2):
+                slot, last, count = plan_stash_slots(orders[r], stages, lanes)
+                # replay: a slot is free again only after the last reader of its occupant
+                held = {}
+                for a in orders[r]:
+                    if a is None or a.stage not in stages or a.mb is None:
+                        continue
+                    if a.op == Op.F:
+                        k = (a.stage,) + slot[(a.stage, a.mb)]
+                        assert k not in held, (name, r, a)
+                        assert k[1] == a.mb % lanes
+                        held[k] = a.mb
+                    if last.get((a.stage, a.mb)) == a.op.value:
+                        k = (a.stage,) + slot[(a.stage, a.mb)]
+                        assert held.pop(k) == a.mb
+                assert not held
+            n = stash_slots_per_stage(orders[r], stages, 1)
+            if name == "1F1B":
+                assert n == {r: P - r}, (r, n)
+            if name == "GPipe":
+                assert n == {r: m}
+            if name == "ZBH1":
+                assert P - r <= n[r] < m

@@ -2,7 +2,8 @@
 microbatch): 256x256 tiles are 384 = 1.5 waves of 256 CUs; 256x192 tiles are 512 = 2 waves.
 Times forced configs (5 = the ping-pong 256x256 engine gemm3, 9 = the ping-pong 256x192
 engine gemm6, 1 = gemm2's 2-stage 256x192, -1 = the planner's choice) and hipBLASLt,
-interleaved.  python tools/gemm_tail_probe.py [--ms 8192,32768,65536] [--cfgs -1,5,9,1]"""
+interleaved.  python tools/gemm_tail_probe.py [--ms 8192,32768,65536] [--cfgs=-1,5,9,1] [--graph]
+(14 = the split-tail engine gemm7)"""
 import argparse
 import os
 import sys
@@ -18,19 +19,38 @@ def t(fn, it=20):
     for _ in range(5):
         fn()
     torch.cuda.synchronize()
+    if GRAPH:   # the in-step condition: launches replayed from one HIP graph
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            g.capture_begin()
+            for _ in range(it):
+                fn()
+            g.capture_end()
+        torch.cuda.current_stream().wait_stream(s)
+        g.replay()
+        torch.cuda.synchronize()
+        fn = g.replay
+        it_ = it
+        it = 3
+    else:
+        it_ = 1
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(it):
         fn()
     e.record()
     torch.cuda.synchronize()
-    return s.elapsed_time(e) / it * 1e3
+    return s.elapsed_time(e) / it / it_ * 1e3
 
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--ms", default="32768,65536")
 ap.add_argument("--cfgs", default="-1,5,9,1")
+ap.add_argument("--graph", action="store_true", help="time 20 launches replayed from one HIP graph")
 a = ap.parse_args()
+GRAPH = a.graph
 CFGS = [int(c) for c in a.cfgs.split(",")]
 for M in [int(m) for m in a.ms.split(",")]:
     for N, K in ((768, 768), (768, 2304), (768, 3072), (2304, 768), (3072, 768)):
