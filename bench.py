@@ -156,7 +156,9 @@ def parse(argv=None):
                     help="reference (L,H) configs of the fp32 phase: 'l8h8', 'all' (the 9 of nb:346-349) or "
                          "'L,H;L,H' (default: all at P = 2 / 4, where the reference published, else L8 H8)")
     ap.add_argument("--ref-p", type=int, default=None, help=argparse.SUPPRESS)
-    ap.add_argument("--phase", default="sched", choices=["sched", "ref", "plan"], help=argparse.SUPPRESS)
+    ap.add_argument("--phase", default="sched", choices=["sched", "ref", "plan", "rate"], help=argparse.SUPPRESS)
+    ap.add_argument("--rate-pp", type=int, default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--rates", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--mbs", type=int, default=None,
                     help="sequences per microbatch (default: 64 on one GPU; with a pipeline the supervisor "
                          "plans 32 or 16 -- engine.pick_microbatch -- and 32 without it)")
@@ -390,8 +392,16 @@ def supervise(a, argv) -> int:
     if a.mbs is None and a.microbatches is None and pp > 1 and os.environ.get("MIPIPE_BENCH_MBS", "auto") == "auto":
         plan_path = os.path.join(d, "mbs.plan")
         if rank == 0:
+            # the per-GPU kernel rate at each candidate microbatch size, measured for THIS
+            # model's per-rank shapes on GPU 0 (engine.rate_probe_config; a GPU box only)
+            rates = None
+            if ref_fp32_on(argparse.Namespace(ref_fp32="auto")) and os.environ.get("MIPIPE_BENCH_RATES", "1") != "0":
+                rates = rate_probe_child(argv, pp, min(120.0, max(10.0, left() - 360.0)))
             # (the first `import torch` on a fresh box can take 1-2 minutes)
-            mbs_plan = plan_microbatch_child(argv, min(150.0, max(10.0, left() - 300.0)))
+            plan_argv = list(argv) + (["--rates", json.dumps(rates["rates"])] if rates and "rates" in rates else [])
+            mbs_plan = plan_microbatch_child(plan_argv, min(150.0, max(10.0, left() - 300.0)))
+            if rates is not None:
+                mbs_plan["rate_probe"] = rates
             _publish(plan_path, json.dumps(mbs_plan))
         else:
             txt = _wait_file(plan_path, 210.0)
@@ -494,6 +504,64 @@ def plan_microbatch_child(argv, timeout_s: float) -> dict:
         return {"error": f"plan child exceeded {timeout_s:.0f}s"}
 
 
+def rate_probe_child(argv, pp: int, timeout_s: float) -> dict:
+    """Run ``bench.py --phase rate`` (one process, GPU 0) and return its JSON, or
+    {"error": ...} -- the planner then uses its GPT-2-small table."""
+    cmd = [sys.executable, os.path.abspath(__file__)] + list(argv) + ["--phase", "rate", "--rate-pp", str(pp)]
+    env = dict(os.environ, MIPIPE_BENCH_CHILD="1", WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", LOCAL_WORLD_SIZE="1")
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode == 0 and lines:
+            return json.loads(lines[-1])
+        return {"error": f"rate child rc={r.returncode}: {r.stderr[-300:]}"}
+    except subprocess.TimeoutExpired:
+        return {"error": f"rate child exceeded {timeout_s:.0f}s"}
+
+
+def run_rate(a) -> None:
+    """--phase rate: tokens/s of one GPU running the per-rank work of a ``--rate-pp``-stage
+    pipeline of the model (engine.rate_probe_config: L / P layers, V / P vocabulary) at each
+    candidate microbatch size -- 1F1B, 4 microbatches on the default lanes, HIP graphs, 2
+    warmup + 5 timed steps each."""
+    import torch
+    import mipipe  # noqa: F401
+    from mipipe.engine import PipelineTrainer, rate_probe_config
+    from mipipe.models.config import NativeConfig
+    kw = {"vocab_size": a.vocab} if a.vocab else {}
+    pp = max(1, a.rate_pp or 1)
+    cfg = rate_probe_config(NativeConfig.by_name(a.model, **kw), pp)
+    gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", 0) if gpu else torch.device("cpu")
+    t0 = time.monotonic()
+    rates = {}
+    for mbs in (32, 16):
+        m = 4
+        tr = PipelineTrainer(cfg, pp=1, schedule="1F1B", n_microbatches=m, mbs=mbs, seq_len=a.seq, device=dev,
+                             seed=0, graphs=gpu)
+        g = torch.Generator(device=dev).manual_seed(5)
+        x = torch.randint(0, cfg.vocab_size, (m * mbs, a.seq), device=dev, generator=g)
+        y = torch.randint(0, cfg.vocab_size, (m * mbs, a.seq), device=dev, generator=g)
+        if gpu:
+            tr.capture_graphs(x, y)
+        for _ in range(2):
+            tr.train_step(x, y)
+        if gpu:
+            torch.cuda.synchronize()
+        t = time.perf_counter()
+        n = 5
+        for _ in range(n):
+            tr.train_step(x, y)
+        if gpu:
+            torch.cuda.synchronize()
+        rates[mbs] = round(m * mbs * a.seq * n / (time.perf_counter() - t), 1)
+        del tr
+        if gpu:
+            torch.cuda.empty_cache()
+    print(json.dumps({"rates": rates, "probe_model": {"n_layers": cfg.n_layers, "vocab": cfg.vocab_size, "pp": pp},
+                      "probe_s": round(time.monotonic() - t0, 1)}), flush=True)
+
+
 def run_plan(a) -> None:
     """--phase plan: the microbatch size for the supervisor (never touches the GPU)."""
     import mipipe  # noqa: F401
@@ -504,7 +572,8 @@ def run_plan(a) -> None:
     kw = {"vocab_size": a.vocab} if a.vocab else {}
     cfg = NativeConfig.by_name(a.model, **kw)
     t0 = time.monotonic()
-    mbs, m, scores = pick_microbatch(cfg, pp, a.seq, 128 * pp)
+    rates = json.loads(a.rates) if a.rates else None
+    mbs, m, scores = pick_microbatch(cfg, pp, a.seq, 128 * pp, rates=rates)
     print(json.dumps({"mbs": mbs, "microbatches": m, "scores": {str(k): v for k, v in scores.items()},
                       "plan_s": round(time.monotonic() - t0, 1)}), flush=True)
 
@@ -971,6 +1040,8 @@ def main():
         run_ref(a)
     elif a.phase == "plan":
         run_plan(a)
+    elif a.phase == "rate":
+        run_rate(a)
     else:
         run(a)
 

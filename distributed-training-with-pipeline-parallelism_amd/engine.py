@@ -320,23 +320,45 @@ def microbatch_rate(tokens: int) -> float:
     return 1.0
 
 
+def rate_probe_config(cfg: NativeConfig, pp: int) -> NativeConfig:
+    """The per-rank work of a ``pp``-stage pipeline of ``cfg`` as a one-GPU model: L / pp of
+    its layers (same shapes) and a vocabulary of V / pp (the distributed head spreads the
+    head's token chunks evenly over the ranks, parallel/headsplit.py) -- what bench.py's
+    microbatch-rate probe times at each candidate microbatch size (``rates`` of
+    :func:`pick_microbatch`)."""
+    import dataclasses
+    v = max(128, (cfg.vocab_size // max(1, pp) + 127) // 128 * 128)
+    return dataclasses.replace(cfg, n_layers=max(1, cfg.n_layers // max(1, pp)), vocab_size=v, vocab_padded=0)
+
+
 def pick_microbatch(cfg: NativeConfig, pp: int, seq_len: int, seqs_per_replica: int,
-                    candidates=(32, 16), margin: float = 0.02) -> Tuple[int, int, Dict[int, dict]]:
+                    candidates=(32, 16), margin: float = 0.02,
+                    rates: Optional[Dict[int, float]] = None) -> Tuple[int, int, Dict[int, dict]]:
     """``--mbs auto`` at PP > 1 with a fixed batch per pipeline replica (weak scaling): for
     each candidate microbatch size the schedule ``pick_schedule`` would run and its planned
-    efficiency (bubble + distributed head + p2p), times the measured per-microbatch kernel
-    rate (``microbatch_rate``).  The first candidate (the larger microbatch) is kept unless
-    another scores more than ``margin`` better.  Returns (mbs, microbatches, {mbs: detail})."""
+    efficiency (bubble + distributed head + p2p), times the per-GPU kernel rate at that
+    microbatch size.  ``rates`` ({mbs: tokens/s}): measured for THIS model's per-rank shapes
+    (bench.py's rate probe, :func:`rate_probe_config`); without it the
+    GPT-2-small table ``microbatch_rate``.  The first candidate (the larger microbatch) is
+    kept unless another scores more than ``margin`` better.  Returns (mbs, microbatches,
+    {mbs: detail})."""
     scores = {}
+    base = None
+    if rates:
+        rates = {int(k): float(v) for k, v in rates.items() if v}
+        base = next((rates[c] for c in candidates if c in rates), None)
     for mbs in candidates:
         if seqs_per_replica % mbs:
             continue
         m = seqs_per_replica // mbs
         sched, eff = pick_schedule(cfg, pp, m, mbs, seq_len)
         e = eff.get(sched, 1.0 if pp == 1 else 0.0)
-        rate = microbatch_rate(mbs * seq_len)
+        if base and mbs in rates:
+            rate, src = rates[mbs] / base, "measured"
+        else:
+            rate, src = microbatch_rate(mbs * seq_len), "gpt2-small table"
         scores[mbs] = {"microbatches": m, "schedule": sched, "planned_efficiency": round(e, 4),
-                       "kernel_rate": round(rate, 4), "score": round(e * rate, 4)}
+                       "kernel_rate": round(rate, 4), "rate_source": src, "score": round(e * rate, 4)}
     if not scores:
         raise ValueError(f"no candidate microbatch size divides {seqs_per_replica} sequences")
     first = next(iter(scores))

@@ -814,9 +814,13 @@ class PipelineRuntime:
                     continue
                 st = self.stages.get(a.stage)
                 if a.op == Op.REDUCE_GRAD:
+                    if not st.has_grad_reduction(self.scale_grads):
+                        # nothing to issue (no DP, scale folded into the loss): the stage's
+                        # lanes are merged at the step's final join -- a join here would drain
+                        # the lanes while the rank's other stages still run backwards
+                        # (interleaved: one mid-step join per extra stage)
+                        continue
                     self._join_lanes(rec, a.stage)
-                    if rec is not None and not st.has_grad_reduction(self.scale_grads):
-                        continue    # nothing to issue (no DP, scale folded into the loss)
                     if rec is not None and not getattr(st, "records_own_collectives", False):
                         # an autograd stage's torch.distributed reduction: a CALL on the tape
                         from .native_runner import record_issue

@@ -376,3 +376,20 @@ def test_trainer_auto_schedule():
     assert tr.schedule == "1F1B" and tr.schedule_choice == {}
     name, eff = pick_schedule(NativeConfig.by_name("gpt2-small"), 2, 8, 32, 1024)
     assert name in eff and eff[name] == max(eff.values()) or (name == "1F1B" and max(eff.values()) < 1.03 * eff["1F1B"])
+
+
+def test_pick_microbatch_uses_rates_measured_for_the_model():
+    """--mbs auto scores each candidate with the kernel rate measured for the
+    model's own per-rank shapes (bench.py --phase rate on engine.rate_probe_config) when
+    given, the GPT-2-small table otherwise."""
+    from mipipe.engine import pick_microbatch, rate_probe_config
+    from mipipe.models.config import NativeConfig
+    cfg = NativeConfig.gpt2("small")
+    mbs, m, sc = pick_microbatch(cfg, 4, 1024, 512, rates={32: 1.0e6, 16: 1.0e6})
+    assert sc[16]["rate_source"] == "measured" and sc[16]["kernel_rate"] == 1.0
+    assert mbs == 16 and m == 32      # same per-token rate: the smaller bubble wins
+    mbs, m, sc = pick_microbatch(cfg, 4, 1024, 512, rates={"32": 1.0e6, "16": 0.5e6})
+    assert mbs == 32 and sc[16]["kernel_rate"] == 0.5 and sc[32]["rate_source"] == "measured"
+    p = rate_probe_config(NativeConfig.llama3("8b"), 8)
+    assert p.n_layers == 4 and p.vocab_size >= 128256 // 8 and p.vocab_size % 128 == 0
+    assert p.vocab_padded >= p.vocab_size
