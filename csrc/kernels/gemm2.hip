@@ -246,7 +246,11 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
                                          const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
                                          bf16_t* __restrict__ AUX, float* __restrict__ WS, int M, int N, int64_t ldc,
                                          int64_t ldr, int64_t ldx, float alpha, int nsplit, float p_drop,
-                                         uint64_t seed) {
+                                         uint64_t seed, const float* __restrict__ parts = nullptr,
+                                         int64_t pstep = 0, int nparts = 0) {
+  // parts (gemm7's tile owner): nparts row-major [BM][BN] f32 partial tiles at parts + p *
+  // pstep, added to the accumulator before the epilogue (published with sc1 stores; the
+  // caller's agent-scope acquire precedes)
   constexpr int RG = BM / WM;      // rows per group
   constexpr int CP = BN + 4;       // f32 pitch
   // 8-column chunks per tile row; the store loop runs on the first NTE threads, a multiple
@@ -302,6 +306,13 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
       const float4 lo = *reinterpret_cast<const float4*>(ct + row * CP + c8);
       const float4 hi = *reinterpret_cast<const float4*>(ct + row * CP + c8 + 4);
       v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      if constexpr (!ACC) {
+        for (int pp = 0; pp < nparts; ++pp) {
+          const float* src = parts + pp * pstep + (int64_t)(pass * RG + row) * BN + c8;
+          const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
+          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+        }
+      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= alpha;
       if constexpr (ACC) {
@@ -573,7 +584,7 @@ __global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2
 gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
              const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
              float* __restrict__ WS, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr,
-             int64_t ldx, float alpha, float p_drop, uint64_t seed) {
+             int64_t ldx, float alpha, float p_drop, uint64_t seed, int tile_lim) {
   if (p_drop > 0.f) seed = step_seed(seed);
   constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
   constexpr int HALF = 128 * 128;          // one half-tile image: 128 rows x 128 B
@@ -581,14 +592,15 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
-  const int nwg = gm * gn;
+  const int nwg = tile_lim > 0 ? tile_lim : gm * gn;
   const int wg = xcd_remap((int)blockIdx.x, nwg);
   constexpr int GROUP = MP_G3_GROUP;   // tile rows per raster group (L2 reuse of the A panels)
   const int group = wg / (GROUP * gn);
   const int first_m = group * GROUP;
   const int gsz = min(gm - first_m, GROUP);
-  const int tm = first_m + (wg % (GROUP * gn)) % gsz;
-  const int tn = (wg % (GROUP * gn)) / gsz;
+  // tile_lim > 0 (gemm7's leading rounds): the first tile_lim tiles in row-major order
+  const int tm = tile_lim > 0 ? wg / gn : first_m + (wg % (GROUP * gn)) % gsz;
+  const int tn = tile_lim > 0 ? wg % gn : (wg % (GROUP * gn)) / gsz;
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
@@ -888,7 +900,7 @@ template <int EPI, bool ACC, bool M16, bool TT = false>
 static int launch3(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
                    int N, int K,
                    int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha, int split,
-                   float p_drop, uint64_t seed, hipStream_t st) {
+                   float p_drop, uint64_t seed, hipStream_t st, int tile_lim = 0) {
   constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
   constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
   constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
@@ -898,9 +910,10 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  const int nwg = ((M + 255) / 256) * ((N + 255) / 256);
+  const int nwg = tile_lim > 0 ? tile_lim : ((M + 255) / 256) * ((N + 255) / 256);
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
-                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
+                                          (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed,
+                                          tile_lim);
   return (int)hipGetLastError();
 }
 
@@ -1124,15 +1137,14 @@ static int launch6(const void* A, const void* B, void* C, const void* bias, cons
 }
 
 // ---------------------------------------------------------------------------------------
-// gemm7: 256x256 NT GEMM (gemm3's 16x16x32 ping-pong main loop) that splits the PARTIAL
-// round of a grid over all CUs -- a pipeline rank's 8K-32K-token microbatches are 96-384
-// tiles of 256x256 for N = 768, i.e. 0.4-1.5 rounds of 256 CUs (profiles/r5_gemm7_*).
+// gemm7: the PARTIAL round of a 256x256 NT GEMM split over all CUs -- a pipeline rank's
+// 8K-32K-token microbatches are 96-384 tiles of 256x256 for N = 768, i.e. 0.4-1.5 rounds of
+// 256 CUs (profiles/r5_gemm7_*).  The host runs the whole rounds as a plain gemm3 launch on
+// the leading rows and this kernel on the remaining tail rows (mp_gemm2, cfg 14).
 //
-// One persistent workgroup per CU (G = gridDim.x = 256).  The whole rounds (dp tiles, a
-// multiple of G) run data-parallel: workgroup b takes tiles b, b + G, ...  The remaining
-// tail tiles are split into 8 XCD groups (consecutive tile ids; block b runs on XCD b % 8)
-// and each of a group's c tiles into S K-chunks: the group's workgroup l (b = x + 8 l, in
-// dispatch order) computes chunk j = l / c of tile l % c.  Workgroups of one chunk index
+// The tail's tiles are split into 8 XCD groups (consecutive tile ids; block b runs on XCD
+// b % 8) and each of a group's c tiles into S K-chunks: the group's workgroup l (b = x + 8 l,
+// in dispatch order) computes chunk j = l / c of tile l % c.  Workgroups of one chunk index
 // walk the same K range of neighbouring tiles at the same time, so A panels are shared in
 // the XCD's L2 (a stream-K walk that staggers K offsets across the tiles of one row band
 // measured 2.4x slower: the A panel is re-read from HBM per tile).  Chunks 0..S-2 publish
@@ -1140,17 +1152,20 @@ static int launch6(const void* A, const void* B, void* C, const void* bias, cons
 // dispatched before it, hold a CU or are done -- no deadlock even when other kernels occupy
 // CUs) and runs the fused epilogue.
 //
-// Hand-off (cdna guide §6 Guideline 16, R1): partial stored with sc1 (write-through)
-// 16-byte buffer stores in register order (thread-linear, coalesced), every wave drains
-// vmcnt, workgroup barrier, one agent-scope flag store; the owner's thread 0 polls the
-// flag (bounded: a lost hand-off sets an error word instead of hanging), barrier, and every
-// wave reads the partial with sc1 buffer loads (no L1 copy can be stale).  The flags are
-// the first 1088 B of the workspace, zeroed by a memset node before every launch.
+// Hand-off (cdna guide §6 Guideline 16, R1): the partial is staged through LDS like the
+// epilogue and stored row-major with sc1 (write-through) 16-byte buffer stores, every wave
+// drains vmcnt, workgroup barrier, one agent-scope 8-byte flag store of a 64-bit tag; the
+// owner's thread 0 polls the flags (bounded: a lost hand-off sets an error word instead of
+// hanging), clears them, takes one agent-scope acquire, barrier, and the epilogue adds the
+// partials (plain loads) to the LDS-staged accumulator before the fused epilogue.  So every flag is back to 0 when a launch ends and no
+// memset node is needed before the next (one measured 5.3 us per call): a fresh workspace
+// from the caching allocator can only hold the tag by a 2^-64 accident.
 // ---------------------------------------------------------------------------------------
 constexpr int SK_SLOT = 256 * 256;          // floats per partial tile
-constexpr int SK_FLAGS = 272;               // flag words + error word (first 1088 B of the workspace)
-constexpr int SK_ERR = 256;                 // index of the error word
+constexpr int SK_FLAGS = 2 * 256 + 16;      // 256 64-bit flags + the error word (floats of workspace)
+constexpr int SK_ERR = 2 * 256;             // error word (as a 32-bit index)
 constexpr int SK_MAX_G = 256;
+constexpr unsigned long long SK_TAG = 0x7FF7A5A55A5AC3C3ull;   // a NaN payload: never f32 data
 
 __device__ __forceinline__ void g7_mainloop(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, int M, int N,
                                             int64_t lda, int64_t ldb, int m0, int n0, int kt0, int nk, char* smem,
@@ -1286,52 +1301,54 @@ __device__ __forceinline__ void g7_mainloop(const bf16_t* __restrict__ A, const 
 
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 
-// a contributor's partial tile -> its slot (sc1, register order), then its flag
-__device__ __forceinline__ void g7_publish(const f32x4 (&acc)[8][4], float* slot, unsigned* flag) {
+// a contributor's partial tile -> its slot, row-major [256][256] f32: staged through LDS one
+// wave-row group at a time exactly like the epilogue (so the accumulators die as they are
+// staged), then sc1 (write-through) 16-byte buffer stores; every wave drains them, a
+// barrier, one agent-scope flag store
+template <class StageF>
+__device__ __forceinline__ void g7_publish(const StageF& stage, char* smem, int wr, float* slot,
+                                           unsigned long long* flag) {
+  constexpr int RG = 128, CP = 256 + 4;
+  float* ct = reinterpret_cast<float*>(smem);
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(slot, 0, SK_SLOT * 4, 0x00020000);
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[i][j]), r, (int)threadIdx.x * 16,
-                                             (i * 4 + j) * NT * 16, 16 /* sc1 */);   // lane part in voffset
+#pragma unroll 1
+  for (int pass = 0; pass < 2; ++pass) {
+    if (wr == pass) stage(ct, CP);
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < RG * 64; idx += NT) {
+      const int row = idx >> 6, c4 = (idx & 63) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(ct + row * CP + c4);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, ((pass * RG + row) * 256 + c4) * 4, 0,
+                                             16 /* sc1 */);
+    }
+    __syncthreads();
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its stores
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(flag, SK_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// the owner adds a contributor's partial once its flag is up (bounded poll)
-__device__ __forceinline__ void g7_absorb(f32x4 (&acc)[8][4], const float* slot, unsigned* flag, unsigned* err) {
+// the owner waits for its contributors' flags (thread 0, bounded poll), clears them for the
+// next launch, and makes their partials visible to this CU: one agent-scope acquire (drops
+// this CU's L1) before a barrier; the epilogue then reads them with plain loads
+__device__ __forceinline__ void g7_await(unsigned long long* flags, int first, int step, int n, unsigned* err) {
   if (threadIdx.x == 0) {
-    unsigned spins = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > (1u << 24)) {     // ~0.5 s: a lost hand-off ends the kernel, flagged
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+    for (int p = 0; p < n; ++p) {
+      unsigned long long* f = flags + first + p * step;
+      unsigned spins = 0;
+      while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != SK_TAG) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 24)) {     // ~0.5 s: a lost hand-off ends the kernel, flagged
+          __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
       }
+      __hip_atomic_store(f, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the poll
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(slot), 0, SK_SLOT * 4,
-                                                                     0x00020000);
-  // 8 loads in flight at a time (all 32 at once would need 128 more VGPRs beside acc)
-#pragma unroll
-  for (int i = 0; i < 8; i += 2) {
-    u32x4_t v[2][4];
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        v[ii][j] = __builtin_amdgcn_raw_buffer_load_b128(r, (int)threadIdx.x * 16, ((i + ii) * 4 + j) * NT * 16,
-                                                         16 /* sc1 */);
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i + ii][j] += __builtin_bit_cast(f32x4, v[ii][j]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
 }
 
 template <int EPI>
@@ -1339,107 +1356,103 @@ __global__ void __launch_bounds__(NT, 1) __attribute__((amdgpu_waves_per_eu(2, 2
 gemm7_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, bf16_t* __restrict__ C,
              const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
              float* __restrict__ colsum, float* __restrict__ ws, int M, int N, int K, int64_t lda, int64_t ldb,
-             int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop, uint64_t seed, int dp_tiles,
-             int sk_tiles, int S) {
+             int64_t ldc, int64_t ldr, int64_t ldx, float alpha, float p_drop, uint64_t seed, int S, int tile0) {
   if (p_drop > 0.f) seed = step_seed(seed);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int G = gridDim.x, b = blockIdx.x;
-  const int gn = (N + 255) / 256;
+  const int b = blockIdx.x;
+  // the tail tiles [tile0, T) of the whole output in row-major tile order (full-matrix
+  // indices: the fused dropout's mask index is the element of the whole output)
+  const int gn = (N + 255) / 256, T = ((M + 255) / 256) * gn - tile0;
   const int kt = K / BK;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave / 4, wn = (wave % 4) * 64;
-  unsigned* flags = reinterpret_cast<unsigned*>(ws);
+  unsigned long long* flags = reinterpret_cast<unsigned long long*>(ws);
   float* part = ws + SK_FLAGS;
-  f32x4 acc[8][4];
-  auto finish = [&](int m0, int n0) {
-    epilogue<256, 256, 2, 4, EPI, false>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, C, bias, R, AUX, colsum,
-                                         M, N, ldc, ldr, ldx, alpha, 1, p_drop, seed);
-  };
-  // data-parallel tiles (whole rounds): each XCD walks a contiguous block of tile rows
-  for (int t = b; t < dp_tiles; t += G) {
-    const int tile = xcd_remap(t, dp_tiles);
-    const int m0 = (tile / gn) * 256, n0 = (tile % gn) * 256;
-    g7_mainloop(A, B, M, N, lda, ldb, m0, n0, 0, kt, smem, acc);
-    finish(m0, n0);
-  }
-  if (sk_tiles <= 0) return;
-  // the partial round: XCD group x = b % 8 owns tiles [t0, t1) (c of them); its q = G / 8
-  // workgroups split each into S chunks, workgroup l taking chunk l / c of tile l % c, so
-  // the workgroups of one chunk index walk the same K range of neighbouring tiles at once
-  // (their A panels are shared through the XCD's L2)
-  const int x = b & 7, q = G >> 3, l = b >> 3;
-  const int t0 = dp_tiles + (int)((int64_t)x * sk_tiles / 8), t1 = dp_tiles + (int)((int64_t)(x + 1) * sk_tiles / 8);
+  // XCD group x owns tiles [t0, t1) (c of them); workgroup l of the group takes chunk
+  // l / c of tile l % c, so one chunk index walks the same K range of neighbouring tiles
+  const int x = b & 7, l = b >> 3;
+  const int t0 = (int)((int64_t)x * T / 8), t1 = (int)((int64_t)(x + 1) * T / 8);
   const int c = t1 - t0;
   if (c <= 0 || l >= c * S) return;
   const int ti = l % c, j = l / c;
   const int k0 = (int)((int64_t)j * kt / S), k1 = (int)((int64_t)(j + 1) * kt / S);
-  const int tile = t0 + ti;
+  const int tile = tile0 + t0 + ti;
   const int m0 = (tile / gn) * 256, n0 = (tile % gn) * 256;
+  f32x4 acc[8][4];
   g7_mainloop(A, B, M, N, lda, ldb, m0, n0, k0, k1 - k0, smem, acc);
-  if (j < S - 1) {
-    g7_publish(acc, part + (int64_t)b * SK_SLOT, flags + b);   // contributor: partial + flag
+  if (j < S - 1) {   // contributor: partial + flag
+    g7_publish(Stage16<8, 4>{acc, wn, lane}, smem, wr, part + (int64_t)b * SK_SLOT, flags + b);
     return;
   }
   // owner (the last chunk): the lower chunks of this tile were dispatched before it
-  for (int jj = 0; jj < S - 1; ++jj) {
-    const int bl = x + 8 * (ti + jj * c);
-    g7_absorb(acc, part + (int64_t)bl * SK_SLOT, flags + bl, flags + SK_ERR);
-  }
-  finish(m0, n0);
+  g7_await(flags, x + 8 * ti, 8 * c, S - 1, reinterpret_cast<unsigned*>(ws) + SK_ERR);
+  epilogue<256, 256, 2, 4, EPI, false>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, C, bias, R, AUX, colsum, M,
+                                       N, ldc, ldr, ldx, alpha, 1, p_drop, seed, part + (int64_t)(x + 8 * ti) * SK_SLOT,
+                                       (int64_t)8 * c * SK_SLOT, S - 1);
 }
 
-// plan of the split-tail engine: 0 if it should not be used for this grid, else the grid
-// size G (data-parallel tiles, tail tiles and chunks per tail tile out)
-static int plan7(int M, int N, int K, int* dp_out, int* sk_out, int* S_out) {
+// plan of the split-tail engine: 0 if it should not be used for this grid, else 1 with the
+// tiles of the leading data-parallel rounds (dp, row-major, run by gemm3), the tail tiles and
+// the chunks per tail tile (S)
+struct Plan7 {
+  int dp, tail, S;
+};
+static int plan7(int M, int N, int K, Plan7* out) {
   const int G = SK_MAX_G, q = G / 8;
   const int T = ((M + 255) / 256) * ((N + 255) / 256);
   const int kt = K / BK;
   if (T < 64 || T % G == 0 || kt < 4) return 0;
-  const int sk = T % G, dp = T - sk;
-  const int cmax = (sk + 7) / 8;                   // tail tiles of the fullest XCD group
+  const int dp = (T / G) * G, tail = T - dp;
+  const int cmax = (tail + 7) / 8;                  // tail tiles of the fullest XCD group
   // modelled k-iteration units: a tile costs kt + 3 (prologue fill, C write); a chunked
   // tail tile ceil(kt / S) + 3, plus 2 per partial its owner reads (256 KiB at the
-  // cross-XCD rate) and 1 for the contributors' publish
+  // cross-XCD rate) and 1 for the contributors' publish; + 2 for a second launch
   const float plain = (float)((T + G - 1) / G) * (kt + 3);
+  const float lead = (float)(dp / G) * (kt + 3) + (dp > 0 ? 2.f : 0.f);
   float best = 3.0e38f;
   int bestS = 0;
   for (int S = 2; S * cmax <= q && S <= 8; ++S) {
-    const float t = (float)(dp / G) * (kt + 3) + (float)((kt + S - 1) / S) + 3.f + 2.f * (S - 1) + 1.f;
+    const float t = lead + (float)((kt + S - 1) / S) + 3.f + 2.f * (S - 1) + 1.f;
     if (t < best) {
       best = t;
       bestS = S;
     }
   }
+  static const int forceS = [] { const char* e = getenv("MIPIPE_GEMM7_S"); return e ? atoi(e) : 0; }();
+  if (forceS >= 1 && forceS * cmax <= q) bestS = forceS, best = 0.f;   // A/B probes
   if (bestS == 0 || best > 0.95f * plain) return 0;
-  *dp_out = dp;
-  *sk_out = sk;
-  *S_out = bestS;
-  return G;
+  out->dp = dp;
+  out->tail = tail;
+  out->S = bestS;
+  return 1;
 }
 
 template <int EPI>
 static int launch7(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* colsum,
                    float* ws, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx,
                    float alpha, float p_drop, uint64_t seed, hipStream_t st) {
-  int dp = 0, sk = 0, S = 0;
-  const int G = plan7(M, N, K, &dp, &sk, &S);
-  if (G == 0 || ws == nullptr) return -1;
+  Plan7 pl{};
+  if (!plan7(M, N, K, &pl) || ws == nullptr) return -1;
   constexpr int LDS_MAIN = 2 * 4 * 128 * 128;
   constexpr int EPI_BYTES = 128 * (256 + 4) * 4;
   constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
+  if (pl.dp > 0) {   // the whole rounds: the ping-pong engine on the first dp tiles (row-major)
+    const int rc = launch3<EPI, false, true>(A, B, C, bias, R, X, colsum, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, 1,
+                                             p_drop, seed, st, pl.dp);
+    if (rc != 0) return rc;
+  }
   auto kern = gemm7_kernel<EPI>;
   static bool attr = false;
   if (!attr) {
     hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
     attr = true;
   }
-  // the flag words: zeroed before every launch (a memset node under graph capture)
-  hipError_t e = hipMemsetAsync(ws, 0, SK_FLAGS * sizeof(unsigned), st);
-  if (e != hipSuccess) return (int)e;
-  kern<<<dim3(G), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, (const bf16_t*)bias,
-                                 (const bf16_t*)R, (bf16_t*)X, colsum, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha,
-                                 p_drop, seed, dp, sk, S);
+  // the tail tiles [dp, T)
+  const int cmax = (pl.tail + 7) / 8;
+  kern<<<dim3(8 * cmax * pl.S), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, (bf16_t*)C, (const bf16_t*)bias,
+                                               (const bf16_t*)R, (bf16_t*)X, colsum, ws, M, N, K, lda, ldb, ldc, ldr,
+                                               ldx, alpha, p_drop, seed, pl.S, pl.dp);
   return (int)hipGetLastError();
 }
 
@@ -2283,10 +2296,10 @@ extern "C" int64_t mp_gemm2_ws_floats(int cfg, int split, int M, int N, int K) {
   if (cfg == 14) {
     // partial slots are indexed by block id; contributors are blocks x + 8 l with
     // l < c (S - 1) for the fullest XCD group's c tail tiles
-    int dp = 0, sk = 0, S = 0;
-    if (plan7(M, N, K, &dp, &sk, &S) == 0) return (int64_t)SK_FLAGS + (int64_t)SK_MAX_G * SK_SLOT;
-    const int cmax = (sk + 7) / 8;
-    const int64_t slots = (int64_t)8 * cmax * (S - 1);
+    Plan7 pl{};
+    if (!plan7(M, N, K, &pl)) return (int64_t)SK_FLAGS + (int64_t)SK_MAX_G * SK_SLOT;
+    const int cmax = (pl.tail + 7) / 8;
+    const int64_t slots = (int64_t)8 * cmax * (pl.S - 1);
     return (int64_t)SK_FLAGS + slots * SK_SLOT;
   }
   return split > 1 ? (int64_t)split * M * N : 0;
@@ -2400,8 +2413,8 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   // slab round trip through HBM + a reduce pass) of the gemm2 tiles alike
   if (!transA && !transB && !c_f32_accum && (force_cfg == 14 || (use_sk && force_cfg < 0 && cfg != 10 &&
                                                                  cfg != 11 && cfg != 12 && cfg != 8))) {
-    int dp = 0, sk = 0, S = 0;
-    if (plan7(M, N, K, &dp, &sk, &S) > 0) {
+    Plan7 pl{};
+    if (plan7(M, N, K, &pl) > 0) {
       cfg = 14;
       split = 1;
     }

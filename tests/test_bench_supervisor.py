@@ -214,8 +214,13 @@ def test_bench_four_ranks_measures_all_three_schedules():
     for name, e in sch.items():
         assert e["tok_s"] > 0 and e["bubble_fraction"] is not None and e["analytic_bubble"] is not None, (name, e)
         assert e["p2p_bytes_per_step"] > 0
-    assert sch["Interleaved1F1B"]["v"] == 2 and sch["GPipe"]["v"] == 1
-    assert sch["Interleaved1F1B"]["analytic_bubble"] < sch["1F1B"]["analytic_bubble"]
+    # 4 layers over 4 ranks: two chunks per rank would leave virtual stages empty, so
+    # interleaved falls back to one chunk -- the reference's own rule when L % 2P != 0
+    # (helper:181-183; VERDICT r4: no empty range in any layer split)
+    assert sch["Interleaved1F1B"]["v"] == 1 and sch["GPipe"]["v"] == 1
+    assert sch["Interleaved1F1B"]["analytic_bubble"] == sch["1F1B"]["analytic_bubble"]
+    for name, e in sch.items():
+        assert all(b > a for a, b in e["layer_split"]), (name, e["layer_split"])
     assert sch["GPipe"]["speedup_vs_gpipe"] == 1.0
     # --schedule auto: the headline is the best-planned schedule, and it is measured once
     head = out["config"]["schedule"]

@@ -434,14 +434,15 @@ def test_gemm2_configs(cfg, M, N, K, epi):
     close(y, ref)
 
 
-@pytest.mark.parametrize("M,N,K,epi", [(8192, 768, 768, "bias"), (4000, 1000, 640, "none"), (9000, 2304, 768, "bias_gelu"),
-                                       (24576, 768, 3072, "res"), (8192, 768, 2304, "dgelu"),
-                                       (16384, 2304, 768, "colsum")])
+@pytest.mark.parametrize("M,N,K,epi", [(8192, 768, 768, "bias"), (4000, 1000, 640, "none"),
+                                       (32768, 768, 2304, "bias_gelu"), (24576, 768, 3072, "res"),
+                                       (8192, 768, 2304, "dgelu"), (8192, 768, 3072, "colsum")])
 def test_gemm7_stream_k(M, N, K, epi):
-    """gemm7 (stream-K over 256 persistent workgroups, XCD-grouped K ranges, sc1 partial
-    hand-off): grids of 64-324 tiles incl. ragged M / N edges, every fused epilogue class,
-    the fused column sums; also bit-for-bit stable across repeated launches (each tile's
-    partials are summed in a fixed order)."""
+    """gemm7 (the partial round split into K chunks over all CUs, XCD-grouped, sc1 partial
+    hand-off; whole rounds first as a gemm3 launch on the leading tiles): grids of 64-384
+    tiles incl. ragged M / N edges, every fused epilogue class, the fused column sums; also
+    bit-for-bit stable across repeated launches (each tile's partials are summed in a fixed
+    order) -- which also checks the self-clearing hand-off flags of the previous launch."""
     from mipipe.ops import kernels as _k
     e = _k.load_ext()
     assert e.gemm2_plan(M, N, K, False, False, False, -1)[0] == 14, "planner should pick stream-K here"

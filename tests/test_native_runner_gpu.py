@@ -210,7 +210,7 @@ def _train_mem(schedule, ring, m=8, steps=4):
         torch.cuda.reset_peak_memory_stats(dev)
         base = torch.cuda.memory_allocated(dev)
         tr = PipelineTrainer(cfg, pp=1, schedule=schedule, n_microbatches=m, mbs=4, seq_len=256, device=dev,
-                             seed=3, graphs=True)
+                             seed=3, graphs=True, lr=1e-2)
         g = torch.Generator(device="cuda").manual_seed(7)
         x = torch.randint(0, cfg.vocab_size, (m * 4, 256), device=dev, generator=g)
         y = torch.randint(0, cfg.vocab_size, (m * 4, 256), device=dev, generator=g)
@@ -232,13 +232,16 @@ def _train_mem(schedule, ring, m=8, steps=4):
 def test_stash_ring_follows_the_schedule_under_graphs():
     """with HIP graphs the captures of a stash slot share one pool, so a
     rank's HBM follows its schedule's in-flight microbatches: 1F1B at P = 1 holds one stash
-    per microbatch lane, GPipe all m = 8 -- and training is unchanged (bitwise: same kernels,
-    same order; only where the stash lives differs)."""
+    per microbatch lane, GPipe all m = 8 -- and training is unchanged (same kernels and order,
+    only where the stash lives differs; equal up to the f32 atomics' summation order, with a
+    learning rate high enough that a backward reading another microbatch's stash would show
+    in the loss at once)."""
     l_on, p_1f1b, s_1f1b = _train_mem("1F1B", True)
     l_off, p_1f1b_off, _ = _train_mem("1F1B", False)
     l_g, p_gpipe, s_gpipe = _train_mem("GPipe", True)
-    assert l_on == l_off
+    assert l_on == pytest.approx(l_off, rel=1e-4)
     assert l_g == pytest.approx(l_on, rel=1e-4)
+    assert l_on[-1] < l_on[0] - 0.1      # it trains
     assert s_gpipe[0] == 8 and s_1f1b[0] <= 2, (s_gpipe, s_1f1b)
     # the stash difference: GPipe holds 8 stashes, 1F1B 1 per lane
     assert p_1f1b < 0.75 * p_gpipe, (p_1f1b, p_gpipe)
