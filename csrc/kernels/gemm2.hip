@@ -240,7 +240,7 @@ struct Stage16 {
   }
 };
 
-template <int BM, int BN, int WM, int WN, int EPI, bool ACC, int NTH = NT, class StageF>
+template <int BM, int BN, int WM, int WN, int EPI, bool ACC, int NTH = NT, bool PARTS = false, class StageF>
 __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0, int n0, int wr,
                                          void* __restrict__ Cv,
                                          const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R,
@@ -268,6 +268,32 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
   for (int pass = 0; pass < WM; ++pass) {
     if (wr == pass) stage(ct, CP);
     __syncthreads();
+    if constexpr (!ACC && PARTS) {
+      if (nparts > 0) {
+        // the partial row blocks added into the staged rows: every thread's loads of one
+        // partial in flight at once (a load inside the store loop would wait per element)
+        constexpr int Q4 = RG * BN / 4, N4 = (Q4 + NTH - 1) / NTH;
+        for (int pp = 0; pp < nparts; ++pp) {
+          const float* src = parts + pp * pstep + (int64_t)(pass * RG) * BN;
+          float4 pv[N4];
+#pragma unroll
+          for (int u = 0; u < N4; ++u) {
+            const int idx = min((int)threadIdx.x + u * NTH, Q4 - 1);
+            pv[u] = *reinterpret_cast<const float4*>(src + (idx / (BN / 4)) * BN + (idx % (BN / 4)) * 4);
+          }
+#pragma unroll
+          for (int u = 0; u < N4; ++u) {
+            const int idx = threadIdx.x + u * NTH;
+            if (idx >= Q4) break;
+            float4* d = reinterpret_cast<float4*>(ct + (idx / (BN / 4)) * CP + (idx % (BN / 4)) * 4);
+            float4 t = *d;
+            t.x += pv[u].x; t.y += pv[u].y; t.z += pv[u].z; t.w += pv[u].w;
+            *d = t;
+          }
+        }
+        __syncthreads();
+      }
+    }
     const int rbase = m0 + pass * RG;
     if constexpr (ACC) {
       if (nsplit > 1 && WS != nullptr) {
@@ -306,13 +332,6 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
       const float4 lo = *reinterpret_cast<const float4*>(ct + row * CP + c8);
       const float4 hi = *reinterpret_cast<const float4*>(ct + row * CP + c8 + 4);
       v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w; v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-      if constexpr (!ACC) {
-        for (int pp = 0; pp < nparts; ++pp) {
-          const float* src = parts + pp * pstep + (int64_t)(pass * RG + row) * BN + c8;
-          const float4 a = *reinterpret_cast<const float4*>(src), b = *reinterpret_cast<const float4*>(src + 4);
-          v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
-        }
-      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] *= alpha;
       if constexpr (ACC) {
@@ -1161,6 +1180,9 @@ static int launch6(const void* A, const void* B, void* C, const void* bias, cons
 // memset node is needed before the next (one measured 5.3 us per call): a fresh workspace
 // from the caching allocator can only hold the tag by a 2^-64 accident.
 // ---------------------------------------------------------------------------------------
+#ifndef MP_G7_SC1
+#define MP_G7_SC1 0   // 1: partials by sc1 write-through buffer stores (no release fence)
+#endif
 constexpr int SK_SLOT = 256 * 256;          // floats per partial tile
 constexpr int SK_FLAGS = 2 * 256 + 16;      // 256 64-bit flags + the error word (floats of workspace)
 constexpr int SK_ERR = 2 * 256;             // error word (as a 32-bit index)
@@ -1318,14 +1340,26 @@ __device__ __forceinline__ void g7_publish(const StageF& stage, char* smem, int 
     for (int idx = threadIdx.x; idx < RG * 64; idx += NT) {
       const int row = idx >> 6, c4 = (idx & 63) * 4;
       const float4 v = *reinterpret_cast<const float4*>(ct + row * CP + c4);
+#if MP_G7_SC1
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), r, ((pass * RG + row) * 256 + c4) * 4, 0,
                                              16 /* sc1 */);
+#else
+      *reinterpret_cast<float4*>(slot + (pass * RG + row) * 256 + c4) = v;   // into this XCD's L2
+#endif
     }
     __syncthreads();
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drains its stores
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, SK_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+#if !MP_G7_SC1
+    // plain stores: one agent-scope release writes the XCD L2's dirty lines back (the
+    // cdna guide's split-K recipe: fence, then an explicit wait, then the signal)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    __hip_atomic_store(flag, SK_TAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // the owner waits for its contributors' flags (thread 0, bounded poll), clears them for the
@@ -1387,8 +1421,9 @@ gemm7_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, bf16_t*
   }
   // owner (the last chunk): the lower chunks of this tile were dispatched before it
   g7_await(flags, x + 8 * ti, 8 * c, S - 1, reinterpret_cast<unsigned*>(ws) + SK_ERR);
-  epilogue<256, 256, 2, 4, EPI, false>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, C, bias, R, AUX, colsum, M,
-                                       N, ldc, ldr, ldx, alpha, 1, p_drop, seed, part + (int64_t)(x + 8 * ti) * SK_SLOT,
+  epilogue<256, 256, 2, 4, EPI, false, NT, true>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, C, bias, R, AUX,
+                                       colsum, M, N, ldc, ldr, ldx, alpha, 1, p_drop, seed,
+                                       part + (int64_t)(x + 8 * ti) * SK_SLOT,
                                        (int64_t)8 * c * SK_SLOT, S - 1);
 }
 
@@ -2407,8 +2442,12 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   }
   if (use5 && cfg == 5 && split == 1 && !c_f32_accum && force_cfg < 0) cfg = 8;
   // the stream-K engine (gemm7) where the 256x256 grid is not whole rounds of 256 CUs
-  // (MIPIPE_GEMM_SK=0 disables; force_cfg 14 selects it wherever plan7 accepts the grid)
-  static const bool use_sk = [] { const char* e = getenv("MIPIPE_GEMM_SK"); return !(e && e[0] == '0'); }();
+  // (force_cfg 14 selects it wherever plan7 accepts the grid)
+  // Opt-in (MIPIPE_GEMM_SK=1): measured null -- on the all-tail M = 8192 grids the split
+  // tail (S = 2) takes 37 vs 23.5 us at K = 768 and 60 vs 55 us at K = 3072; the hand-off of
+  // a 256x256 f32 partial (LDS staging + 256 KiB out and back in, sc1 or plain + release
+  // alike) costs about what the halved K loop saves (profiles/r5_gemm7_split_tail_null.txt)
+  static const bool use_sk = [] { const char* e = getenv("MIPIPE_GEMM_SK"); return e && e[0] == '1'; }();
   // replaces the ping-pong engine's partial rounds and the bf16-output split-K slabs (f32
   // slab round trip through HBM + a reduce pass) of the gemm2 tiles alike
   if (!transA && !transB && !c_f32_accum && (force_cfg == 14 || (use_sk && force_cfg < 0 && cfg != 10 &&

@@ -445,7 +445,7 @@ def test_gemm7_stream_k(M, N, K, epi):
     order) -- which also checks the self-clearing hand-off flags of the previous launch."""
     from mipipe.ops import kernels as _k
     e = _k.load_ext()
-    assert e.gemm2_plan(M, N, K, False, False, False, -1)[0] == 14, "planner should pick stream-K here"
+    assert e.gemm2_plan(M, N, K, False, False, False, 14)[0] == 14, "split-tail engine should accept this grid"
     torch.manual_seed(0)
     x, w, b, r = rnd(M, K), rnd(N, K, scale=K ** -0.5), rnd(N, scale=0.1), rnd(M, N)
     xg, wg, bg, rg = (t.to(DEV) for t in (x, w, b, r))
@@ -455,7 +455,7 @@ def test_gemm7_stream_k(M, N, K, epi):
     cs = torch.zeros(N, device=DEV) if epi == "colsum" else None
     run = lambda out: _k._gemm(xg, wg, out, bias=bg if "bias" in epi else None,  # noqa: E731
                                residual=rg if epi == "res" else None, aux=aux if "gelu" in epi else None,
-                               epi=epi_id, colsum=cs)
+                               epi=epi_id, colsum=cs, cfg=14)
     run(y)
     ref = x.float() @ w.float().t()
     if "bias" in epi:

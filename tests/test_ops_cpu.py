@@ -171,20 +171,23 @@ def test_use_f32_kernels_swaps_module_classes_only():
     assert F.linear is orig_linear
 
 
-def test_gemm_planner_picks_stream_k_only_for_partial_rounds():
-    """gemm2.hip mp_gemm2_plan (host code, runs without a GPU): the stream-K engine (cfg 14)
-    for NT grids that are not whole rounds of 256 CUs -- a pipeline rank's 8K-32K-token
-    microbatches -- and the ping-pong engine (5) for whole rounds (64K tokens, N = 768:
-    768 tiles = 3 rounds); never for dW (TT, f32 accumulate) or short-token grids."""
+def test_gemm_planner_split_tail_is_opt_in(monkeypatch):
+    """gemm2.hip mp_gemm2_plan (host code, runs without a GPU): the split-tail engine (cfg
+    14, opt-in) accepts NT grids that are not whole rounds of 256 CUs -- a pipeline rank's
+    8K-32K-token microbatches -- and never whole rounds (64K tokens, N = 768: 768 tiles = 3
+    rounds), dW (TT, f32 accumulate) or short-token grids."""
     from mipipe.ops import kernels as K
     e = K.load_ext()
     if e is None or not hasattr(e, "gemm2_plan"):
         pytest.skip("extension not built")
-    plan = lambda M, N, Kd, ta=False, tb=False, acc=False: e.gemm2_plan(M, N, Kd, ta, tb, acc, -1)[0]  # noqa: E731
+    # default: off (a measured null, gemm2.hip); force_cfg 14 plans it where it applies
+    assert e.gemm2_plan(8192, 768, 768, False, False, False, -1)[0] != 14
+    assert e.gemm2_plan(8192, 768, 768, False, False, False, 14)[0] == 14
+    plan = lambda M, N, Kd, ta=False, tb=False, acc=False: e.gemm2_plan(M, N, Kd, ta, tb, acc, 14)[0]  # noqa: E731
     for M, N, Kd in ((8192, 768, 768), (8192, 768, 3072), (32768, 768, 3072), (32768, 768, 2304)):
         assert plan(M, N, Kd) == 14, (M, N, Kd)
     # whole rounds, or a tail too wide to split into chunks (16K x 768: 192 tiles)
     for M, N, Kd in ((65536, 768, 768), (65536, 768, 3072), (65536, 3072, 768), (16384, 768, 3072)):
         assert plan(M, N, Kd) != 14, (M, N, Kd)
-    assert plan(2048, 768, 768) != 14                       # 24 tiles: the small-tile engine
+    assert plan(2048, 768, 768) != 14                       # 24 tiles: below the split threshold
     assert plan(768, 3072, 32768, True, True, True) != 14    # dW
