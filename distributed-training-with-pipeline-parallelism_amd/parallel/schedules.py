@@ -247,8 +247,13 @@ def _greedy_schedule(pp: int, m: int, v: int, style: str, costs: Dict[Op, float]
 def gen_zb_h1(pp: int, m: int, v: int = 1, style: str = "loop") -> Dict[int, List[Action]]:
     if v != 1:
         raise ValueError("ZBH1 runs one stage per rank")
+    # one chunk more in flight than 1F1B's P - r lets W fill the bubble at P > 1; at P = 1
+    # there is no bubble to fill, and the extra chunk (a whole microbatch's activations plus
+    # its deferred weight-gradient inputs) only cost HBM: 72.4 vs 52.9 GB on GPT-2 small
+    # (BENCH_r04) -- there ZBH1 is F I W per microbatch, 1F1B's memory
+    extra = 1 if pp > 1 else 0
     return _greedy_schedule(pp, m, 1, style, {Op.F: 1.0, Op.I: 1.0, Op.W: 1.0, Op.B: 2.0},
-                            max_inflight=lambda r: pp - r + 1, split_backward=True)
+                            max_inflight=lambda r: pp - r + extra, split_backward=True)
 
 
 def gen_zbv(pp: int, m: int, v: int = 2, style: str = "v") -> Dict[int, List[Action]]:
