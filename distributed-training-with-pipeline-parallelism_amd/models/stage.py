@@ -77,7 +77,7 @@ class NativeStage(StageBase):
 
     def _pool(self, mb: int):
         c = self._slot_of.get(mb)
-        if c is None:
+        if c is None or self.model.device.type != "cuda":
             return None
         p = self._pools.get(c)
         if p is None:

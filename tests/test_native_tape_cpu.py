@@ -62,7 +62,7 @@ class FakeGraph:
 
 
 class FakeGraphCache(GraphCache):
-    def run(self, key, inputs, fn, keep=None):
+    def run(self, key, inputs, fn, keep=None, pool=None):
         rec = native_runner.active()
         entry = self.graphs.get(key)
         if entry is None:
