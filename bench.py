@@ -126,9 +126,11 @@ BASE_CONFIGS = {
         ("llama3-8b 1F1B PP=8 recompute (configs/llama3_8b_1f1b_pp8.yaml)",
          ["--model", "llama3-8b", "--schedule", "1F1B", "--mbs", "1", "--microbatches", "16", "--seq", "8192",
           "--recompute", "1"], 120.0),
-        ("llama3-8b DP=2 x PP=4 recompute (configs/llama3_8b_dp2_pp4.yaml)",
+        # (BASELINE.json names recompute only for the PP = 8 config; here the HBM plan decides
+        # from the schedule's real in-flight stashes -- parallel/stash.py)
+        ("llama3-8b DP=2 x PP=4 recompute auto (configs/llama3_8b_dp2_pp4.yaml)",
          ["--model", "llama3-8b", "--dp", "2", "--schedule", "1F1B", "--mbs", "1", "--microbatches", "8", "--seq",
-          "8192", "--recompute", "1"], 120.0)],
+          "8192", "--recompute", "auto"], 120.0)],
 }
 
 
@@ -678,6 +680,18 @@ def emit(out: dict, partial: bool = False) -> None:
         print(json.dumps(out), flush=True)
 
 
+def _memory_plan_summary(trainer):
+    """This rank's HBM plan (engine.plan_recompute): the stash slots per local stage that the
+    schedule keeps alive (parallel/stash.py) and the planned bytes with / without recompute."""
+    p = getattr(trainer, "memory_plan", None)
+    if not p:
+        return None
+    return {"stash_slots": {str(k): v for k, v in p.get("stash_slots", {}).items()},
+            "planned_gb_no_recompute": round(p["bytes_no_recompute"] / 1e9, 1),
+            "planned_gb_recompute": round(p["bytes_recompute"] / 1e9, 1),
+            "recompute_needed": bool(p["recompute"])}
+
+
 def _plain_summary():
     """Plain forward / dX GEMM shapes per backend (ops.kernels MIPIPE_GEMM=auto timing)."""
     from mipipe.ops import kernels as K
@@ -874,6 +888,7 @@ def run(a) -> None:
                                        else "f32") if dp > 1 else None,
                    "head_zero": bool(getattr(trainer, "head_zero", False)) and trainer.head is not None,
                    "recompute": trainer.recompute,
+                   "memory_plan": _memory_plan_summary(trainer),
                    "recv_arena_mb": round(rt.recv_arena_bytes / 2 ** 20, 1),
                    "plain_gemms": _plain_summary(),
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None

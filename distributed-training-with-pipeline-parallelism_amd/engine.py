@@ -463,7 +463,9 @@ class PipelineTrainer:
         # ZeRO-1 over DP replicas (see below): known before the HBM plan
         self.dp_zero = (self.mesh.dp > 1 and os.environ.get("MIPIPE_DP_ZERO", "1") != "0"
                         and not (tied_pp or self._tie_local))
-        if recompute == "auto":
+        # the plan is made (and reported: bench.py's config.memory_plan) whatever the
+        # setting; recompute="auto" acts on it
+        if True:
             order = (orders if orders is not None else
                      generate(self.schedule, pp, n_microbatches, v, style)).get(self.mesh.pp_rank, [])
             head_tokens = (self.head_chunks[self.mesh.pp_rank] if self.head_chunks is not None else
@@ -475,7 +477,8 @@ class PipelineTrainer:
                                               graphs=graphs and self.device.type == "cuda",
                                               lanes=2 if (graphs and self.device.type == "cuda" and
                                                           n_microbatches >= 2) else 1)
-            recompute = self.memory_plan["recompute"]
+            if recompute == "auto":
+                recompute = self.memory_plan["recompute"]
         self.recompute = bool(recompute)
         # ZeRO-1 over DP replicas (MIPIPE_DP_ZERO=0: replicated master / moments, gradient
         # all-reduced): each replica owns 1/dp of every stage arena -- its f32 master and Adam

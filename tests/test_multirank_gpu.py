@@ -125,3 +125,21 @@ def test_rccl_pp8_matches_single(reference8, schedule, v):
     res = _run(8, *args, port=29890 + v, backend="nccl")
     assert res["losses"] == pytest.approx(reference8, rel=2e-3)
     assert res["p2p"] == "native", res
+
+
+def test_multirank_stash_follows_the_schedule():
+    """with HIP graphs on every rank (4 ranks, P = 4, m = 16), each rank holds
+    its schedule's in-flight activation stashes: 1F1B P - r per microbatch lane (rounded),
+    GPipe all 16 -- the HBM above each rank's post-init level is ordered GPipe > 1F1B on
+    every rank, and on the last rank (1F1B: one stash per lane) well under half of GPipe's."""
+    res = {}
+    for sched in ("GPipe", "1F1B"):
+        res[sched] = _run(4, "--schedule", sched, "--graphs", "1", "--split-head", "1", "--m", "16", "--mem", "1",
+                          "--steps", "2", port=29940 + len(sched))
+    g, o = res["GPipe"]["mem"], res["1F1B"]["mem"]
+    lanes = res["1F1B"]["lanes"]
+    assert g["stash_slots"] == [16] * 4, g
+    assert all(s_ <= -(-(4 - r) // lanes) * lanes for r, s_ in enumerate(o["stash_slots"])), (o, lanes)
+    for r in range(4):
+        assert o["peak_above_init"][r] < g["peak_above_init"][r], (r, o, g)
+    assert o["peak_above_init"][3] < 0.5 * g["peak_above_init"][3], (o, g)

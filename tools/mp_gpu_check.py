@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--dp", type=int, default=1, help="data-parallel replicas (pp = world / dp)")
     ap.add_argument("--vstages", type=int, default=None, help="virtual stages per rank (Interleaved1F1B)")
     ap.add_argument("--layers", type=int, default=4)
+    ap.add_argument("--m", type=int, default=8, help="microbatches per replica x dp (same data for every world)")
+    ap.add_argument("--mem", type=int, default=0, help="report every rank's HBM peak above its post-init level")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -28,9 +30,12 @@ def main():
     from mipipe.parallel.mesh import init_distributed
     rank, world, _, device = init_distributed()
     cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=a.layers, n_heads=4, d_ff=1024, max_seq_len=256)
-    m, mbs, S = 8, 2, 256   # same data for every world size
+    m, mbs, S = a.m, 2, 256   # same data for every world size
     dp = a.dp
     pp = world // dp
+    if a.mem:
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(device)
     tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m // dp,
                          mbs=mbs,
                          seq_len=S, device=device, seed=3, graphs=bool(a.graphs),
@@ -42,6 +47,7 @@ def main():
         n = x.shape[0] // dp
         r = tr.mesh.dp_rank
         x, y = x[r * n:(r + 1) * n].contiguous(), y[r * n:(r + 1) * n].contiguous()
+    base = torch.cuda.memory_allocated(device) if a.mem else 0
     if a.graphs:
         tr.capture_graphs(x, y)
     losses = []
@@ -53,8 +59,17 @@ def main():
             # the loss lives on one rank per replica (last stage) or on every rank (distributed head)
             v /= dp * (pp if tr.head is not None else 1)
         losses.append(float(v.item()))
+    mem = None
+    if a.mem:
+        torch.cuda.synchronize()
+        mine = torch.tensor([torch.cuda.max_memory_allocated(device) - base,
+                             float(sum(st.stash_slots() for st in tr.stages))], dtype=torch.float64, device=device)
+        allv = [torch.zeros_like(mine) for _ in range(world)] if world > 1 else [mine]
+        if world > 1:
+            dist.all_gather(allv, mine)
+        mem = {"peak_above_init": [float(v[0]) for v in allv], "stash_slots": [int(v[1]) for v in allv]}
     if rank == 0:
-        print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses,
+        print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses, "mem": mem,
                           "native_runner": tr.runtime.native_runner is not None,
                           "native_reason": tr.runtime.native_reason,
                           "p2p": getattr(tr.runtime.p2p, "kind", None), "lanes": tr.runtime.lanes,
