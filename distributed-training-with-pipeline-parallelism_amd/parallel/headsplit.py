@@ -21,6 +21,8 @@ actions are placed into each rank's compute order by a list-scheduling simulatio
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
@@ -166,7 +168,8 @@ def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v
                        head_costs: Dict[int, float], stage_costs: Optional[Sequence[float]] = None,
                        comm: float = 0.05, lags: Sequence[int] = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32),
                        policies: Sequence[str] = ("head_first", "fill"),
-                       regen: Optional[Callable[[int], Dict[int, Sequence[Optional[Action]]]]] = None
+                       regen: Optional[Callable[[int], Dict[int, Sequence[Optional[Action]]]]] = None,
+                       lag_tol: Optional[float] = None, max_lag: Optional[int] = None
                        ) -> Tuple[Dict[int, List[Action]], int, float]:
     """Best of ``insert_head_ops`` over the candidate last-stage lags (simulated
     makespan).  Returns (orders, lag, makespan).
@@ -175,22 +178,29 @@ def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v
     waits for its F(i) -- a round trip on the critical cycle unless the last stage has
     `lag` more forwards to run meanwhile.  GPT-2 small, PP=2, m=8: lag <= 2 planned 0.755
     of ideal, lag 8 0.912; each unit of lag stashes one more microbatch per stage
-    (hundreds of MB at GPT-2 scale, cheap next to 288 GB of HBM).
+    (hundreds of MB at GPT-2 scale, cheap next to 288 GB of HBM) -- but not free: a lag of m
+    turns 1F1B's stash into GPipe's.  So the plan takes the SMALLEST lag whose makespan is
+    within ``lag_tol`` (default 1 %, ``MIPIPE_HEAD_LAG_TOL``) of the best, and never more than
+    ``max_lag`` (``MIPIPE_HEAD_MAX_LAG``; e.g. from an HBM budget).
 
     ``regen(lag)``: the schedule regenerated with ``lag`` extra warmup forwards on every
     rank (schedules.generate(..., warmup_extra=lag)).  Tried next to the re-sort of
     ``_lag_last_stage``, which deadlocks for interleaved orders (it moves one chunk's
     backwards past the other chunk's forwards): with it, GPT-2 small Interleaved1F1B (v=2,
     m=4P) plans 0.952 / 0.935 / 0.894 of ideal at P=2/4/8 instead of 0.845 / 0.927 / 0.773."""
+    if lag_tol is None:
+        lag_tol = float(os.environ.get("MIPIPE_HEAD_LAG_TOL", "0.01"))
+    if max_lag is None and os.environ.get("MIPIPE_HEAD_MAX_LAG"):
+        max_lag = int(os.environ["MIPIPE_HEAD_MAX_LAG"])
     cands = []
     nmb = 1 + max((a.mb for es in orders.values() for a in es if a is not None), default=0)
     for lag in lags:
-        if lag > nmb * max(1, v):
+        if lag > nmb * max(1, v) or (max_lag is not None and lag > max_lag):
             continue
         cands.append((lag, orders, lag))
         if regen is not None and lag > 0:
             cands.append((lag, None, 0))
-    best = None
+    found = []
     regen_cache: Dict[int, Dict[int, Sequence[Optional[Action]]]] = {}
     for pol in policies:
         for lag, base, ins_lag in cands:
@@ -203,11 +213,12 @@ def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v
                 res = simulate(o, pp, v, style, comm_latency=comm, stage_costs=stage_costs, head_costs=head_costs)
             except (RuntimeError, ValueError):
                 continue
-            if best is None or res.makespan < best[2] - 1e-9:
-                best = (o, lag, res.makespan)
-    if best is None:
+            found.append((o, lag, res.makespan))
+    if not found:
         raise RuntimeError("no feasible head placement")
-    return best
+    fastest = min(f[2] for f in found)
+    # first (policy order) of the smallest lags that stay within the tolerance
+    return min((f for f in found if f[2] <= fastest * (1.0 + lag_tol) + 1e-9), key=lambda f: f[1])
 
 
 @dataclass

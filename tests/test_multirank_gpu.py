@@ -131,11 +131,13 @@ def test_multirank_stash_follows_the_schedule():
     """with HIP graphs on every rank (4 ranks, P = 4, m = 16), each rank holds
     its schedule's in-flight activation stashes: 1F1B P - r per microbatch lane (rounded),
     GPipe all 16 -- the HBM above each rank's post-init level is ordered GPipe > 1F1B on
-    every rank, and on the last rank (1F1B: one stash per lane) well under half of GPipe's."""
+    every rank, and on the last rank (1F1B: one stash per lane) well under half of GPipe's.
+    The head lag is capped at 0: this toy model is all p2p latency in the cost model, so the
+    head planner would otherwise buy a lag of m (= GPipe's stash) for a 4x shorter plan."""
     res = {}
     for sched in ("GPipe", "1F1B"):
-        res[sched] = _run(4, "--schedule", sched, "--graphs", "1", "--split-head", "1", "--m", "16", "--mem", "1",
-                          "--steps", "2", port=29940 + len(sched))
+        res[sched] = _run(4, "--schedule", sched, "--graphs", "1", "--split-head", "1", "--microbatches", "16", "--mem", "1",
+                          "--steps", "2", port=29940 + len(sched), extra_env={"MIPIPE_HEAD_MAX_LAG": "0"})
     g, o = res["GPipe"]["mem"], res["1F1B"]["mem"]
     lanes = res["1F1B"]["lanes"]
     assert g["stash_slots"] == [16] * 4, g

@@ -286,7 +286,8 @@ def test_interleaved_with_head_plans_ahead_of_1f1b_and_gpipe(P):
         check_lowered(lower(o, P, v, "loop", head_costs=hc, stage_costs=sc), S)
         eff[name] = (3.0 * sum(sc) + sum(hc.values())) * m / P / mk
     assert eff["Interleaved1F1B"] > max(eff["1F1B"], eff["GPipe"]) + 0.02, eff
-    assert eff["1F1B"] >= eff["GPipe"] - 1e-6, eff
+    # 1F1B may give up to the head planner's lag tolerance (1 %) for a smaller stash
+    assert eff["1F1B"] >= eff["GPipe"] * (1 - 0.01) - 1e-6, eff
 
 
 @pytest.mark.parametrize("name,v", [("GPipe", 1), ("1F1B", 1), ("Interleaved1F1B", 2)])
@@ -381,3 +382,26 @@ def test_stash_slot_plan_follows_the_schedule():
                 assert n == {r: m}
             if name == "ZBH1":
                 assert P - r <= n[r] < m
+
+
+def test_head_plan_takes_the_smallest_lag_within_tolerance():
+    """A head lag of m turns 1F1B's stash into GPipe's: the plan takes the smallest lag whose
+    makespan is within lag_tol of the best, and honours max_lag."""
+    from mipipe.engine import plan_head_pipeline
+    from mipipe.models.config import NativeConfig
+    from mipipe.parallel.headsplit import plan_head_schedule
+    cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=4, n_heads=4, d_ff=1024, max_seq_len=256)
+    P, m = 4, 16
+    base = plan_head_pipeline(cfg, P, "1F1B", m, 2, 256)
+    sc, hc = base["stage_costs"], base["head_costs"]
+    o = generate("1F1B", P, m, 1)
+    _, lag_best, mk_best = plan_head_schedule(o, P, 1, "loop", hc, sc, comm=base["comm"], lag_tol=0.0)
+    _, lag_loose, mk_loose = plan_head_schedule(o, P, 1, "loop", hc, sc, comm=base["comm"], lag_tol=10.0)
+    assert lag_loose == 0 and lag_best > 0 and mk_loose >= mk_best
+    _, lag_cap, mk_cap = plan_head_schedule(o, P, 1, "loop", hc, sc, comm=base["comm"], max_lag=2)
+    assert lag_cap <= 2 and mk_cap >= mk_best
+    # the cap shows in the stash plan: rank 0 holds fewer microbatches
+    from mipipe.parallel.stash import stash_slots_per_stage
+    full = plan_head_pipeline(cfg, P, "1F1B", m, 2, 256)["orders"]
+    cap = plan_head_schedule(o, P, 1, "loop", hc, sc, comm=base["comm"], max_lag=0)[0]
+    assert sum(stash_slots_per_stage(cap[0], [0], 1).values()) < sum(stash_slots_per_stage(full[0], [0], 1).values())

@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--dp", type=int, default=1, help="data-parallel replicas (pp = world / dp)")
     ap.add_argument("--vstages", type=int, default=None, help="virtual stages per rank (Interleaved1F1B)")
     ap.add_argument("--layers", type=int, default=4)
-    ap.add_argument("--m", type=int, default=8, help="microbatches per replica x dp (same data for every world)")
+    ap.add_argument("--microbatches", type=int, default=8, help="microbatches per replica x dp (same data for every world)")
     ap.add_argument("--mem", type=int, default=0, help="report every rank's HBM peak above its post-init level")
     a = ap.parse_args()
     import torch
@@ -30,7 +30,7 @@ def main():
     from mipipe.parallel.mesh import init_distributed
     rank, world, _, device = init_distributed()
     cfg = NativeConfig.gpt2("tiny", vocab_size=1000, d_model=256, n_layers=a.layers, n_heads=4, d_ff=1024, max_seq_len=256)
-    m, mbs, S = a.m, 2, 256   # same data for every world size
+    m, mbs, S = a.microbatches, 2, 256   # same data for every world size
     dp = a.dp
     pp = world // dp
     if a.mem:
