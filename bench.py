@@ -773,7 +773,7 @@ def run(a) -> None:
                                   recompute=a.recompute if a.recompute == "auto" else a.recompute == "1", seed=0,
                                   split_head=False if a.no_split_head else None, graphs=bool(a.graphs) and gpu,
                                   dtype=dtype)
-        describe["fn"] = trainer.runtime.describe
+        describe["fn"] = trainer.describe
         gb = dp * m * a.mbs
         g = torch.Generator(device=device).manual_seed(1234 + trainer.mesh.dp_rank)
         tokens = torch.randint(0, cfg.vocab_size, (m * a.mbs, a.seq), device=device, generator=g)

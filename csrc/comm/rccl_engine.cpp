@@ -21,6 +21,8 @@ void register_rccl(py::module& m) {
       .def("close", &RcclEngine::close)
       .def("abort", &RcclEngine::abort)
       .def("async_error", &RcclEngine::async_error)
+      .def("progress", &RcclEngine::progress)
+      .def("issued", &RcclEngine::issued)
       .def("stream_handle", &RcclEngine::stream_handle)
       .def("slot", &RcclEngine::slot)
       .def_property_readonly("channels", &RcclEngine::channels)

@@ -42,7 +42,10 @@
 
 #include <dlfcn.h>
 
+#include <algorithm>
 #include <array>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -290,7 +293,9 @@ class RcclEngine {
       MP_NCCL(g_rccl->Recv(o.ptr, o.count, o.type, o.peer, comm, cs));
     }
     MP_NCCL(g_rccl->GroupEnd());
-    return finish(cs);
+    const int64_t h = finish(cs);
+    trace(channel, -1, cs, sends, recvs);
+    return h;
   }
 
   int64_t coll_raw(int channel, int op, void* send, void* recv, size_t count, ncclDataType_t type,
@@ -306,7 +311,9 @@ class RcclEngine {
       case ALL_GATHER: MP_NCCL(g_rccl->AllGather(send, recv, count, type, comm, cs)); break;
       default: TORCH_CHECK(false, "RcclEngine: bad collective ", op);
     }
-    return finish(cs);
+    const int64_t h = finish(cs);
+    trace(channel, op, cs, {RawOp{send, count, type, -1}}, {});
+    return h;
   }
 
   void wait_raw(int64_t h, hipStream_t compute) {
@@ -342,6 +349,32 @@ class RcclEngine {
     auto it = pending_.find(h);
     return it == pending_.end() || hipEventQuery(it->second) == hipSuccess;
   }
+
+  // Hang diagnostics: the groups of the last kTrace posts / collectives (per engine) that
+  // have not completed on their channel stream, oldest first -- channel, kind (-1 p2p,
+  // else CollOp), peers, bytes, seconds since the host issued it.  A watchdog report then
+  // names the transfer every rank is stuck in instead of only the Python stack.
+  py::list progress() {
+    py::list out;
+    if (!trace_on_) return out;
+    const auto now = std::chrono::steady_clock::now();
+    const size_t n = std::min<size_t>(trace_head_, kTrace);
+    for (size_t i = trace_head_ - n; i < trace_head_; ++i) {
+      const TraceEntry& e = trace_[i % kTrace];
+      if (e.ev == nullptr || hipEventQuery(e.ev) != hipErrorNotReady) continue;
+      py::dict d;
+      d["seq"] = e.seq;
+      d["channel"] = e.channel;
+      d["kind"] = e.kind < 0 ? std::string("p2p") : std::string(coll_name(e.kind));
+      d["sends"] = py::cast(std::vector<int>(e.send_peers, e.send_peers + e.nsend));
+      d["recvs"] = py::cast(std::vector<int>(e.recv_peers, e.recv_peers + e.nrecv));
+      d["bytes"] = (int64_t)e.bytes;
+      d["age_s"] = std::chrono::duration<double>(now - e.t).count();
+      out.append(d);
+    }
+    return out;
+  }
+  int64_t issued() const { return (int64_t)trace_head_; }
 
   void synchronize() {
     if (open_)
@@ -399,11 +432,72 @@ class RcclEngine {
   }
 
   void release_events() {
+    for (auto& e : trace_)
+      if (e.ev != nullptr) hipEventDestroy(e.ev);
+    trace_.clear();
+    trace_head_ = 0;
     for (auto& kv : pending_) hipEventDestroy(kv.second);
     pending_.clear();
     for (hipEvent_t e : pool_) hipEventDestroy(e);
     pool_.clear();
   }
+
+  static constexpr size_t kTrace = 256;
+  static constexpr int kPeers = 8;
+  struct TraceEntry {
+    hipEvent_t ev = nullptr;
+    int64_t seq = 0;
+    int channel = 0, kind = -1, nsend = 0, nrecv = 0;
+    int send_peers[kPeers], recv_peers[kPeers];
+    size_t bytes = 0;
+    std::chrono::steady_clock::time_point t;
+  };
+  static const char* coll_name(int op) {
+    switch (op) {
+      case ALLREDUCE_SUM: return "all_reduce";
+      case ALLREDUCE_MAX: return "all_reduce_max";
+      case REDUCE_SCATTER_SUM: return "reduce_scatter";
+      case ALL_GATHER: return "all_gather";
+      default: return "?";
+    }
+  }
+  static size_t type_bytes(ncclDataType_t t) {
+    switch (t) {
+      case ncclInt8: case ncclUint8: return 1;
+      case ncclFloat16: case ncclBfloat16: return 2;
+      case ncclInt32: case ncclUint32: case ncclFloat32: return 4;
+      default: return 8;
+    }
+  }
+  // one extra event record per group (MIPIPE_COMM_TRACE=0: none)
+  void trace(int channel, int kind, hipStream_t cs, const std::vector<RawOp>& sends, const std::vector<RawOp>& recvs) {
+    if (!trace_on_) return;
+    if (trace_.empty()) trace_.resize(kTrace);
+    TraceEntry& e = trace_[trace_head_ % kTrace];
+    if (e.ev == nullptr) MP_HIP(hipEventCreateWithFlags(&e.ev, hipEventDisableTiming));
+    MP_HIP(hipEventRecord(e.ev, cs));
+    e.seq = (int64_t)trace_head_;
+    e.channel = channel;
+    e.kind = kind;
+    e.nsend = e.nrecv = 0;
+    e.bytes = 0;
+    for (const auto& o : sends) {
+      if (o.peer >= 0 && e.nsend < kPeers) e.send_peers[e.nsend++] = o.peer;
+      e.bytes += o.count * type_bytes(o.type);
+    }
+    for (const auto& o : recvs) {
+      if (e.nrecv < kPeers) e.recv_peers[e.nrecv++] = o.peer;
+      e.bytes += o.count * type_bytes(o.type);
+    }
+    e.t = std::chrono::steady_clock::now();
+    ++trace_head_;
+  }
+  bool trace_on_ = [] {
+    const char* v = std::getenv("MIPIPE_COMM_TRACE");
+    return v == nullptr || std::string(v) != "0";
+  }();
+  std::vector<TraceEntry> trace_;
+  size_t trace_head_ = 0;
 
   std::vector<ncclComm_t> comm_;
   std::vector<hipStream_t> stream_;

@@ -642,6 +642,14 @@ class PipelineTrainer:
             return torch.stack(losses).mean()
         return None
 
+    def describe(self) -> str:
+        """Hang report (utils/metrics.Watchdog): the runtime's program grid plus, for every
+        native RCCL engine of this rank, the issued groups that have not completed."""
+        from .parallel.comm import comm_progress_report
+        eng = {"p2p": getattr(self.runtime.p2p, "engine", None),
+               "dp": getattr(self.coll, "dp_engine", None), "embed": getattr(self.coll, "embed_engine", None)}
+        return self.runtime.describe() + "\n" + comm_progress_report(eng)
+
     def capture_graphs(self, tokens: Optional[torch.Tensor] = None, targets: Optional[torch.Tensor] = None) -> None:
         """Setup, not training: run the pipeline program twice without an optimizer step
         (eager lazy-init, then HIP-graph capture of every per-microbatch action) and

@@ -20,7 +20,7 @@ from __future__ import annotations
 import logging
 import os
 import time
-from typing import List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -95,6 +95,31 @@ def load_native_rccl(ext) -> None:
 # channel 2 carries the pipeline group's collectives (parallel/collectives.py)
 CHANNEL_OF_KIND = {"F": 0, "H": 0, "B": 1, "D": 1}
 PIPE_CHANNEL_SLOTS = (0, 1, 2)   # channel c issues on comm stream slot c (rccl_engine.h)
+
+
+def comm_progress_report(engines: Dict[str, object], limit: int = 6) -> str:
+    """One block per native engine: groups issued, the incomplete ones (oldest first: channel,
+    kind, peer ranks within the engine's group, bytes, seconds since issue) and any RCCL
+    async error.  Read by the watchdog when a step stalls: the oldest incomplete group on
+    every rank names the transfer the pipeline waits on (csrc/comm/rccl_engine.h progress)."""
+    lines = []
+    for name, eng in engines.items():
+        if eng is None or not hasattr(eng, "progress"):
+            continue
+        try:
+            pend, issued, err = eng.progress(), int(eng.issued()), eng.async_error()
+        except Exception as e:  # pragma: no cover - diagnostics only
+            lines.append(f"[comm] {name}: progress unavailable ({e})")
+            continue
+        lines.append(f"[comm] {name} engine (rank {eng.rank}/{eng.nranks}): {issued} groups issued, "
+                     f"{len(pend)} incomplete" + (f", RCCL async error: {err}" if err else ""))
+        for d in pend[:limit]:
+            peers = (f" send->{d['sends']}" if d["sends"] else "") + (f" recv<-{d['recvs']}" if d["recvs"] else "")
+            lines.append(f"[comm]   #{d['seq']} channel {d['channel']} {d['kind']}{peers} "
+                         f"{d['bytes'] / 1e6:.2f} MB, issued {d['age_s']:.1f}s ago")
+        if len(pend) > limit:
+            lines.append(f"[comm]   ... {len(pend) - limit} more")
+    return "\n".join(lines) if lines else "[comm] no native RCCL engine on this rank"
 
 
 def make_native_engine(group, ranks: Sequence[int], my_pipe_rank: int, device: torch.device):

@@ -191,3 +191,29 @@ def test_gemm_planner_split_tail_is_opt_in(monkeypatch):
         assert plan(M, N, Kd) != 14, (M, N, Kd)
     assert plan(2048, 768, 768) != 14                       # 24 tiles: below the split threshold
     assert plan(768, 3072, 32768, True, True, True) != 14    # dW
+
+
+def test_comm_progress_report_formats_incomplete_groups():
+    """The watchdog's comm block: engines without progress() are skipped, incomplete groups
+    are listed oldest first with a cap."""
+    from mipipe.parallel.comm import comm_progress_report
+
+    class Eng:
+        rank, nranks = 2, 4
+
+        def progress(self):
+            return [{"seq": 40 + i, "channel": i % 2, "kind": "p2p", "sends": [3], "recvs": [1],
+                     "bytes": 3_145_728, "age_s": 61.0 - i} for i in range(8)]
+
+        def issued(self):
+            return 48
+
+        def async_error(self):
+            return ""
+
+    rep = comm_progress_report({"p2p": Eng(), "dp": None, "x": object()}, limit=3)
+    lines = rep.splitlines()
+    assert lines[0] == "[comm] p2p engine (rank 2/4): 48 groups issued, 8 incomplete"
+    assert lines[1] == "[comm]   #40 channel 0 p2p send->[3] recv<-[1] 3.15 MB, issued 61.0s ago"
+    assert lines[-1] == "[comm]   ... 5 more" and len(lines) == 5
+    assert comm_progress_report({}) == "[comm] no native RCCL engine on this rank"

@@ -79,7 +79,6 @@ def main():
     import mipipe  # noqa: F401
     from mipipe.config import RunConfig, lr_at
     from mipipe.engine import PipelineTrainer
-    from mipipe.parallel.ir import Action, format_compute_grid
     from mipipe.parallel.mesh import init_distributed
     from mipipe.utils.metrics import MetricsLogger, Watchdog
 
@@ -119,9 +118,7 @@ def main():
         # the native stage runner once one step has been recorded
         trainer.capture_graphs(*data.batch(start))
     log = MetricsLogger(t.metrics_file, rank, device)
-    grid = lambda: format_compute_grid({r: [e for e in es if isinstance(e, Action)]
-                                        for r, es in trainer.runtime.program_all.items()})
-    wd = Watchdog(t.watchdog_s, describe=grid)
+    wd = Watchdog(t.watchdog_s, describe=trainer.describe)
     tokens_per_step = p.dp * m * t.micro_batch * t.seq_len
     for step in range(start, t.steps):
         x, y = data.batch(step)
