@@ -118,19 +118,34 @@ def insert_head_ops(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: i
     out: Dict[int, List[Action]] = {r: [] for r in range(pp)}
     total = sum(len(b) for b in base.values()) + len(head) * len(mbs)
 
+    deps: Dict[Action, list] = {}
+
     def ready_time(a: Action, r: int) -> Optional[float]:
+        dl = deps.get(a)
+        if dl is None:
+            dl = deps[a] = [(d, action_rank(d, s2r) != r) for d, _ in in_messages(a, S, split, head)]
         t = avail[r]
-        for d, _ in in_messages(a, S, split, head):
-            if d not in end:
+        for d, remote in dl:
+            e = end.get(d)
+            if e is None:
+                waiters.setdefault(d, []).append(r)
                 return None
-            lat = comm if action_rank(d, s2r) != r else 0.0
-            t = max(t, end[d] + lat)
+            t = max(t, e + comm) if remote else max(t, e)
         return t
 
+    # a rank's candidates change only when it runs an action (its ``avail``) or when an
+    # input one of them waits for is scheduled: otherwise they are reused (same result)
+    cached: Dict[int, list] = {}
+    waiters: Dict[Action, List[int]] = {}
     done = 0
     while done < total:
         best = None  # (start, tie, rank, action, is_head)
         for r in range(pp):
+            if r in cached:
+                for c in cached[r]:
+                    if best is None or (c[0], c[1], c[2]) < (best[0], best[1], best[2]):
+                        best = c
+                continue
             cands = []
             if r in head and hptr[r] < len(mbs):
                 h = Action(r, Op.H, mbs[hptr[r]])
@@ -146,6 +161,7 @@ def insert_head_ops(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: i
                 cands = cands[1:]   # the scheduled action can start now: head chunks only fill gaps
             elif policy == "fill" and len(cands) == 2:
                 cands = [cands[0]] if cands[0][0] <= cands[1][0] else [cands[1]]
+            cached[r] = cands
             for c in cands:
                 if best is None or (c[0], c[1], c[2]) < (best[0], best[1], best[2]):
                     best = c
@@ -155,6 +171,9 @@ def insert_head_ops(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v: i
         t, _, r, a, is_head = best
         end[a] = t + cost(a)
         avail[r] = end[a]
+        cached.pop(r, None)
+        for w in waiters.pop(a, ()):
+            cached.pop(w, None)
         out[r].append(a)
         if is_head:
             hptr[r] += 1
@@ -194,6 +213,10 @@ def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v
         max_lag = int(os.environ["MIPIPE_HEAD_MAX_LAG"])
     cands = []
     nmb = 1 + max((a.mb for es in orders.values() for a in es if a is not None), default=0)
+    # up to a full-depth warmup (lag m: every forward first, GPipe's order): at P = 8 with
+    # GPT-2 small's 16-sequence microbatches a hop costs about a layer forward and 1F1B
+    # plans 0.79 at lag 32 but 0.88 at lag m = 64
+    lags = sorted(set(lags) | {l for l in (48, 64, 96, 128) if l < nmb * max(1, v)} | {nmb * max(1, v)})
     for lag in lags:
         if lag > nmb * max(1, v) or (max_lag is not None and lag > max_lag):
             continue
