@@ -564,7 +564,10 @@ class PipelineTrainer:
         self.optimizer = FlatAdamW(arenas, lr=lr, eps=adam_eps, weight_decay=weight_decay, max_grad_norm=max_grad_norm,
                                    pp_group=self.mesh.pp_group if pp > 1 else None, norm_skip=norm_skip,
                                    norm_exclude=norm_exclude, grad_scale=1.0 / self.mesh.dp, coll=self.coll,
-                                   merged_norm=self.mesh.dp == 1, merged_norm_skip=merged_skip)
+                                   merged_norm=self.mesh.dp == 1,
+                                   # (MIPIPE_MERGED_NORM_SKIP=0: the pre-fix behaviour, for A/B tests only)
+                                   merged_norm_skip=merged_skip if os.environ.get("MIPIPE_MERGED_NORM_SKIP", "1") != "0"
+                                   else ())
         self.last_losses: List[torch.Tensor] = []
 
     def _head_reduce(self) -> list:

@@ -145,3 +145,19 @@ def test_multirank_stash_follows_the_schedule():
     for r in range(4):
         assert o["peak_above_init"][r] < g["peak_above_init"][r], (r, o, g)
     assert o["peak_above_init"][3] < 0.5 * g["peak_above_init"][3], (o, g)
+
+
+@pytest.mark.parametrize("split_head,extra", [(0, {}), (1, {"MIPIPE_HEAD_ZERO": "0"})])
+def test_multirank_lanes_keep_the_clip_norm(split_head, extra):
+    """with microbatch lanes the fused lane merge's sum of squares must
+    not stand in for the clip norm of an arena that is reduced further after the merge (the
+    stage-0 arena holding a tied embedding; the replicated head with MIPIPE_HEAD_ZERO=0).
+    PP = 2 with graphs: the pre-clip global norms of 4 steps with 2 lanes match one lane."""
+    res = {}
+    for lanes in ("2", "1"):
+        res[lanes] = _run(2, "--graphs", "1", "--split-head", str(split_head), "--steps", "4", "--clip", "0.05",
+                          port=29960 + 2 * split_head + int(lanes), extra_env={"MIPIPE_LANES": lanes, **extra})
+    assert res["2"]["lanes"] == 2 and res["1"]["lanes"] == 1, (res["2"]["lanes"], res["1"]["lanes"])
+    # (without the fix the first step's norm is 2 % off: the tied / replicated part counted unreduced)
+    assert res["2"]["norms"] == pytest.approx(res["1"]["norms"], rel=5e-3), (res["2"]["norms"], res["1"]["norms"])
+    assert res["2"]["losses"] == pytest.approx(res["1"]["losses"], rel=2e-3)

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--microbatches", type=int, default=8, help="microbatches per replica x dp (same data for every world)")
     ap.add_argument("--mem", type=int, default=0, help="report every rank's HBM peak above its post-init level")
+    ap.add_argument("--clip", type=float, default=1.0, help="max grad norm (the reported norms are pre-clip)")
     a = ap.parse_args()
     import torch
     import torch.distributed as dist
@@ -39,7 +40,8 @@ def main():
     tr = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule if pp > 1 else "1F1B", n_microbatches=m // dp,
                          mbs=mbs,
                          seq_len=S, device=device, seed=3, graphs=bool(a.graphs),
-                         split_head=bool(a.split_head), lr=1e-3, v=a.vstages if pp > 1 else None)
+                         split_head=bool(a.split_head), lr=1e-3, v=a.vstages if pp > 1 else None,
+                         max_grad_norm=a.clip)
     g = torch.Generator(device=device).manual_seed(11)
     x = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
     y = torch.randint(0, cfg.vocab_size, (m * mbs, S), device=device, generator=g)
@@ -50,9 +52,10 @@ def main():
     base = torch.cuda.memory_allocated(device) if a.mem else 0
     if a.graphs:
         tr.capture_graphs(x, y)
-    losses = []
+    losses, norms = [], []
     for _ in range(a.steps):
         loss = tr.train_step(x, y)
+        norms.append(float(tr.optimizer.sumsq.sqrt()) if a.clip > 0 else None)
         v = torch.tensor([float(loss) if loss is not None else 0.0], dtype=torch.float64, device=device)
         if world > 1:
             dist.all_reduce(v)
@@ -69,7 +72,7 @@ def main():
             dist.all_gather(allv, mine)
         mem = {"peak_above_init": [float(v[0]) for v in allv], "stash_slots": [int(v[1]) for v in allv]}
     if rank == 0:
-        print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses, "mem": mem,
+        print(json.dumps({"world": world, "schedule": a.schedule, "losses": losses, "mem": mem, "norms": norms,
                           "native_runner": tr.runtime.native_runner is not None,
                           "native_reason": tr.runtime.native_reason,
                           "p2p": getattr(tr.runtime.p2p, "kind", None), "lanes": tr.runtime.lanes,
