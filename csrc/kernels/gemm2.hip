@@ -247,7 +247,7 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
                                          bf16_t* __restrict__ AUX, float* __restrict__ WS, int M, int N, int64_t ldc,
                                          int64_t ldr, int64_t ldx, float alpha, int nsplit, float p_drop,
                                          uint64_t seed, const float* __restrict__ parts = nullptr,
-                                         int64_t pstep = 0, int nparts = 0) {
+                                         int64_t pstep = 0, int nparts = 0, int split_idx = -1) {
   // parts (gemm7's tile owner): nparts row-major [BM][BN] f32 partial tiles at parts + p *
   // pstep, added to the accumulator before the epilogue (published with sc1 stores; the
   // caller's agent-scope acquire precedes)
@@ -300,7 +300,7 @@ __device__ __forceinline__ void epilogue(const StageF& stage, char* smem, int m0
         // split-K partial slab [split][M][N] with plain 16-byte stores; a reduce kernel
         // adds the slabs into C (f32 atomics run at ~1.3 TB/s chip-wide and bounded the
         // dW GEMMs; MI355X_MICROARCH.md "Global float atomics")
-        float* slab = WS + (int64_t)blockIdx.y * M * N;
+        float* slab = WS + (int64_t)(split_idx >= 0 ? split_idx : (int)blockIdx.y) * M * N;
         for (int idx = threadIdx.x; idx < RG * BN / 4; idx += NTH) {
           const int row = idx / (BN / 4), c4 = (idx % (BN / 4)) * 4;
           const int gr = rbase + row, gc = n0 + c4;
@@ -612,7 +612,20 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
 
   const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
   const int nwg = tile_lim > 0 ? tile_lim : gm * gn;
-  const int wg = xcd_remap((int)blockIdx.x, nwg);
+  // split-K grids: workgroups are dealt to the 8 XCDs round-robin in LINEAR id order
+  // (x + gridDim.x * y), so remap that id, then cut it into (split, tile): an XCD's L2 holds
+  // the panels of ONE split's neighbouring tiles.  Remapping blockIdx.x alone assumed XCD =
+  // x % 8, which is wrong for y > 0 whenever gridDim.x % 8 != 0 and scattered the tiles that
+  // share a panel over all XCDs (the dW GEMMs read ~4x their unique bytes from HBM)
+  int wg, split;
+  if (gridDim.y > 1 && tile_lim == 0) {   // (tile_lim = -1: the x-only remap, MIPIPE_G3_SPLIT_REMAP=0)
+    const int v = xcd_remap((int)blockIdx.x + (int)gridDim.x * (int)blockIdx.y, nwg * (int)gridDim.y);
+    split = v / nwg;
+    wg = v % nwg;
+  } else {
+    wg = xcd_remap((int)blockIdx.x, nwg);
+    split = (int)blockIdx.y;
+  }
   constexpr int GROUP = MP_G3_GROUP;   // tile rows per raster group (L2 reuse of the A panels)
   const int group = wg / (GROUP * gn);
   const int first_m = group * GROUP;
@@ -629,8 +642,8 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
 
   const int nsplit = gridDim.y;
   const int ktiles = K / BK;
-  const int kt0 = (int)blockIdx.y * ktiles / nsplit;
-  const int nk = ((int)blockIdx.y + 1) * ktiles / nsplit - kt0;
+  const int kt0 = split * ktiles / nsplit;
+  const int nk = (split + 1) * ktiles / nsplit - kt0;
 
   // staging: this wave's two 1 KiB pieces (j = 0, 1) of every half-tile.  Piece rows
   // i = 64 j + 8 wave + (lane >> 3); swz8 reads row bits 1-3, i.e. i & 15 = 8 (wave & 1) + lr.
@@ -802,7 +815,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
   __syncthreads();
   epilogue<BM, BN, WM, WN, EPI, ACC>(Stage32<4, 2>{acc, wn, hl, l32}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M,
-                                     N, ldc, ldr, ldx, alpha, nsplit, p_drop, seed);
+                                     N, ldc, ldr, ldx, alpha, nsplit, p_drop, seed, nullptr, 0, 0, split);
   } else {
   // 16x16x32 MFMAs: same phases, DMA and barriers; a phase quadrant (64 rows x 32 cols)
   // is 4 x 2 blocks of 16x16, K = 64 in two 32-deep steps (16 MFMAs of 16 cycles)
@@ -911,7 +924,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   if (wr == 0) __builtin_amdgcn_s_barrier();  // re-align the staggered wave rows
   __syncthreads();
   epilogue<BM, BN, WM, WN, EPI, ACC>(Stage16<8, 4>{acc, wn, lane}, smem, m0, n0, wr, Cv, bias, R, AUX, WS, M, N, ldc,
-                                     ldr, ldx, alpha, nsplit, p_drop, seed);
+                                     ldr, ldx, alpha, nsplit, p_drop, seed, nullptr, 0, 0, split);
   }
 }
 
@@ -930,6 +943,11 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
     attr = true;
   }
   const int nwg = tile_lim > 0 ? tile_lim : ((M + 255) / 256) * ((N + 255) / 256);
+  static const bool split_remap = [] {
+    const char* e = getenv("MIPIPE_G3_SPLIT_REMAP");
+    return !(e && e[0] == '0');
+  }();
+  if (tile_lim == 0 && !split_remap) tile_lim = -1;
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
                                           (const bf16_t*)R, (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed,
                                           tile_lim);
