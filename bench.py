@@ -874,7 +874,8 @@ def run(a) -> None:
         conc = _concurrency_record(trainer)
         if world > 1:
             allc = [None] * world
-            dist.all_gather_object(allc, conc)
+            # over the gloo control group (host objects; no device tensors on the RCCL group)
+            dist.all_gather_object(allc, conc, group=trainer.mesh.world_ctrl)
         else:
             allc = [conc]
     out = {
