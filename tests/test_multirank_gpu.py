@@ -161,3 +161,22 @@ def test_multirank_lanes_keep_the_clip_norm(split_head, extra):
     # (without the fix the first step's norm is 2 % off: the tied / replicated part counted unreduced)
     assert res["2"]["norms"] == pytest.approx(res["1"]["norms"], rel=5e-3), (res["2"]["norms"], res["1"]["norms"])
     assert res["2"]["losses"] == pytest.approx(res["1"]["losses"], rel=2e-3)
+
+
+def test_multirank_stash_ring_zbh1_and_interleaved_train_like_gpipe():
+    """The stash ring with split backwards (ZBH1: a stash's last reader is W) and with two
+    virtual stages per rank (interleaved, v = 2, 8 layers): the same losses as GPipe over 3
+    steps (HIP graphs, 4 ranks, m = 16), fewer slots than GPipe's 16 per stage on every rank
+    and a lower HBM peak on the last rank."""
+    res = {}
+    for sched, extra in (("GPipe", ()), ("ZBH1", ()), ("Interleaved1F1B", ("--vstages", "2"))):
+        res[sched] = _run(4, "--schedule", sched, "--layers", "8", "--graphs", "1", "--split-head", "1",
+                          "--microbatches", "16", "--mem", "1", "--steps", "3", *extra,
+                          port=29980 + len(sched), extra_env={"MIPIPE_HEAD_MAX_LAG": "0"})
+    g = res["GPipe"]
+    for sched in ("ZBH1", "Interleaved1F1B"):
+        r = res[sched]
+        assert r["losses"] == pytest.approx(g["losses"], rel=2e-3), (sched, r["losses"], g["losses"])
+        nst = 2 if sched == "Interleaved1F1B" else 1
+        assert all(s_ < 16 * nst for s_ in r["mem"]["stash_slots"]), (sched, r["mem"])
+        assert r["mem"]["peak_above_init"][3] < g["mem"]["peak_above_init"][3], (sched, r["mem"], g["mem"])
