@@ -206,6 +206,17 @@ __device__ __forceinline__ float gelu_tanh_grad(float x) {
   return sg + 2.0f * x * sg * (1.0f - sg) * k0 * (1.0f + 3.0f * k1 * x2);
 }
 
+// GELU and its derivative from one sigmoid: the forward GEMM epilogue saves the derivative
+// (bf16) for the backward, whose dX epilogue is then a plain multiply (no exp / rcp there)
+__device__ __forceinline__ void gelu_tanh_and_grad(float x, float& g, float& d) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  const float x2 = x * x;
+  const float u = k0 * (x + k1 * x2 * x);
+  const float sg = sigmoid_fast(2.0f * u);
+  g = x * sg;
+  d = sg + 2.0f * x * sg * (1.0f - sg) * k0 * (1.0f + 3.0f * k1 * x2);
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 
 }  // namespace mp

@@ -233,14 +233,20 @@ __global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__
         for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[e]);
       }
       if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
-        u16x8 pre;
+        u16x8 sv;   // ReLU: the pre-activation; GELU: its derivative (gemm2.hip epi_store8)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          pre[e] = f2bf(v[e]);
-          const float x = bf2f(pre[e]);  // activation of exactly what is saved for the backward
-          v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
+          const float x = bf2f(f2bf(v[e]));
+          if constexpr (EPI == EPI_BIAS_GELU) {
+            float d;
+            gelu_tanh_and_grad(x, v[e], d);
+            sv[e] = f2bf(d);
+          } else {
+            sv[e] = f2bf(x);
+            v[e] = fmaxf(x, 0.f);
+          }
         }
-        *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
+        *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = sv;
       }
       if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
         u16x8 rv = *reinterpret_cast<const u16x8*>(R + (int64_t)gr * ldr + gc);
@@ -252,7 +258,7 @@ __global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float x = bf2f(xv[e]);
-          v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
+          v[e] *= EPI == EPI_DGELU ? x : (x > 0.f ? 1.f : 0.f);
         }
       }
       u16x8 o;

@@ -164,17 +164,27 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int gr, int gc, bf16_t
     for (int e = 0; e < 8; ++e) v[e] += bf2f(bv[e]);
   }
   if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_RELU) {
-    u16x8 pre;
+    // AUX: what the backward's dX epilogue needs -- the pre-activation for ReLU (its sign),
+    // GELU's derivative for GELU (computed here beside the activation from one sigmoid, so
+    // the backward multiplies instead of re-evaluating it: dGELU dX 505 -> ~440 us at 64K x
+    // 3072, profiles/r5_gemm_epilogue_cost.md)
+    u16x8 sv;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      pre[e] = f2bf(v[e]);
-      const float x = bf2f(pre[e]);
-      v[e] = EPI == EPI_BIAS_GELU ? gelu_tanh(x) : fmaxf(x, 0.f);
+      const float x = bf2f(f2bf(v[e]));   // the activation of the bf16-rounded pre-activation
+      if constexpr (EPI == EPI_BIAS_GELU) {
+        float d;
+        gelu_tanh_and_grad(x, v[e], d);
+        sv[e] = f2bf(d);
+      } else {
+        sv[e] = f2bf(x);
+        v[e] = fmaxf(x, 0.f);
+      }
       // dropout after the activation (the reference FFN's drop(relu(.))), mask index =
       // element index of the contiguous output, as act_fwd / act_bwd regenerate it
       if (p_drop > 0.f) v[e] *= dropout_scale(seed, (uint64_t)gr * ldc + gc + e, p_drop);
     }
-    *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = pre;
+    *reinterpret_cast<u16x8*>(AUX + (int64_t)gr * ldx + gc) = sv;
   }
   if constexpr (EPI == EPI_BIAS_RES || EPI == EPI_RES) {
     u16x8 rv = *reinterpret_cast<const u16x8*>(R + (int64_t)gr * ldr + gc);
@@ -185,8 +195,8 @@ __device__ __forceinline__ void epi_store8(float (&v)[8], int gr, int gc, bf16_t
     u16x8 xv = *reinterpret_cast<const u16x8*>(AUX + (int64_t)gr * ldx + gc);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float x = bf2f(xv[e]);
-      v[e] *= EPI == EPI_DGELU ? gelu_tanh_grad(x) : (x > 0.f ? 1.f : 0.f);
+      const float x = bf2f(xv[e]);   // GELU: the saved derivative; ReLU: the pre-activation
+      v[e] *= EPI == EPI_DGELU ? x : (x > 0.f ? 1.f : 0.f);
       if (p_drop > 0.f) v[e] *= dropout_scale(seed, (uint64_t)gr * ldc + gc + e, p_drop);
     }
   }

@@ -326,8 +326,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
            residual: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None,
            aux: Optional[torch.Tensor] = None, p_drop: float = 0.0, seed: int = 0):
     """y = drop(act(x @ w^T + bias)) (+ residual).  x [T,K], w [N,K].  With an activation
-    the pre-activation is written to ``aux`` (needed by the backward); ``p_drop`` (ReLU
-    only) applies the fused dropout of the reference FFN.  Returns (y, aux)."""
+    ``aux`` receives what the backward's dX epilogue needs (``linear_dx(act_input=aux)``):
+    the pre-activation for ReLU, GELU's derivative at the pre-activation for GELU (one
+    sigmoid serves both here; the backward then multiplies).  ``p_drop`` (ReLU only) applies
+    the fused dropout of the reference FFN.  Returns (y, aux)."""
     if p_drop > 0 and act != "relu":
         raise ValueError("the fused GEMM dropout follows a ReLU epilogue")
     T, K = x.shape
@@ -369,7 +371,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
         y = y + bias.float()
     if act != "none":
         pre = y.to(x.dtype)
-        aux.copy_(pre)
+        aux.copy_(_act_grad_cpu(pre.float(), act) if ACT[act] == 1 else pre)
         y = _act_cpu(pre.float(), act)
         if p_drop > 0:
             y = y * _cpu_dropout_mask(y.shape, p_drop, seed, y.device)
@@ -414,9 +416,10 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
               out: Optional[torch.Tensor] = None, residual: Optional[torch.Tensor] = None,
               wt: Optional[torch.Tensor] = None, colsum: Optional[torch.Tensor] = None, p_drop: float = 0.0,
               seed: int = 0):
-    """dx = dy @ w  (w [N,K]), optionally times act'(act_input) (the previous layer's
-    pre-activation) and plus ``residual``.  With ``wt`` (= w^T, [K,N], kept by the param
-    arena) the GEMM runs in the both-K-contiguous form on the v2 engine."""
+    """dx = dy @ w  (w [N,K]), optionally times act'(.) given by ``act_input`` -- what
+    ``linear(act=...)`` saved in ``aux``: ReLU's pre-activation, or GELU's derivative itself
+    -- and plus ``residual``.  With ``wt`` (= w^T, [K,N], kept by the param arena) the GEMM
+    runs in the both-K-contiguous form on the v2 engine."""
     T, N = dy.shape
     K = w.shape[1]
     if out is None:
@@ -470,7 +473,7 @@ def linear_dx(dy: torch.Tensor, w: torch.Tensor, act_input: Optional[torch.Tenso
         return out
     g = dy.float() @ w.float()
     if act != "none":
-        g = g * _act_grad_cpu(act_input.float(), act)
+        g = g * (act_input.float() if ACT[act] == 1 else _act_grad_cpu(act_input.float(), act))
         if p_drop > 0:
             g = g * _cpu_dropout_mask(g.shape, p_drop, seed, g.device)
     if residual is not None:

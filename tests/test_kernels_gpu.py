@@ -25,6 +25,13 @@ def rnd(*shape, scale=1.0, dtype=torch.bfloat16):
     return (torch.randn(*shape) * scale).to(dtype)
 
 
+def gelu_grad_ref(a):
+    """d/dx of tanh-GELU (f32), what the GELU GEMM epilogue saves for the backward."""
+    k0, k1 = 0.7978845608028654, 0.044715
+    t = torch.tanh(k0 * (a + k1 * a ** 3))
+    return 0.5 * (1 + t) + 0.5 * a * (1 - t * t) * k0 * (1 + 3 * k1 * a * a)
+
+
 def close(a, b, atol=2e-2, rtol=2e-2):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), atol=atol, rtol=rtol)
 
@@ -422,15 +429,13 @@ def test_gemm2_configs(cfg, M, N, K, epi):
     if "bias" in epi:
         ref = ref + b.float()
     if epi == "bias_gelu":
-        close(aux, ref.to(torch.bfloat16))
+        # aux: GELU's derivative at the (bf16-rounded) pre-activation
+        close(aux, gelu_grad_ref(ref.to(torch.bfloat16).float()).to(torch.bfloat16))
         ref = torch.nn.functional.gelu(ref.to(torch.bfloat16).float(), approximate="tanh")
     if epi == "res":
         ref = ref + r.float()
     if epi == "dgelu":
-        a = aux.float().cpu()
-        k0, k1 = 0.7978845608028654, 0.044715
-        t = torch.tanh(k0 * (a + k1 * a ** 3))
-        ref = ref * (0.5 * (1 + t) + 0.5 * a * (1 - t * t) * k0 * (1 + 3 * k1 * a * a))
+        ref = ref * aux.float().cpu()          # aux holds the saved GELU derivative
     close(y, ref)
 
 
@@ -461,15 +466,13 @@ def test_gemm7_stream_k(M, N, K, epi):
     if "bias" in epi:
         ref = ref + b.float()
     if epi == "bias_gelu":
-        close(aux, ref.to(torch.bfloat16))
+        # aux: GELU's derivative at the (bf16-rounded) pre-activation
+        close(aux, gelu_grad_ref(ref.to(torch.bfloat16).float()).to(torch.bfloat16))
         ref = torch.nn.functional.gelu(ref.to(torch.bfloat16).float(), approximate="tanh")
     if epi == "res":
         ref = ref + r.float()
     if epi == "dgelu":
-        a = aux.float().cpu()
-        k0, k1 = 0.7978845608028654, 0.044715
-        t = torch.tanh(k0 * (a + k1 * a ** 3))
-        ref = ref * (0.5 * (1 + t) + 0.5 * a * (1 - t * t) * k0 * (1 + 3 * k1 * a * a))
+        ref = ref * aux.float().cpu()          # aux holds the saved GELU derivative
     close(y, ref)
     if cs is not None:
         torch.testing.assert_close(cs.cpu(), y.float().sum(0).cpu(), rtol=2e-2, atol=2e-1 * M ** 0.5 * 1e-1)

@@ -92,7 +92,11 @@ def test_linear_family_matches_autograd():
     (y * dy).sum().backward()
     yo, aux = ops.linear(x, w, b, act="gelu_tanh")
     torch.testing.assert_close(yo, y.detach(), atol=1e-5, rtol=1e-5)
-    da = ops.act_bwd(dy, aux, "gelu_tanh", dbias=(db := torch.zeros(N)))
+    # GELU: aux is the derivative at the pre-activation (act_bwd takes the pre-activation)
+    p0 = pre.detach()
+    torch.testing.assert_close(aux, torch.autograd.functional.jvp(lambda t: F.gelu(t, approximate="tanh"), p0,
+                                                                  torch.ones_like(p0))[1], atol=1e-5, rtol=1e-5)
+    da = ops.act_bwd(dy, p0, "gelu_tanh", dbias=(db := torch.zeros(N)))
     torch.testing.assert_close(db, ba.grad, atol=1e-4, rtol=1e-4)
     dw = ops.linear_dw(da, x, torch.zeros(N, K))
     torch.testing.assert_close(dw, wa.grad, atol=1e-4, rtol=1e-4)
@@ -102,7 +106,7 @@ def test_linear_family_matches_autograd():
     w2 = f32(5, N)
     dz = f32(T, 5)
     fused = ops.linear_dx(dz, w2, act_input=aux, act="gelu_tanh")
-    unf = ops.act_bwd(ops.linear_dx(dz, w2), aux, "gelu_tanh")
+    unf = ops.act_bwd(ops.linear_dx(dz, w2), p0, "gelu_tanh")
     torch.testing.assert_close(fused, unf, atol=1e-5, rtol=1e-5)
     yr, _ = ops.linear(x, w, b, residual=r)
     torch.testing.assert_close(yr, x @ w.t() + b + r, atol=1e-5, rtol=1e-5)
