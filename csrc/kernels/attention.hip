@@ -74,6 +74,15 @@ __device__ __forceinline__ bf16x8 cat44(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
+// max of three as ONE v_max3_f32: fmaxf on MFMA outputs makes the compiler canonicalise
+// each input first (an extra v_max_f32 x, x, x per score under IEEE mode, ~32 per tile);
+// scores are never signalling NaNs here (MI355X_MICROARCH.md: canonicalising v_max)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
@@ -146,7 +155,8 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
   const int mb = CAUSAL ? (nmb - 1 - lin / nbh) : (int)blockIdx.x;
   const int bh = CAUSAL ? lin % nbh : (int)blockIdx.y;
   const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // wave-uniform: scalar branches
   const int m0 = mb * 128;
   const int qrow = m0 + 32 * w + l32;  // this lane's query
   const bool qvalid = qrow < Sq;
@@ -219,7 +229,7 @@ __global__ void __launch_bounds__(256, DP <= 128 ? 2 : 1) attn_fwd_kernel(
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+      for (int r = 0; r < 16; ++r) mx = max3_raw(mx, s0[r], s1[r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run, mx * c);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
@@ -408,7 +418,7 @@ __global__ void __launch_bounds__(256, 2) attn_fwd_ks2_kernel(
       }
       float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+      for (int r = 0; r < 16; ++r) mx = max3_raw(mx, s0[r], s1[r]);
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float m_new = fmaxf(m_run, mx * c);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
