@@ -217,6 +217,15 @@ __device__ __forceinline__ void gelu_tanh_and_grad(float x, float& g, float& d) 
   d = sg + 2.0f * x * sg * (1.0f - sg) * k0 * (1.0f + 3.0f * k1 * x2);
 }
 
+// max of three as ONE v_max3_f32.  fmaxf makes the compiler canonicalise each input first
+// (an extra v_max_f32 x, x, x per value under IEEE mode: 32 per attention tile, ~2 per logit
+// in the fused CE); the values here are never signalling NaNs (MI355X_MICROARCH.md)
+__device__ __forceinline__ float max3_raw(float a, float b, float c) {
+  float r;
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 __device__ __forceinline__ float silu(float x) { return x / (1.0f + __expf(-x)); }
 
 }  // namespace mp

@@ -74,15 +74,6 @@ __device__ __forceinline__ bf16x8 cat44(s16x4 lo, s16x4 hi) {
   return __builtin_bit_cast(bf16x8, r);
 }
 
-// max of three as ONE v_max3_f32: fmaxf on MFMA outputs makes the compiler canonicalise
-// each input first (an extra v_max_f32 x, x, x per score under IEEE mode, ~32 per tile);
-// scores are never signalling NaNs here (MI355X_MICROARCH.md: canonicalising v_max)
-__device__ __forceinline__ float max3_raw(float a, float b, float c) {
-  float r;
-  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
 __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
