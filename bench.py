@@ -696,8 +696,11 @@ def _concurrency_record(trainer) -> dict:
     for name in ("dp_engine", "embed_engine"):
         e = getattr(trainer.coll, name, None)
         comms += int(e.channels) if e is not None else 0
+    au = getattr(trainer, "comm_audit", None)
     return {"queue_probe": probe, "rccl_communicators": comms, "lanes": int(getattr(trainer, "lanes", 1)),
-            "p2p_channels": int(getattr(rt.p2p, "channels", 1)), "collective_placement": rt.coll_placement}
+            "p2p_channels": int(getattr(rt.p2p, "channels", 1)), "collective_placement": rt.coll_placement,
+            # first-step cross-rank check of the issued p2p order and collective sequences
+            "comm_audit": None if au is None else (f"ok ({au['entries']} groups)" if au["ok"] else au["problems"])}
 
 
 def _memory_plan_summary(trainer):

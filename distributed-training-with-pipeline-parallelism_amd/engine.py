@@ -626,6 +626,7 @@ class PipelineTrainer:
             inputs = [(c,) for c in torch.tensor_split(tokens, self.m, dim=0)]
         tg = list(torch.tensor_split(targets, self.m, dim=0)) if self.is_last else None
         losses: List[torch.Tensor] = []
+        audit = self._begin_comm_audit()
         self.runtime.step(inputs, tg, losses, return_outputs=False)
         if self._tie_local:
             by_idx = {st.stage_index: st for st in self.stages}
@@ -640,10 +641,41 @@ class PipelineTrainer:
             self.coll.all_reduce(parts, "pp").wait()
             losses = list(parts / (self.mbs * self.S))
         self.optimizer.step(lr)
+        if audit is not None:
+            self._end_comm_audit(audit)
         self.last_losses = losses
         if losses:
             return torch.stack(losses).mean()
         return None
+
+    # ------------------------------------------------------------------ comm audit
+    comm_audit: Optional[dict] = None
+
+    def _begin_comm_audit(self):
+        """First training step of a multi-rank job (MIPIPE_COMM_AUDIT=0: never): log every
+        p2p post and collective this rank issues (parallel/audit.py)."""
+        if (self.comm_audit is not None or self.mesh.world <= 1 or not dist.is_initialized()
+                or os.environ.get("MIPIPE_COMM_AUDIT", "1") == "0"):
+            return None
+        from .parallel.audit import CommAudit
+        audit = CommAudit(self.mesh.rank)
+        self.runtime.p2p.audit = audit
+        if self.coll is not None:
+            self.coll.audit = audit
+        return audit
+
+    def _end_comm_audit(self, audit) -> None:
+        """Exchange the logs over the gloo control group and check p2p order per pair and
+        channel and collective sequences per group; raise on the first divergence."""
+        from .parallel.audit import gather_and_check
+        self.runtime.p2p.audit = None
+        if self.coll is not None:
+            self.coll.audit = None
+        ok, problems, n = gather_and_check(audit, self.mesh.world_ctrl)
+        self.comm_audit = {"ok": ok, "entries": n, "problems": problems}
+        if not ok:
+            raise RuntimeError("communication issued by the ranks does not match (would hang under RCCL):\n  "
+                               + "\n  ".join(problems))
 
     def describe(self) -> str:
         """Hang report (utils/metrics.Watchdog): the runtime's program grid plus, for every

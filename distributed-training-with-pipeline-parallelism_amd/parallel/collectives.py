@@ -134,6 +134,20 @@ class Collectives:
             self.dp_kind = "native" if self.dp_engine is not None else "torch"
         else:
             self.dp_kind = "none"
+        self.audit = None   # parallel/audit.CommAudit while a step is audited
+
+    def _members(self, scope: str) -> list:
+        """Global ranks of a scope's group (mesh layout: rank = dp_rank * pp + pp_rank)."""
+        d, s = self.mesh.dp_rank, self.mesh.pp_rank
+        if scope == "pp":
+            return [d * self.pp + i for i in range(self.pp)]
+        if scope == "embed":
+            return sorted({d * self.pp, d * self.pp + self.pp - 1})
+        return [i * self.pp + s for i in range(self.dp)]
+
+    def _log(self, scope: str, op: str, t: torch.Tensor) -> None:
+        if self.audit is not None:
+            self.audit.coll(scope, self._members(scope), op, t)
 
     def _dp_native_wanted(self) -> bool:
         """This rank's own view: RCCL backend on a GPU and a native pipeline engine (or no
@@ -198,6 +212,7 @@ class Collectives:
         """In-place all-reduce (``op`` sum | max)."""
         if self._size(scope) <= 1:
             return _Done()
+        self._log(scope, "all_reduce_" + op, t)
         eng, _ = self._engine(scope)
         if eng is not None:
             return self._native(scope, ALLREDUCE_SUM if op == "sum" else ALLREDUCE_MAX, t, t)
@@ -214,6 +229,7 @@ class Collectives:
         shard = full[r * n:(r + 1) * n]
         if n_ranks <= 1:
             return _Done(), shard
+        self._log(scope, "reduce_scatter", full)
         eng, _ = self._engine(scope)
         if eng is not None:
             return self._native(scope, REDUCE_SCATTER_SUM, full, shard), shard
@@ -236,6 +252,7 @@ class Collectives:
         r = self.mesh.pp_rank if scope == "pp" else self.mesh.dp_rank
         n = full.numel() // n_ranks
         shard = full[r * n:(r + 1) * n]
+        self._log(scope, "all_gather", full)
         eng, _ = self._engine(scope)
         if eng is not None:
             return self._native(scope, ALL_GATHER, shard, full)

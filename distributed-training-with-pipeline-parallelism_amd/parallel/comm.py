@@ -223,6 +223,7 @@ class P2P:
         self.channels = 1
         self.fallback_reason = ""
         self._live: List = []       # native works of the current step (release_works)
+        self.audit = None           # parallel/audit.CommAudit while a step is audited
         capable = (device.type == "cuda" and dist.is_initialized() and not self.host_staged and len(self.ranks) > 1)
         if mode != "torch" and capable:
             timeout = preflight_timeout if preflight_timeout is not None else \
@@ -294,6 +295,9 @@ class P2P:
             for ch in sorted(set(sc) | set(rc)):
                 s_ = [sends[i] for i in range(len(sends)) if sc[i] == ch]
                 r_ = [recvs[i] for i in range(len(recvs)) if rc[i] == ch]
+                if self.audit is not None:
+                    self.audit.p2p(ch, [(t, self.global_rank(p)) for t, p in s_],
+                                   [(t, self.global_rank(p)) for t, p in r_])
                 h = self.engine.post(ch, s_, r_)
                 slot = rec.native_post(self.engine, ch, s_, r_) if rec is not None else -1
                 w = _NativeWork(self.engine, h, rec, slot)
@@ -305,6 +309,8 @@ class P2P:
                     if rc[i] == ch:
                         works_r[i] = w
             return works_s, works_r
+        if self.audit is not None and (sends or recvs):
+            self.audit.p2p(0, [(t, self.global_rank(p)) for t, p in sends], [(t, self.global_rank(p)) for t, p in recvs])
         if rec is not None:
             # transfers through torch.distributed replay as CALLs on the same tensors
             ns = len(sends)

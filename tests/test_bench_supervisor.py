@@ -231,7 +231,8 @@ def test_bench_four_ranks_measures_all_three_schedules():
     # every rank's live concurrency features (VERDICT r4 #6c): one entry per rank
     conc = out["per_rank_concurrency"]
     assert len(conc) == 4 and all(set(c) >= {"queue_probe", "rccl_communicators", "lanes", "p2p_channels",
-                                             "collective_placement"} for c in conc), conc
+                                             "collective_placement", "comm_audit"} for c in conc), conc
+    assert all(str(c["comm_audit"]).startswith("ok (") for c in conc), conc
     assert dt < 540, dt
 
 

@@ -48,7 +48,7 @@ def _train(name, pp, dp, schedule, steps=2, split_head=None, layer_ranges="auto"
         if l is not None:
             losses.append(float(l))
     sd = {k: v.numpy().copy() for k, v in tr.state_dict().items()}
-    return dict(losses=losses, sd=sd)
+    return dict(losses=losses, sd=sd, audit=tr.comm_audit)
 
 
 def _worker(rank, world, name, pp, dp, schedule, split_head=None, layer_ranges="auto", max_grad_norm=1.0,
@@ -393,3 +393,36 @@ def test_pick_microbatch_uses_rates_measured_for_the_model():
     p = rate_probe_config(NativeConfig.llama3("8b"), 8)
     assert p.n_layers == 4 and p.vocab_size >= 128256 // 8 and p.vocab_size % 128 == 0
     assert p.vocab_padded >= p.vocab_size
+
+
+def test_first_step_comm_audit_passes_on_every_rank():
+    """the first step's issued p2p (per pair and channel, in order) and
+    collectives (per group) agree across all ranks -- DP = 2 x PP = 2 with the distributed
+    head exercises pipeline p2p, the head reductions, the DP gradient and the clip norm."""
+    res = run_world(_worker, 4, "gpt2", 2, 2, "1F1B", True)
+    for r in range(4):
+        a = res[r]["audit"]
+        assert a is not None and a["ok"] and a["problems"] == [], (r, a)
+        assert a["entries"] > 0
+
+
+def test_comm_audit_finds_order_and_collective_mismatches():
+    """parallel/audit.check: a send order that differs from the receiver's, a missing
+    receive and a collective sequence that differs within its group are each reported."""
+    from mipipe.parallel.audit import check
+    f32 = "float32"
+    ok = {0: [("p2p", 0, ((1, 64, f32),), ()), ("p2p", 0, ((1, 32, f32),), ()),
+              ("coll", "pp", (0, 1), "all_reduce_sum", 8, f32)],
+          1: [("p2p", 0, (), ((0, 64, f32),)), ("p2p", 0, (), ((0, 32, f32),)),
+              ("coll", "pp", (0, 1), "all_reduce_sum", 8, f32)]}
+    assert check(ok) == []
+    swapped = {0: ok[0], 1: [ok[1][1], ok[1][0], ok[1][2]]}
+    p = check(swapped)
+    assert len(p) == 1 and p[0].startswith("p2p 0->1 channel 0") and "#0" in p[0], p
+    missing = {0: ok[0], 1: [ok[1][0], ok[1][2]]}
+    assert any("2 sends vs 1 receives" in x for x in check(missing))
+    coll = {0: ok[0], 1: ok[1][:2] + [("coll", "pp", (0, 1), "all_gather", 8, f32)]}
+    assert any(x.startswith("pp collectives over [0, 1]") for x in check(coll))
+    # another channel is another match queue
+    ch = {0: [("p2p", 1, ((1, 64, f32),), ())], 1: [("p2p", 0, (), ((0, 64, f32),))]}
+    assert len(check(ch)) == 2
