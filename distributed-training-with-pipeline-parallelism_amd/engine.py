@@ -683,7 +683,15 @@ class PipelineTrainer:
         from .parallel.comm import comm_progress_report
         eng = {"p2p": getattr(self.runtime.p2p, "engine", None),
                "dp": getattr(self.coll, "dp_engine", None), "embed": getattr(self.coll, "embed_engine", None)}
-        return self.runtime.describe() + "\n" + comm_progress_report(eng)
+        out = self.runtime.describe() + "\n" + comm_progress_report(eng)
+        audit = getattr(self.runtime.p2p, "audit", None)
+        if audit is not None:
+            # stalled inside the audited first step: what this rank issued so far, in order
+            # (compare across the ranks' reports: the first entry without a partner blocks)
+            tail = audit.entries[-8:]
+            out += f"\n[comm audit] {len(audit.entries)} issued this step; last {len(tail)}:\n" + \
+                "\n".join(f"[comm audit]   {e}" for e in tail)
+        return out
 
     def capture_graphs(self, tokens: Optional[torch.Tensor] = None, targets: Optional[torch.Tensor] = None) -> None:
         """Setup, not training: run the pipeline program twice without an optimizer step
