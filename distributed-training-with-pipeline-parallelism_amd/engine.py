@@ -627,7 +627,14 @@ class PipelineTrainer:
         tg = list(torch.tensor_split(targets, self.m, dim=0)) if self.is_last else None
         losses: List[torch.Tensor] = []
         audit = self._begin_comm_audit()
-        self.runtime.step(inputs, tg, losses, return_outputs=False)
+        try:
+            self.runtime.step(inputs, tg, losses, return_outputs=False)
+        except BaseException:
+            if audit is not None:     # a failed step leaves no logger attached
+                self.runtime.p2p.audit = None
+                if self.coll is not None:
+                    self.coll.audit = None
+            raise
         if self._tie_local:
             by_idx = {st.stage_index: st for st in self.stages}
             g0 = by_idx[0].arena.g("tok_embeddings.weight")
