@@ -226,7 +226,11 @@ def test_bench_four_ranks_measures_all_three_schedules():
     head = out["config"]["schedule"]
     assert out["value"] == sch[head]["tok_s"] and set(out["config"]["schedule_choice"]["auto"]) == set(sch)
     eff = out["config"]["schedule_choice"]["auto"]
-    assert eff[head] == max(eff.values()) or (head == "1F1B" and max(eff.values()) < 1.03 * eff["1F1B"])
+    # the best plan among candidates that beat 1F1B by their margin (3 % with more p2p
+    # than 1F1B -- interleaved v > 1 --, 1 % with the same messages), else 1F1B
+    v_of = {k: e["v"] for k, e in sch.items()}
+    beats = [k for k in eff if k != "1F1B" and eff[k] >= eff["1F1B"] * (1.03 if v_of.get(k, 1) > 1 else 1.01)]
+    assert head == (max(beats, key=lambda k: eff[k]) if beats else "1F1B"), (head, eff, v_of)
     assert out["p2p_bytes_per_step"] > 0 and "rccl_ranks" in out
     # every rank's live concurrency features (VERDICT r4 #6c): one entry per rank
     conc = out["per_rank_concurrency"]

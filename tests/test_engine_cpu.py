@@ -375,7 +375,8 @@ def test_trainer_auto_schedule():
     tr = PipelineTrainer(cfg, pp=1, schedule="auto", n_microbatches=2, mbs=2, seq_len=16, device="cpu")
     assert tr.schedule == "1F1B" and tr.schedule_choice == {}
     name, eff = pick_schedule(NativeConfig.by_name("gpt2-small"), 2, 8, 32, 1024)
-    assert name in eff and eff[name] == max(eff.values()) or (name == "1F1B" and max(eff.values()) < 1.03 * eff["1F1B"])
+    beats = [k for k in eff if k != "1F1B" and eff[k] >= eff["1F1B"] * 1.01]
+    assert name in eff and (name == max(beats, key=lambda k: eff[k]) if beats else name == "1F1B"), (name, eff)
 
 
 def test_pick_microbatch_uses_rates_measured_for_the_model():
