@@ -47,7 +47,7 @@ def _sleep_worker(rank, world, m, sched, tf, tb):
     targets = [torch.zeros(4) for _ in range(m)] if rank == world - 1 else None
     rt.step(inputs, targets, [], return_outputs=False)
     out = []
-    for _ in range(2):
+    for _ in range(3):   # min over 3: a loaded machine (parallel test workers) only adds time
         dist.barrier()
         rt.profile = True
         rt.step(inputs, targets, [], return_outputs=False)

@@ -10,9 +10,12 @@ from mipipe.bench import compat
 
 
 @pytest.mark.parametrize("engine", ["torch", "native"])
-def test_run_one_experiment(engine):
+def test_run_one_experiment(engine, monkeypatch):
+    # spawned ranks re-import torch; under a parallel test run (xdist) with every rank
+    # taking all cores this took > 300 s: two threads per rank and a longer deadline
+    monkeypatch.setenv("OMP_NUM_THREADS", "2")
     m = compat.run_one_experiment(4, 4, 2, "1F1B", batch_size=8, seq_length=16, num_iterations=1, device="cpu",
-                                  engine=engine, timeout=300)
+                                  engine=engine, timeout=900)
     assert "error" not in m, m
     assert m["tokens_processed"] == 8 * 16 * 1 and m["throughput"] > 0
 
