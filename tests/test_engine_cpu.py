@@ -427,3 +427,20 @@ def test_comm_audit_finds_order_and_collective_mismatches():
     # another channel is another match queue
     ch = {0: [("p2p", 1, ((1, 64, f32),), ())], 1: [("p2p", 0, (), ((0, 64, f32),))]}
     assert len(check(ch)) == 2
+
+
+def test_schedule_margin_depends_on_traffic():
+    """pick_schedule: a candidate that sends exactly 1F1B's messages (ZBH1, GPipe, v = 1
+    interleaved) needs a 1 % better plan, one that sends more (interleaved v > 1) 3 %.
+    GPT-2 small at P = 8 with 16-sequence microbatches: ZBH1 plans 2.7 % over 1F1B and is
+    taken; with a 3 % margin for every candidate it would not be."""
+    from mipipe.engine import pick_schedule
+    from mipipe.models.config import NativeConfig
+    cfg = NativeConfig.by_name("gpt2-small")
+    name, eff = pick_schedule(cfg, 8, 64, 16, 1024, candidates=("1F1B", "ZBH1"))
+    assert 1.01 <= eff["ZBH1"] / eff["1F1B"] < 1.03 and name == "ZBH1", eff
+    name3, _ = pick_schedule(cfg, 8, 64, 16, 1024, candidates=("1F1B", "ZBH1"), same_traffic_margin=0.03)
+    assert name3 == "1F1B"
+    # interleaved with two chunks per rank sends twice the activations: the full margin
+    name_i, eff_i = pick_schedule(cfg, 2, 8, 32, 1024, candidates=("1F1B", "Interleaved1F1B"))
+    assert eff_i["Interleaved1F1B"] < eff_i["1F1B"] * 1.03 and name_i == "1F1B", eff_i
