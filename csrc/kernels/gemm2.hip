@@ -628,7 +628,7 @@ gemm3_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* _
   // x % 8, which is wrong for y > 0 whenever gridDim.x % 8 != 0 and scattered the tiles that
   // share a panel over all XCDs (the dW GEMMs read ~4x their unique bytes from HBM)
   int wg, split;
-  if (gridDim.y > 1 && tile_lim == 0) {   // (tile_lim = -1: the x-only remap, MIPIPE_G3_SPLIT_REMAP=0)
+  if (gridDim.y > 1 && tile_lim == 0) {   // (tile_lim = -1: the x-only remap, the default)
     const int v = xcd_remap((int)blockIdx.x + (int)gridDim.x * (int)blockIdx.y, nwg * (int)gridDim.y);
     split = v / nwg;
     wg = v % nwg;
@@ -953,9 +953,12 @@ static int launch3(const void* A, const void* B, void* C, const void* bias, cons
     attr = true;
   }
   const int nwg = tile_lim > 0 ? tile_lim : ((M + 255) / 256) * ((N + 255) / 256);
+  // opt-in (MIPIPE_G3_SPLIT_REMAP=1): +3-10 % on GPT-2 small's dW GEMMs standalone, neutral
+  // in that step, but -0.8 % on the GPT-2 large step (2 same-box pairs,
+  // profiles/r5_gemm3_splitk_xcd_remap.md)
   static const bool split_remap = [] {
     const char* e = getenv("MIPIPE_G3_SPLIT_REMAP");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (tile_lim == 0 && !split_remap) tile_lim = -1;
   kern<<<dim3(nwg, split), NT, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias,
