@@ -58,6 +58,7 @@ int mp_attn_f32_bwd(const float* q, const float* k, const float* v, const float*
                     int64_t dvs, int causal, float scale, float p_drop, uint64_t seed, hipStream_t st);
 int mp_set_drop_step_attn_f32(uint64_t v, hipStream_t st);
 int mp_set_drop_step_gemm_f32(uint64_t v, hipStream_t st);
+int mp_gemm_f32_set_lanes(int lanes);
 int mp_transpose(const void* in, void* out, int R, int C, int64_t ldi, int64_t ldo, hipStream_t st);
 int mp_transpose_batched(const void* src, void* dst, const int64_t* desc, const int* tile0, int n, int total_tiles,
                          hipStream_t st);
@@ -634,6 +635,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("scaled_sum", &scaled_sum);
   m.def("zero_", &zero_);
   m.def("gemm_f32", &gemm_f32);
+  m.def("gemm_f32_set_lanes", &mp_gemm_f32_set_lanes);
   m.def("gemm_f32_ex", &gemm_f32_ex, pybind11::arg("A"), pybind11::arg("B"), pybind11::arg("C"), pybind11::arg("bias"),
         pybind11::arg("R"), pybind11::arg("X"), pybind11::arg("epi") = 0, pybind11::arg("alpha") = 1.0,
         pybind11::arg("accumulate") = false, pybind11::arg("p_drop") = 0.0, pybind11::arg("seed") = 0,

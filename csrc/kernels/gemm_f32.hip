@@ -565,14 +565,30 @@ static int launch_big(Args p, int split, hipStream_t st) {
 // plus ~1 for the slab pass.  Fitted to the measured s = 1..8 sweep of the reference's
 // GEMMs (profiles/r3_f32_gemm_sweep.json): e.g. dX of the LM head (192 tiles, 157 pairs)
 // -> 4, the forward out_proj (192 tiles, 12 pairs) -> 1.
+// CUs one GEMM can count on.  With L microbatch lanes replaying concurrently, each lane's
+// GEMM shares the chip with the others, so the split is planned for 256 / L CUs: fewer
+// slabs and reduce passes, whose only purpose was to fill CUs the other lanes now fill.
+// mp_gemm_f32_set_lanes (the runtime's set_lanes) sets it; MIPIPE_F32_CUS overrides it.
+static int g_lanes = 1;
+static int plan_cus() {
+  static const int env = [] {
+    const char* e = getenv("MIPIPE_F32_CUS");
+    return e ? atoi(e) : 0;
+  }();
+  if (env > 0) return env;
+  const int c = 256 / (g_lanes > 0 ? g_lanes : 1);
+  return c < 32 ? 32 : c;
+}
+
 static int pick_split(int M, int N, int K) {
   const int tiles = ((M + BT - 1) / BT) * ((N + BT - 1) / BT);
   const int npairs = (K + 2 * BK - 1) / (2 * BK);
+  const int cus = plan_cus();
   int best = 1;
   double best_cost = 1e30;
   for (int s = 1; s <= 8; ++s) {
     if (s > 1 && npairs < 2 * s) break;
-    const double rounds = (double)((tiles * s + 255) / 256);
+    const double rounds = (double)((tiles * s + cus - 1) / cus);
     const double cost = rounds * ((double)npairs / s + 3.0) + (s > 1 ? 1.0 : 0.0);
     if (cost < best_cost - 1e-9) {
       best_cost = cost;
@@ -735,3 +751,10 @@ extern "C" int mp_gemm_f32(const float* A, const float* B, float* C, const float
 }
 
 MP_DROP_STEP_SETTER(mp_set_drop_step_gemm_f32)
+
+// concurrent microbatch lanes the split-K planner assumes (see plan_cus); returns the CUs
+// it now plans for
+extern "C" int mp_gemm_f32_set_lanes(int lanes) {
+  gf32::g_lanes = lanes > 0 ? lanes : 1;
+  return gf32::plan_cus();
+}

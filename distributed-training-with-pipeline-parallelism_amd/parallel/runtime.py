@@ -348,6 +348,13 @@ class PipelineRuntime:
             check_lowered(self.program_all, self.num_stages, channels=getattr(self.p2p, "channels", 1), dp=self.dp,
                           lanes=n)
         self.lanes = n
+        if self.device.type == "cuda":
+            # the f32 split-K planner counts 256 / n CUs per GEMM: the other lanes fill the
+            # rest (+1.4 % on the reference fp32 workload with 4 lanes, r5_f32_lane_split.md)
+            from ..ops.kernels import load_ext
+            ext = load_ext()
+            if ext is not None and hasattr(ext, "gemm_f32_set_lanes"):
+                ext.gemm_f32_set_lanes(n)
         self.lane_streams += chosen[: n - 1]
         for st in self.stages.values():
             st.arena.set_lanes(n)
