@@ -1070,7 +1070,8 @@ def main():
     if n != world_env and world_env > 1 and not (a.phase == "ref" and a.ref_p == world_env):
         # (a reference child on ranks 0..P-1 of the launch runs with WORLD_SIZE = P)
         raise SystemExit(f"--gpus {n} but WORLD_SIZE={world_env}")
-    if os.environ.get("MIPIPE_BENCH_CHILD") != "1" and not a.no_supervise:
+    if os.environ.get("MIPIPE_BENCH_CHILD") != "1" and not a.no_supervise and a.phase == "sched":
+        # (an explicit internal --phase runs that phase here, e.g. under a profiler)
         # drop a --graphs the supervisor will set per attempt
         child_argv, skip = [], False
         for x in argv:
