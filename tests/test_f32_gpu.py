@@ -126,6 +126,30 @@ def test_gemm_f32_stream_k(M, N, K, layout, epi):
         close(C, 0.5 * ref + base.double().cpu(), atol=2e-4 * math.sqrt(K / 64), rtol=1e-5)
 
 
+@pytest.mark.parametrize("lanes", [1, 2, 4])
+def test_gemm_f32_lane_aware_split(lanes):
+    """The split-K planner counts 256 / lanes CUs (PipelineRuntime.set_lanes): the splits it
+    picks for the reference's 1024-token shapes change, the results do not (plain store and
+    f32 accumulate; the dX of the LM head has K = vocab = 10000)."""
+    e = ops.kernels._ext()
+    try:
+        assert e.gemm_f32_set_lanes(lanes) == 256 // lanes
+        torch.manual_seed(4)
+        for M, N, K in ((1024, 768, 10000), (1024, 768, 3072), (768, 3072, 1024), (1024, 2304, 768)):
+            a64, b64 = torch.randn(M, K, dtype=torch.float64), torch.randn(K, N, dtype=torch.float64) / math.sqrt(K)
+            A, B = a64.float().to(DEV), b64.float().to(DEV)
+            ref = a64.float().double() @ b64.float().double()
+            C = torch.full((M, N), float("nan"), device=DEV)
+            ops.kernels._gemm_f32(A, B, C)
+            close(C, ref, atol=2e-4 * math.sqrt(K / 64), rtol=1e-5)
+            base = torch.randn(M, N, device=DEV)
+            C.copy_(base)
+            ops.kernels._gemm_f32(A, B, C, alpha=0.5, accumulate=True)
+            close(C, 0.5 * ref + base.double().cpu(), atol=2e-4 * math.sqrt(K / 64), rtol=1e-5)
+    finally:
+        e.gemm_f32_set_lanes(1)
+
+
 def test_linear_dw_f32_matches_torch():
     torch.manual_seed(2)
     T, N, K = 1024, 2304, 768
