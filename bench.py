@@ -86,8 +86,17 @@ BASELINE_NOTE = ("no same-config reference number: BASELINE.md only has the refe
 ATTEMPTS = [("auto", 1), ("auto-safe", 1), ("torch", 1), ("torch", 0), ("gloo", 1)]
 # the reference's three schedules (helper:215-220), measured back to back in one call
 SCHEDULES = ("GPipe", "1F1B", "Interleaved1F1B")
-# ... and the ones measured next to them by --schedules all: the zero-bubble ZBH1 too
-ALL_SCHEDULES = SCHEDULES + ("ZBH1",)
+# ... and the entries measured next to them by --schedules all: 1F1B at the
+# reference's own warmup depth (P - s forwards, torch schedules.py:873-876: the distributed
+# head's lag capped at 0) next to 1F1B with the planner's head lag ("1F1B+lag"), and the
+# zero-bubble ZBH1.  Entry -> (schedule, extra argv).  A result is labelled by what it ran:
+# "<schedule>+lag<k>" when its head lag k > 0
+SCHED_VARIANTS = {"GPipe": ("GPipe", []), "1F1B": ("1F1B", ["--head-max-lag", "0"]), "1F1B+lag": ("1F1B", []),
+                  "Interleaved1F1B": ("Interleaved1F1B", []), "ZBH1": ("ZBH1", [])}
+ALL_SCHEDULES = ("GPipe", "1F1B", "1F1B+lag", "Interleaved1F1B", "ZBH1")
+# layers of the named models (the supervisor imports nothing: model_layers); "name:L" overrides
+MODEL_LAYERS = {"gpt2-tiny": 4, "gpt2": 12, "gpt2-small": 12, "gpt2-medium": 24, "gpt2-large": 36, "gpt2-xl": 48,
+                "llama3": 32, "llama3-8b": 32, "llama3-1b": 16, "llama3-tiny": 4}
 # the reference's 9 (L, H) configs (nb:346-349), L8 H8 first; its published rows are
 # mipipe.bench.published (nb:679-732) -- imported lazily: the
 # supervisor itself imports nothing that could touch HIP
@@ -185,7 +194,47 @@ def parse(argv=None):
                                                                   "no other schedules)")
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"], help="default bf16 on GPU, fp32 on CPU")
     ap.add_argument("--vocab", type=int, default=None, help="override the vocabulary (CPU tests)")
+    ap.add_argument("--head-max-lag", type=int, default=None,
+                    help="cap on the distributed head's lag (extra warmup forwards; 0 = the schedule's own depth)")
+    ap.add_argument("--compare-model", default="auto",
+                    help="model of the schedule comparison (``schedules``): 'same', a name ('name:L' = L layers), or "
+                         "auto: the headline model, unless it cannot interleave two chunks per rank at this pipeline "
+                         "size (fewer than 2P layers: GPT-2 small at P = 8), then the smallest GPT-2 that can")
     return ap.parse_args(argv)
+
+
+def model_layers(name: str):
+    base, _, L = name.partition(":")
+    return int(L) if L else MODEL_LAYERS.get(base.lower())
+
+
+def model_config(name: str, vocab=None):
+    """NativeConfig of ``name`` ('name:L': with L layers), vocabulary overridden by ``vocab``."""
+    from mipipe.models.config import NativeConfig
+    base, _, L = name.partition(":")
+    kw = {"vocab_size": vocab} if vocab else {}
+    if L:
+        kw["n_layers"] = int(L)
+    return NativeConfig.by_name(base, **kw)
+
+
+def compare_model(a, pp: int) -> str:
+    """The model the schedule comparison runs on (``--compare-model``): the reference's result
+    is GPipe vs 1F1B vs Interleaved at the same (L, H, P) (helper:215-220), so every entry
+    must be able to run the schedule it names -- interleaving needs 2P layers."""
+    cm = (a.compare_model or "auto").strip()
+    if cm == "same":
+        return a.model
+    if cm != "auto":
+        return cm
+    L = model_layers(a.model)
+    if pp <= 1 or L is None or L >= 2 * pp:
+        return a.model
+    if a.model.lower().startswith("gpt2"):
+        for cand in ("gpt2-medium", "gpt2-large", "gpt2-xl"):
+            if MODEL_LAYERS[cand] >= 2 * pp:
+                return cand
+    return a.model
 
 
 def extra_schedules(a) -> list:
@@ -195,7 +244,7 @@ def extra_schedules(a) -> list:
     elif s.lower() == "all":
         names = list(ALL_SCHEDULES)
     else:
-        names = [_canon(x) for x in s.split(",") if x.strip()]
+        names = [x.strip() if x.strip() in SCHED_VARIANTS else _canon(x) for x in s.split(",") if x.strip()]
     return names
 
 
@@ -301,9 +350,18 @@ def plan_phases(a, argv) -> list:
     headline's attempts first, then every other schedule of ``--schedules`` on the same
     model/config, then the reference's fp32 config per schedule."""
     tags = [(f"h{k}", "headline", list(argv), a.schedule) for k in range(max(1, a.max_attempts))]
-    # every schedule gets a slot; the one the headline ran (known once it is in) is skipped
+    # every comparison entry gets a slot (on the comparison model: compare_model); the one the
+    # headline ran (known once it is in: same model, planned lag) is skipped.  One GPU has no
+    # pipeline and no head lag: "1F1B+lag" would repeat "1F1B"
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    pp = max(1, world // max(1, a.dp))
+    cmodel = compare_model(a, pp)
     for s in extra_schedules(a):
-        tags.append((f"x_{s}", "sched", list(argv) + ["--schedule", s], s))
+        sched, extra = SCHED_VARIANTS.get(s, (s, []))
+        if s == "1F1B+lag" and pp == 1:
+            continue
+        margv = [] if cmodel == a.model else ["--model", cmodel]
+        tags.append((f"x_{s}", "sched", list(argv) + ["--schedule", sched] + extra + margv, s))
     if ref_fp32_on(a):
         world = int(os.environ.get("WORLD_SIZE", "1"))
         for P in ref_ps(world):
@@ -427,8 +485,10 @@ def supervise(a, argv) -> int:
                 b = attempt_budget(deadline - left(), deadline, cap)
                 if headline is None and k < len(attempts) and b > 0:
                     decision = f"go {b:.0f} {attempts[k][0]} {attempts[k][1]} {k}"
-            elif headline is not None and kind == "sched" and sched == headline["config"]["schedule"]:
-                pass        # the headline's own schedule: already measured
+            elif (headline is not None and kind == "sched" and SCHED_VARIANTS.get(sched, (sched, []))[1] == []
+                  and SCHED_VARIANTS.get(sched, (sched, []))[0] == headline["config"]["schedule"]
+                  and compare_model(a, pp) == a.model and a.head_max_lag is None):
+                pass        # the headline's own schedule (same model, planned lag): already measured
             elif headline is not None:
                 kb = kind
                 if kind == "base":
@@ -448,8 +508,9 @@ def supervise(a, argv) -> int:
         if not decision.startswith("go"):
             continue
         _, b, p2p, graphs, att = decision.split()
-        if kind == "headline" and int(att) >= 2 and _canon(a.schedule) == "auto":
-            # a planned schedule that failed twice is not retried: the later attempts run 1F1B
+        if kind == "headline" and int(att) >= 1 and _canon(a.schedule) == "auto":
+            # a planned schedule that failed once is not retried: the later attempts run 1F1B,
+            # the schedule every multi-rank test runs
             child_argv = list(child_argv) + ["--schedule", "1F1B"]
         sub = None
         if kind == "ref":
@@ -530,9 +591,8 @@ def run_rate(a) -> None:
     import mipipe  # noqa: F401
     from mipipe.engine import PipelineTrainer, rate_probe_config
     from mipipe.models.config import NativeConfig
-    kw = {"vocab_size": a.vocab} if a.vocab else {}
     pp = max(1, a.rate_pp or 1)
-    cfg = rate_probe_config(NativeConfig.by_name(a.model, **kw), pp)
+    cfg = rate_probe_config(model_config(a.model, a.vocab), pp)
     gpu = torch.cuda.is_available()
     dev = torch.device("cuda", 0) if gpu else torch.device("cpu")
     t0 = time.monotonic()
@@ -571,8 +631,7 @@ def run_plan(a) -> None:
     from mipipe.models.config import NativeConfig
     world = int(os.environ.get("WORLD_SIZE", "1"))
     pp = max(1, world // max(1, a.dp))
-    kw = {"vocab_size": a.vocab} if a.vocab else {}
-    cfg = NativeConfig.by_name(a.model, **kw)
+    cfg = model_config(a.model, a.vocab)
     t0 = time.monotonic()
     rates = json.loads(a.rates) if a.rates else None
     mbs, m, scores = pick_microbatch(cfg, pp, a.seq, 128 * pp, rates=rates)
@@ -584,12 +643,13 @@ def _sched_entry(r: dict) -> dict:
     if "error" in r or "skipped" in r:
         return r
     keys = ("value", "ms_per_step", "bubble_fraction", "bubble_per_rank", "analytic_bubble", "hbm_peak_gb_per_gpu",
-            "model_tflops_per_gpu", "p2p_bytes_per_step", "rccl_ranks", "attempt")
+            "hbm_reserved_peak_gb_per_gpu", "hbm_device_used_gb_per_gpu", "model_tflops_per_gpu", "p2p_bytes_per_step",
+            "rccl_ranks", "attempt", "stash_slots_per_rank")
     out = {"tok_s": r.get("value")}
     out.update({k: r.get(k) for k in keys if k != "value" and k in r})
     c = r.get("config", {})
-    for k in ("v", "microbatches", "micro_batch", "head_lag", "planned_efficiency", "native_runner", "p2p",
-              "layer_split"):
+    for k in ("model", "schedule", "v", "microbatches", "micro_batch", "head_lag", "head_max_lag", "planned_efficiency",
+              "native_runner", "p2p", "layer_split", "microbatch_lanes"):
         if k in c:
             out[k] = c[k]
     return out
@@ -635,22 +695,49 @@ def merge_reference(refs: dict, world: int, a) -> dict:
 
 
 def merge_results(headline: dict, results: dict, a) -> dict:
-    """The headline's JSON line + ``schedules`` (every measured schedule of the same
-    model/config, the headline's own included) + ``reference_fp32``."""
+    """The headline's JSON line + ``schedules`` (every measured schedule of the comparison
+    model at the same microbatches, the headline's own included when it ran that model, each
+    labelled by what it ran: ``<schedule>+lag<k>`` with a head lag) + ``reference_fp32`` +
+    ``baseline_configs``."""
     out = dict(headline)
-    sched = {headline["config"]["schedule"]: _sched_entry(headline)}
+    world = headline.get("n_gpus", 1)
+    pp = max(1, world // max(1, getattr(a, "dp", 1) or 1))
+    cmodel = compare_model(a, pp) if hasattr(a, "compare_model") else headline["config"].get("model")
+    sched = {}
+
+    def label(e, fallback):
+        # what the entry ran: "<schedule>+lag<k>" when its distributed head ran k extra
+        # warmup forwards (VERDICT r5 #1c), else the schedule's name
+        if "tok_s" not in e or not e.get("schedule"):
+            return fallback
+        lag = e.get("head_lag") or 0
+        return e["schedule"] + (f"+lag{lag}" if lag else "")
+
+    def put(key, e):
+        while key in sched:          # e.g. the planner chose lag 0 for "1F1B+lag"
+            key += " (planned)"
+        sched[key] = e
+    if cmodel == headline["config"].get("model"):
+        e = _sched_entry(headline)
+        put(label(e, headline["config"]["schedule"]), e)
     for tag, r in results.items():
         if tag.startswith("x_"):
-            sched[tag[2:]] = _sched_entry(r)
+            e = _sched_entry(r)
+            put(label(e, tag[2:]), e)
     out["schedules"] = sched
+    out["schedules_model"] = cmodel
+    if cmodel != headline["config"].get("model"):
+        out["schedules_note"] = (f"{headline['config'].get('model')} cannot interleave two chunks per rank at P = {pp} "
+                                 f"(fewer than 2P layers): the comparison runs on {cmodel}, same microbatches for "
+                                 "every schedule")
     ok = {k: v for k, v in sched.items() if "tok_s" in v and v["tok_s"]}
-    if "GPipe" in ok:
+    gp = next((v for k, v in ok.items() if k.startswith("GPipe")), None)
+    if gp is not None:
         for k, v in ok.items():
-            v["speedup_vs_gpipe"] = round(v["tok_s"] / ok["GPipe"]["tok_s"], 4)
+            v["speedup_vs_gpipe"] = round(v["tok_s"] / gp["tok_s"], 4)
     refs = {tag: r for tag, r in results.items() if tag.startswith("r") and tag[1:].isdigit()}
     if refs:
         out["reference_fp32"] = merge_reference(refs, headline["n_gpus"], a)
-    world = headline.get("n_gpus", 1)
     base = {}
     for tag, r in results.items():
         if tag.startswith("b") and tag[1:].isdigit() and world in BASE_CONFIGS:
@@ -697,7 +784,9 @@ def _concurrency_record(trainer) -> dict:
         e = getattr(trainer.coll, name, None)
         comms += int(e.channels) if e is not None else 0
     au = getattr(trainer, "comm_audit", None)
+    mp = getattr(trainer, "memory_plan", None) or {}
     return {"queue_probe": probe, "rccl_communicators": comms, "lanes": int(getattr(trainer, "lanes", 1)),
+            "stash_slots": {str(k): v for k, v in mp.get("stash_slots", {}).items()},
             "p2p_channels": int(getattr(rt.p2p, "channels", 1)), "collective_placement": rt.coll_placement,
             # first-step cross-rank check of the issued p2p order and collective sequences
             "comm_audit": None if au is None else (f"ok ({au['entries']} groups)" if au["ok"] else au["problems"])}
@@ -760,13 +849,13 @@ def run(a) -> None:
         else:
             m_default = 4 * pp
         m = a.microbatches if a.microbatches is not None else m_default
-        kw = {"vocab_size": a.vocab} if a.vocab else {}
-        cfg = NativeConfig.by_name(a.model, **kw)
+        cfg = model_config(a.model, a.vocab)
         planned = {}
+        plan_details = {}
         was_auto = _canon(a.schedule) == "auto"
         if was_auto:
             from mipipe.engine import pick_schedule
-            a.schedule, planned = pick_schedule(cfg, pp, m, a.mbs, a.seq)
+            a.schedule, planned = pick_schedule(cfg, pp, m, a.mbs, a.seq, details=plan_details)
         gpu = device.type == "cuda"
         if a.graphs is None:
             a.graphs = 1 if gpu else 0
@@ -775,7 +864,7 @@ def run(a) -> None:
                                   mbs=a.mbs, seq_len=a.seq, v=a.vstages, device=device,
                                   recompute=a.recompute if a.recompute == "auto" else a.recompute == "1", seed=0,
                                   split_head=False if a.no_split_head else None, graphs=bool(a.graphs) and gpu,
-                                  dtype=dtype)
+                                  dtype=dtype, head_max_lag=a.head_max_lag)
         describe["fn"] = trainer.describe
         gb = dp * m * a.mbs
         g = torch.Generator(device=device).manual_seed(1234 + trainer.mesh.dp_rank)
@@ -852,13 +941,19 @@ def run(a) -> None:
             lv = torch.tensor([loss_val if loss_val is not None else 0.0], device=device, dtype=torch.float64)
             dist.all_reduce(lv, op=dist.ReduceOp.SUM)
             loss_val = float(lv.item()) / dp
-    hbm_peak = None
+    hbm_peak = hbm_reserved = hbm_used = None
     if gpu:
         with wd.step(init_to):
-            hp = torch.tensor([torch.cuda.max_memory_allocated(device) / 2 ** 30], device=device, dtype=torch.float64)
+            # allocated peak (what live tensors held), reserved peak (what the caching allocator
+            # and the HIP-graph pools held: a graph pool keeps its freed blocks reserved), and the
+            # device's used bytes (mem_get_info: also RCCL buffers, code objects, workspaces)
+            free, total = torch.cuda.mem_get_info(device)
+            hp = torch.tensor([torch.cuda.max_memory_allocated(device) / 2 ** 30,
+                               torch.cuda.max_memory_reserved(device) / 2 ** 30, (total - free) / 2 ** 30],
+                              device=device, dtype=torch.float64)
             if world > 1:
                 dist.all_reduce(hp, op=dist.ReduceOp.MAX)
-            hbm_peak = round(float(hp.item()), 1)
+            hbm_peak, hbm_reserved, hbm_used = (round(float(x), 1) for x in hp.tolist())
     flops = cfg.flops_per_token(a.seq) * value
     rt = trainer.runtime
     with wd.step(init_to):
@@ -900,7 +995,9 @@ def run(a) -> None:
         "bubble_source": src,
         "analytic_bubble": round(analytic_bubble(trainer.schedule, pp, m, trainer.v), 4),
         "model_tflops_per_gpu": round(flops / world / 1e12, 1),
-        "hbm_peak_gb_per_gpu": hbm_peak,   # max over ranks of the caching allocator's peak
+        "hbm_peak_gb_per_gpu": hbm_peak,   # max over ranks of the caching allocator's allocated peak
+        "hbm_reserved_peak_gb_per_gpu": hbm_reserved,
+        "hbm_device_used_gb_per_gpu": hbm_used,
         "attempt": attempt,
         "attempt_mode": os.environ.get("MIPIPE_BENCH_MODE", "in-process"),
         "config": {"model": a.model, "params": cfg.n_params(), "global_batch": gb, "seq_len": a.seq,
@@ -926,16 +1023,19 @@ def run(a) -> None:
                    "head": ("distributed, token chunks " + str(trainer.head_chunks)) if trainer.head is not None
                    else "last stage",
                    "head_lag": getattr(trainer, "head_lag", None),
+                   "head_max_lag": a.head_max_lag,
                    "planned_efficiency": None if getattr(trainer, "planned_makespan", None) is None else
                    round(trainer.planned_ideal / trainer.planned_makespan, 3),
-                   "schedule_choice": ({"auto": {k: round(v_, 3) for k, v_ in planned.items()}} if planned
-                                       else ("auto (one GPU: 1F1B)" if was_auto else "given"))},
+                   "schedule_choice": ({"auto": {k: round(v_, 3) for k, v_ in planned.items()}, "plans": plan_details}
+                                       if planned else ("auto (one GPU: 1F1B)" if was_auto else "given"))},
     }
     if loss_val is not None:
         out["last_loss"] = round(loss_val, 4)
     out["p2p_bytes_per_step"] = p2p_bytes
     out["rccl_ranks"] = rccl_ranks
     out["per_rank_concurrency"] = allc
+    # every rank's stash slots per local stage (parallel/stash.py plan of its compute order)
+    out["stash_slots_per_rank"] = [c.get("stash_slots") for c in allc]
     if rank == 0:
         emit(out)
     with wd.step(init_to):

@@ -1187,6 +1187,226 @@ static int launch6(const void* A, const void* B, void* C, const void* bias, cons
 }
 
 // ---------------------------------------------------------------------------------------
+// gemm8: 256x192 NT, FOUR waves -- one wave per SIMD, a 128 x 96 accumulator tile per wave
+// (8 x 6 blocks of 16x16x32, 192 accumulator registers) -- register-staged with a whole
+// K-tile of prefetch in flight.  The main-loop shape of the library kernel torch picks for
+// GPT-2's K = 768 GEMMs on gfx950 (hipBLASLt MT192x256x64 MI16x16x1 MIWT6_8 PGR2, its
+// .s read in profiles/r6_hipblaslt_mainloop.md), where gemm3's two ping-pong waves per SIMD
+// run at 0.6-0.89x the library (profiles/r6_gemm_step_shapes.md).
+//
+// Per K-tile (BK = 64) a wave issues 96 MFMAs (2 k-steps x 8 x 6) and, in the MFMA gaps:
+//   * the 14 ds_read_b128 fragments of the NEXT k-step (register double buffer), the
+//     k-step-0 ones of the next K-tile right after the barrier, under the last 18 MFMAs;
+//   * the 14 staging pairs: ds_write_b128 of K-tile t+1 (loaded during tile t-1) into the
+//     other LDS buffer, then buffer_load_dwordx4 of K-tile t+2 into the freed registers
+//     (the compiler's counted vmcnt(13) per write retires exactly its own load).
+// One barrier per K-tile; two LDS buffers 64 KiB apart.  Nothing here is a DMA-to-LDS
+// (global_load_lds): a register-staged ring keeps one K-tile more in flight than two LDS
+// buffers of glds can (the gemm5 probe: 0.7-0.8x gemm3 with a one-tile glds ring).
+// The epilogue is gemm2's LDS-staged one (2 passes of 128 rows).
+// ---------------------------------------------------------------------------------------
+typedef unsigned int u32x4g8 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void g8_wait_lgkm0() {
+  // s_waitcnt lgkmcnt(0), vmcnt / expcnt left at their maxima (no wait)
+  __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
+}
+
+template <int EPI, bool ACC, int PGR>
+__global__ void __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm8_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B, void* __restrict__ Cv,
+             const bf16_t* __restrict__ bias, const bf16_t* __restrict__ R, bf16_t* __restrict__ AUX,
+             float* __restrict__ WS, int M, int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr,
+             int64_t ldx, float alpha, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  constexpr int BM = 256, BN = 192, NTH8 = 256;
+  constexpr int AIMG = BM * 128;     // A image [256 rows][64 k], 128-byte rows (swzq)
+  constexpr int BUFSTRIDE = 0x10000; // B image at +AIMG; buffer 1 at +64 KiB
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int gm = (M + BM - 1) / BM, gn = (N + BN - 1) / BN;
+  const int nwg = gm * gn;
+  const int wg = xcd_remap((int)blockIdx.x, nwg);
+  constexpr int GROUP = MP_G3_GROUP;
+  const int group = wg / (GROUP * gn);
+  const int first_m = group * GROUP;
+  const int gsz = min(gm - first_m, GROUP);
+  const int tm = first_m + (wg % (GROUP * gn)) % gsz;
+  const int tn = (wg % (GROUP * gn)) / gsz;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nk = K / BK;
+
+  // staging: thread t moves 16-byte chunk (t & 7) of tile rows (t >> 3) + 32 u; the LDS
+  // slot is that row's chunk ^ swz8(row) (row bits 1-3 = those of t >> 3: one base).  One
+  // buffer resource per operand at the tile's first row: row u of a thread is a scalar
+  // offset (32 u rows), and rows past the M / N edge fall outside num_records, so the
+  // hardware returns zeros for them (masked outputs only) -- no per-row clamp registers
+  const int srow = tid >> 3, sch = tid & 7;
+  const int mrows = min(BM, M - m0), nrows = min(BN, N - n0);
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(A + (int64_t)m0 * lda), 0, (int)(((int64_t)(mrows - 1) * lda + K) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(B + (int64_t)n0 * ldb), 0, (int)(((int64_t)(nrows - 1) * ldb + K) * 2), 0x00020000);
+  const int voa = (int)(((int64_t)srow * lda + sch * 8) * 2);
+  const int vob = (int)(((int64_t)srow * ldb + sch * 8) * 2);
+  const int rsa = (int)(32 * lda * 2), rsb = (int)(32 * ldb * 2);   // bytes per 32 rows
+  const int dst = srow * 128 + 16 * (sch ^ swz8(srow));   // + 4096 u (A), + AIMG + 4096 u (B)
+
+  // fragment reads (32x32x16: lane reads row base + (lane & 31), k-chunk 2 s + hl of the
+  // 16-deep k-step s): chunk ^ swz8(row) with row bits 1-3 = lane bits 1-3, so per k-step one
+  // base per operand and + 4096 per 32-row block
+  const int hl = lane >> 5, l32 = lane & 31;
+  const int c0 = hl ^ swz8(l32);
+  int fa_off[4], fb_off[4];
+#pragma unroll
+  for (int s_ = 0; s_ < 4; ++s_) {
+    fa_off[s_] = (wr * 128 + l32) * 128 + 16 * ((2 * s_) ^ c0);
+    fb_off[s_] = AIMG + (wc * 96 + l32) * 128 + 16 * ((2 * s_) ^ c0);
+  }
+
+  // PGR K-tiles in flight: K-tile t+1 waits in register set (t+1) % NSET while the loads of
+  // K-tile t+PGR go out into the set just written (PGR 2: one set, hipBLASLt's PGR2)
+  constexpr int NSET = PGR - 1;
+  u32x4g8 st[NSET][14];
+  bf16x8 fx[7], fy[7];     // fragments of even / odd k-steps: A blocks 0-3, B blocks 0-2
+  f32x16 acc[4][3];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) acc[i][j] = f32x16{};
+
+  auto gload = [&](auto SET, int u, int kt) {
+    constexpr int S = decltype(SET)::value;
+    if (u < 8) st[S][u] = __builtin_amdgcn_raw_buffer_load_b128(ra, voa, kt * 128 + u * rsa, 0);
+    else st[S][u] = __builtin_amdgcn_raw_buffer_load_b128(rb, vob, kt * 128 + (u - 8) * rsb, 0);
+  };
+  auto swrite = [&](auto SET, int boff, int u) {
+    constexpr int S = decltype(SET)::value;
+    const int off = u < 8 ? dst + 4096 * u : AIMG + dst + 4096 * (u - 8);
+    *reinterpret_cast<u32x4g8*>(smem + boff + off) = st[S][u];
+  };
+  auto fread = [&](bf16x8 (&f)[7], int boff, int s_) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = *reinterpret_cast<const bf16x8*>(smem + boff + fa_off[s_] + 4096 * i);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) f[4 + j] = *reinterpret_cast<const bf16x8*>(smem + boff + fb_off[s_] + 4096 * j);
+  };
+  auto mma = [&](const bf16x8 (&f)[7]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) acc[i][j] = mfma32(f[i], f[4 + j], acc[i][j]);
+  };
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, NSET - 1>;   // set of odd K-tiles
+
+  // prologue: K-tiles 0 .. PGR-1 in flight, K-tile 0 into LDS buffer 0, k-step-0 fragments
+#pragma unroll
+  for (int u = 0; u < 14; ++u) gload(I0{}, u, 0);
+  if constexpr (NSET > 1) {
+#pragma unroll
+    for (int u = 0; u < 14; ++u) gload(I1{}, u, min(1, nk - 1));
+  }
+#pragma unroll
+  for (int u = 0; u < 14; ++u) swrite(I0{}, 0, u);
+#pragma unroll
+  for (int u = 0; u < 14; ++u) gload(I0{}, u, min(NSET, nk - 1));
+  g8_wait_lgkm0();
+  __builtin_amdgcn_s_barrier();
+  fread(fx, 0, 0);
+
+  // K-tile t from the buffer at `cur` (0 / 64 KiB, toggled per K-tile); K-tile t+1 staged
+  // into the other one during k-steps 0-2 (5 + 5 + 4 write / load pairs), one barrier, and
+  // the next K-tile's k-step-0 fragments read under k-step 3
+  int cur = 0;
+  auto ktile = [&](int t, auto SET) {
+    const int nxt = cur ^ BUFSTRIDE;
+    const int kl = min(t + PGR, nk - 1);   // the tail re-loads the last K-tile: never read
+    // k-steps 0-2: each issues the next k-step's 7 fragment reads under its first 7 MFMAs,
+    // then (ds_write, buffer_load) staging pairs under the rest (5 + 5 + 4 pairs); a
+    // sched_barrier closes every k-step, so no MFMA moves next to the reads it waits on
+    auto kstep = [&](auto& fcur, auto& fnext, int s_next, int u0, auto U1) {
+      constexpr int u1 = decltype(U1)::value, rest = u1 == 14 ? 2 : 0;
+      fread(fnext, cur, s_next);
+      mma(fcur);
+#pragma unroll
+      for (int u = u0; u < u1; ++u) {
+        swrite(SET, nxt, u);
+        gload(SET, u, kl);
+      }
+#pragma unroll
+      for (int g = 0; g < 7; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+      }
+#pragma unroll
+      for (int g = 0; g < u1 - u0; ++g) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+      if constexpr (rest > 0) __builtin_amdgcn_sched_group_barrier(0x008, rest, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    kstep(fx, fy, 1, 0, std::integral_constant<int, 5>{});
+    kstep(fy, fx, 2, 5, std::integral_constant<int, 10>{});
+    kstep(fx, fy, 3, 10, std::integral_constant<int, 14>{});
+    // every wave's staging writes of K-tile t+1 and fragment reads of K-tile t are done
+    g8_wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    // k-step 3 covers the next K-tile's k-step-0 fragment reads
+    fread(fx, nxt, 0);
+    mma(fy);
+#pragma unroll
+    for (int g = 0; g < 7; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 1, 1);
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 5, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    cur = nxt;
+  };
+  int t = 0;
+  if constexpr (NSET == 1) {
+#pragma unroll 1
+    for (; t < nk; ++t) ktile(t, I0{});
+  } else {
+#pragma unroll 1
+    for (; t + 1 < nk; t += 2) {
+      ktile(t, I1{});       // K-tile t+1 (odd) waits in set 1
+      ktile(t + 1, I0{});
+    }
+    if (t < nk) ktile(t, I1{});
+  }
+  __syncthreads();
+  epilogue<BM, BN, 2, 2, EPI, ACC, NTH8>(Stage32<4, 3>{acc, wc * 96, hl, l32}, smem, m0, n0, wr, Cv, bias, R, AUX,
+                                         WS, M, N, ldc, ldr, ldx, alpha, 1, p_drop, seed);
+}
+
+template <int EPI, bool ACC, int PGR = 2>
+static int launch8(const void* A, const void* B, void* C, const void* bias, const void* R, void* X, float* ws, int M,
+                   int N, int K, int64_t lda, int64_t ldb, int64_t ldc, int64_t ldr, int64_t ldx, float alpha,
+                   float p_drop, uint64_t seed, hipStream_t st) {
+  constexpr int LDS_MAIN = 0x10000 + 256 * 128 + 192 * 128;   // buffer 1 ends at 120 KiB
+  constexpr int EPI_BYTES = 128 * (192 + 4) * 4;
+  constexpr int LDS = LDS_MAIN > EPI_BYTES ? LDS_MAIN : EPI_BYTES;
+  auto kern = gemm8_kernel<EPI, ACC, PGR>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, LDS);
+    attr = true;
+  }
+  const int nwg = ((M + 255) / 256) * ((N + 191) / 192);
+  kern<<<dim3(nwg, 1), 256, LDS, st>>>((const bf16_t*)A, (const bf16_t*)B, C, (const bf16_t*)bias, (const bf16_t*)R,
+                                       (bf16_t*)X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
 // gemm7: the PARTIAL round of a 256x256 NT GEMM split over all CUs -- a pipeline rank's
 // 8K-32K-token microbatches are 96-384 tiles of 256x256 for N = 768, i.e. 0.4-1.5 rounds of
 // 256 CUs (profiles/r5_gemm7_*).  The host runs the whole rounds as a plain gemm3 launch on
@@ -2275,6 +2495,8 @@ static int dispatch(int cfg, const void* A, const void* B, void* C, const void* 
     if (cfg == 4) return launch3<EPI, ACC, false>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 5) return launch3<EPI, ACC, true>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, split, p_drop, seed, st);
     if (cfg == 9) return launch6<EPI, ACC>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
+    if (cfg == 15) return launch8<EPI, ACC, 2>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
+    if (cfg == 16) return launch8<EPI, ACC, 3>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
 #ifdef MP_PROBE_ENGINES
     if constexpr (!ACC) {
       if (cfg == 8) return launch5<EPI>(A, B, C, bias, R, X, ws, M, N, K, lda, ldb, ldc, ldr, ldx, alpha, p_drop, seed, st);
@@ -2472,6 +2694,13 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
     }
   }
   if (use5 && cfg == 5 && split == 1 && !c_f32_accum && force_cfg < 0) cfg = 8;
+  // 15: the four-wave register-staged 256x192 NT engine (gemm8); MIPIPE_GEMM8=1 uses it
+  // wherever gemm3's M16 build would run without split-K
+  static const bool use8 = [] { const char* e = getenv("MIPIPE_GEMM8"); return e && e[0] == '1'; }();
+  if (!transA && !transB && (force_cfg == 15 || force_cfg == 16 || (use8 && cfg == 5 && split == 1 && force_cfg < 0))) {
+    *split_out = 1;
+    return force_cfg == 16 ? 16 : 15;
+  }
   // the stream-K engine (gemm7) where the 256x256 grid is not whole rounds of 256 CUs
   // (force_cfg 14 selects it wherever plan7 accepts the grid)
   // Opt-in (MIPIPE_GEMM_SK=1): measured null -- on the all-tail M = 8192 grids the split

@@ -157,7 +157,8 @@ def max_inflight_microbatches(order, stages) -> int:
 
 def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, seq_len: int, device,
                    head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1,
-                   stage_shards: int = 1, dtype=torch.bfloat16, graphs: bool = False, lanes: int = 1) -> dict:
+                   stage_shards: int = 1, dtype=torch.bfloat16, graphs: bool = False, lanes: int = 1,
+                   hbm: Optional[float] = None) -> dict:
     """HBM plan of one pipeline rank and the recompute decision of ``recompute="auto"``:
     recompute only if the activation stash would not fit ``budget_frac`` of the device.
 
@@ -176,7 +177,8 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     The stash is counted per stage from the slot plan of the rank's order
     (parallel/stash.py): the in-flight microbatches of each stage -- also with HIP graphs,
     whose captures share one pool per stash slot (``lanes``: slots are per microbatch lane;
-    MIPIPE_STASH_RING=0 restores one private pool per graph, i.e. all m stashes)."""
+    MIPIPE_STASH_RING=0 restores one private pool per graph, i.e. all m stashes).
+    ``hbm``: the device's bytes (default: the device's own; unbounded off the GPU)."""
     T = mbs * seq_len
     from .parallel.stash import stash_slots_per_stage
     layers_of = {s: layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages}
@@ -201,11 +203,38 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     full = fixed + stash_layers * cfg.stash_bytes_per_layer(T, recompute=False)
     rec = fixed + stash_layers * cfg.stash_bytes_per_layer(T, recompute=True) + \
         cfg.stash_bytes_per_layer(T, recompute=False)
-    total = torch.cuda.get_device_properties(device).total_memory if device.type == "cuda" else float("inf")
+    if hbm is not None:
+        total = float(hbm)
+    else:
+        total = torch.cuda.get_device_properties(device).total_memory if device.type == "cuda" else float("inf")
     return dict(inflight=inflight, stash_slots=slots, layers=nlayers, bytes_no_recompute=full, bytes_recompute=rec,
                 hbm=total,
                 recompute=bool(full > budget_frac * total), head_state_bytes=head_state,
                 head_optimizer_bytes=head_opt)
+
+
+# HBM the planners assume off the GPU (CPU tests, the supervisor's plan child): one MI355X
+MI355X_HBM_BYTES = 288 * 2 ** 30
+
+
+def plan_rank_memory(cfg: NativeConfig, pp: int, v: int, style: str, layer_ranges, chunks, orders, mbs: int,
+                     seq_len: int, dtype=torch.bfloat16, graphs: bool = True, lanes: int = 2, head_zero: bool = True,
+                     dp: int = 1, dp_zero: bool = False, hbm: Optional[float] = None) -> Dict[int, dict]:
+    """:func:`plan_recompute` of every pipeline rank for one set of compute orders, without a
+    device (``hbm``: default one MI355X) -- what a schedule's warmup depth (its head lag)
+    costs in stash slots and bytes on each rank.  ``chunks``: the distributed head's token
+    chunk per rank (None: the head on the last stage)."""
+    out = {}
+    S = pp * v
+    for r in range(pp):
+        my = rank_stages(r, pp, v, style)
+        ht = chunks[r] if chunks is not None else (mbs * seq_len if (S - 1) in my else 0)
+        out[r] = plan_recompute(cfg, layer_ranges, my, orders.get(r, []), mbs, seq_len, torch.device("cpu"),
+                                head_tokens=ht,
+                                head_shards=pp if (head_zero and pp > 1 and chunks is not None) else 1,
+                                stage_shards=dp if dp_zero else 1, dtype=dtype, graphs=graphs, lanes=lanes,
+                                hbm=MI355X_HBM_BYTES if hbm is None else hbm)
+    return out
 
 
 def resolve_v(cfg: NativeConfig, schedule: str, pp: int, v: Optional[int], seq_len: int,
@@ -230,12 +259,20 @@ def resolve_v(cfg: NativeConfig, schedule: str, pp: int, v: Optional[int], seq_l
 
 def plan_head_pipeline(cfg: NativeConfig, pp: int, schedule: str, m: int, mbs: int, seq_len: int,
                        v: Optional[int] = None, style: str = "loop", layer_ranges=None,
-                       head_align: Optional[int] = None) -> dict:
+                       head_align: Optional[int] = None, max_lag: Optional[int] = None,
+                       mem_bound: Optional[dict] = None) -> dict:
     """The distributed-head pipeline plan of one schedule (what PipelineTrainer runs at
     PP > 1): layer split, per-stage costs (stage_cost_model units), water-filled head token
     chunks, and the head-aware compute orders with their simulated makespan
     (headsplit.plan_head_schedule).  ``ideal`` is the no-bubble time in the same units, so
-    ideal / makespan is the planned pipeline efficiency."""
+    ideal / makespan is the planned pipeline efficiency.
+
+    ``max_lag``: cap on the head lag, the extra warmup forwards every rank runs (0: the
+    schedule's own warmup, e.g. torch 1F1B's P - s).  ``mem_bound``: keyword arguments of
+    :func:`plan_rank_memory` plus ``budget_frac`` (default 0.85) and ``recompute``: a lag
+    whose HBM plan exceeds ``budget_frac`` of the device on any rank is not a candidate
+    (a deep lag turns 1F1B's and ZBH1's stash into GPipe's).  ``memory`` in
+    the result: the chosen orders' per-rank plan (with a bound)."""
     schedule = canonical_name(schedule)
     style = REQUIRED_STYLE.get(schedule, style)
     v = resolve_v(cfg, schedule, pp, v, seq_len) if layer_ranges is None else \
@@ -255,18 +292,33 @@ def plan_head_pipeline(cfg: NativeConfig, pp: int, schedule: str, m: int, mbs: i
     regen = ((lambda lag: generate(schedule, pp, m, v, style, warmup_extra=lag)) if schedule in WARMUP_EXTRA
              else None)
     comm = comm_units(cfg, seq_len, tokens=T)
-    orders, lag, makespan = plan_head_schedule(base, pp, v, style, head_costs, stage_costs, regen=regen, comm=comm)
+    fits = None
+    mb_kw = {}
+    if mem_bound is not None:
+        mb_kw = {k: x for k, x in mem_bound.items() if k not in ("budget_frac", "recompute")}
+        frac = float(mem_bound.get("budget_frac", 0.85))
+        key = "bytes_recompute" if mem_bound.get("recompute") is True else "bytes_no_recompute"
+
+        def fits(o):
+            plans = plan_rank_memory(cfg, pp, v, style, layer_ranges, chunks, o, mbs, seq_len, **mb_kw)
+            return all(p[key] <= frac * p["hbm"] for p in plans.values())
+    orders, lag, makespan = plan_head_schedule(base, pp, v, style, head_costs, stage_costs, regen=regen, comm=comm,
+                                               max_lag=max_lag, fits=fits)
+    memory = None
+    if mem_bound is not None:
+        memory = plan_rank_memory(cfg, pp, v, style, layer_ranges, chunks, orders, mbs, seq_len, **mb_kw)
     # no-bubble time in the same units (F = 1, B = 2 per stage-cost unit)
     ideal = (3.0 * sum(stage_costs) + sum(head_costs.values())) * m / pp
     return dict(schedule=schedule, v=v, style=style, layer_ranges=layer_ranges, stage_costs=stage_costs, comm=comm,
                 chunks=chunks, head_costs=head_costs, orders=orders, lag=lag, makespan=makespan, ideal=ideal,
-                efficiency=ideal / makespan if makespan > 0 else 0.0)
+                efficiency=ideal / makespan if makespan > 0 else 0.0, memory=memory)
 
 
 def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
                   candidates=("GPipe", "1F1B", "Interleaved1F1B", "ZBH1"),
                   margin: float = 0.03, v: Optional[int] = None, style: str = "loop", layer_ranges=None,
-                  head_align: Optional[int] = None, same_traffic_margin: float = 0.01) -> Tuple[str, Dict[str, float]]:
+                  head_align: Optional[int] = None, same_traffic_margin: float = 0.01,
+                  mem_bound: Optional[dict] = None, details: Optional[dict] = None) -> Tuple[str, Dict[str, float]]:
     """``schedule="auto"``: 1F1B unless another candidate's head-aware plan is more
     efficient by more than ``margin`` (relative) -- the plan's p2p model is an estimate, and
     an interleaved rank sends twice the activations (1F1B at PP = 1, where every schedule is
@@ -281,11 +333,18 @@ def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
     full only to a candidate that sends MORE than 1F1B (interleaved with v > 1). GPipe,
     ZBH1 and v = 1 interleaved send exactly 1F1B's messages and need only
     ``same_traffic_margin``.  GPT-2 small at P = 8, 16-sequence microbatches: ZBH1 plans
-    0.906 vs 0.8825, which a 3 % margin would throw away."""
+    0.906 vs 0.8825, which a 3 % margin would throw away.
+
+    Every candidate is planned under ``mem_bound`` (plan_head_pipeline; default: bf16 with HIP
+    graphs and 2 lanes on one MI355X): its head lag is the smallest within the lag tolerance
+    of its best plan AND whose stash fits the HBM budget on every rank.
+    ``details`` (a dict, filled): per candidate its planned efficiency, v, the head lag it
+    assumed, the largest per-rank stash slot count and planned GB."""
     if pp == 1:
         return "1F1B", {}
     eff = {}
     vs: Dict[str, int] = {}
+    mem_bound = {} if mem_bound is None else mem_bound
     for c in candidates:
         try:
             cv = v if SCHEDULES[canonical_name(c)][2] else 1
@@ -293,8 +352,14 @@ def pick_schedule(cfg: NativeConfig, pp: int, m: int, mbs: int, seq_len: int,
             if rng is not None and len(rng) != pp * (cv if cv is not None else SCHEDULES[canonical_name(c)][1]):
                 continue
             plan = plan_head_pipeline(cfg, pp, c, m, mbs, seq_len, v=cv, style=style, layer_ranges=rng,
-                                      head_align=head_align)
+                                      head_align=head_align, mem_bound=mem_bound)
             eff[c], vs[c] = plan["efficiency"], int(plan["v"])
+            if details is not None:
+                mem = plan["memory"] or {}
+                details[c] = {"efficiency": round(plan["efficiency"], 4), "v": int(plan["v"]), "head_lag": plan["lag"],
+                              "stash_slots_max": max((sum(p["stash_slots"].values()) for p in mem.values()), default=None),
+                              "planned_gb_max": round(max((p["bytes_no_recompute"] for p in mem.values()), default=0.0)
+                                                      / 1e9, 1)}
         except (ValueError, RuntimeError, KeyError):
             continue
     if "1F1B" not in eff:
@@ -408,7 +473,10 @@ class PipelineTrainer:
                  recompute: bool = False, profile: bool = False, seed: int = 0, style: str = "loop",
                  mesh: Optional[Mesh] = None, layer_ranges=None, dtype=torch.bfloat16,
                  split_head: Optional[bool] = None, head_align: Optional[int] = None, graphs: bool = False,
-                 adam_eps: float = 1e-8):
+                 adam_eps: float = 1e-8, head_max_lag: Optional[int] = None):
+        """``head_max_lag``: cap on the distributed head's lag (extra warmup forwards; 0 = the
+        schedule's own depth, e.g. 1F1B's P - s).  Whatever the cap, the lag is bounded by
+        the HBM plan (``self.mem_bound``)."""
         self.cfg = cfg
         # schedule="auto": the best head-aware plan (pick_schedule; 1F1B at PP = 1)
         self.schedule_choice = None
@@ -450,13 +518,41 @@ class PipelineTrainer:
         self.head: Optional[HeadShard] = None
         orders = head_plan = head_costs = stage_costs = None
         self.head_chunks = None
+        self.head_lag = None
         # ZeRO-1 for the replicated head: master / Adam moments sharded over the pipeline
         # group (MIPIPE_HEAD_ZERO=0: fully replicated, gradient all-reduced)
         self.head_zero = self.split_head and os.environ.get("MIPIPE_HEAD_ZERO", "1") != "0"
+        # ZeRO-1 over DP replicas (see below): known before the HBM plan
+        self.dp_zero = (self.mesh.dp > 1 and os.environ.get("MIPIPE_DP_ZERO", "1") != "0"
+                        and not (tied_pp or self._tie_local))
+        graphed = bool(graphs) and self.device.type == "cuda"
+        # microbatch lanes (PipelineRuntime.set_lanes), decided BEFORE the HBM plan: slots of
+        # the stash ring are per lane (the plan used to assume 2).  MIPIPE_LANES=
+        # auto|1 (off)|n.  Not with plain GEMMs on hipBLASLt (MIPIPE_GEMM=blas|auto): its
+        # stream-K kernels synchronise their workgroups and assume all of them resident; a
+        # second lane's kernels holding CUs left a Llama-3 1B step hung in that mode
+        # (profiles/r3_model_families_1gpu.txt)
+        from .ops.kernels import GEMM_BACKEND
+        my_layers = sum(layer_ranges[st][1] - layer_ranges[st][0] for st in my_stages)
+        params_est = (cfg.layer_params() * my_layers + (cfg.vocab_padded * cfg.d_model if 0 in my_stages else 0)
+                      + (cfg.vocab_padded * cfg.d_model if self.split_head else 0))
+        if os.environ.get("MIPIPE_LANES", "auto") == "auto":
+            self.planned_lanes = auto_lanes(cfg, pp, v, graphs, self.device, n_microbatches, mbs * seq_len,
+                                            params_est, my_layers, recompute is True)
+        else:
+            self.planned_lanes = max(1, int(os.environ["MIPIPE_LANES"]))
+        if GEMM_BACKEND != "hip":
+            self.planned_lanes = 1
+        hbm = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" \
+            else MI355X_HBM_BYTES
+        # the head lag's memory bound (plan_head_pipeline): every rank's stash within 85 % of HBM
+        self.mem_bound = dict(dtype=dtype, graphs=graphed, lanes=self.planned_lanes if graphed else 1,
+                              head_zero=self.head_zero, dp=self.mesh.dp, dp_zero=self.dp_zero, hbm=hbm,
+                              budget_frac=0.85, recompute=recompute)
         if self.split_head:
             self.head = HeadShard(cfg, self.device, seed=seed, dtype=dtype, shards=pp if self.head_zero else 1)
             plan = plan_head_pipeline(cfg, pp, self.schedule, n_microbatches, mbs, seq_len, v, style, layer_ranges,
-                                      head_align)
+                                      head_align, max_lag=head_max_lag, mem_bound=self.mem_bound)
             orders, self.head_lag, self.planned_makespan = plan["orders"], plan["lag"], plan["makespan"]
             stage_costs, head_costs, chunks = plan["stage_costs"], plan["head_costs"], plan["chunks"]
             self.planned_ideal = plan["ideal"]
@@ -467,27 +563,16 @@ class PipelineTrainer:
                 head_plan.graphs = GraphCache(f"{self.mesh.pp_rank}")
             self.head_chunks = chunks
         # recompute="auto": HBM plan from the schedule's in-flight microbatches (288 GB per
-        # MI355X usually holds the whole stash, and recompute costs a forward per layer)
-        self.memory_plan = None
-        # ZeRO-1 over DP replicas (see below): known before the HBM plan
-        self.dp_zero = (self.mesh.dp > 1 and os.environ.get("MIPIPE_DP_ZERO", "1") != "0"
-                        and not (tied_pp or self._tie_local))
-        # the plan is made (and reported: bench.py's config.memory_plan) whatever the
+        # MI355X usually holds the whole stash, and recompute costs a forward per layer).
+        # The plan is made (and reported: bench.py's config.memory_plan) whatever the
         # setting; recompute="auto" acts on it
-        if True:
-            order = (orders if orders is not None else
-                     generate(self.schedule, pp, n_microbatches, v, style)).get(self.mesh.pp_rank, [])
-            head_tokens = (self.head_chunks[self.mesh.pp_rank] if self.head_chunks is not None else
-                           (mbs * seq_len if (num_stages - 1) in my_stages else 0))
-            self.memory_plan = plan_recompute(cfg, layer_ranges, my_stages, order, mbs, seq_len, self.device,
-                                              head_tokens=head_tokens,
-                                              head_shards=pp if (self.head_zero and pp > 1) else 1,
-                                              stage_shards=self.mesh.dp if self.dp_zero else 1, dtype=dtype,
-                                              graphs=graphs and self.device.type == "cuda",
-                                              lanes=2 if (graphs and self.device.type == "cuda" and
-                                                          n_microbatches >= 2) else 1)
-            if recompute == "auto":
-                recompute = self.memory_plan["recompute"]
+        self._order = (orders if orders is not None else
+                       generate(self.schedule, pp, n_microbatches, v, style)).get(self.mesh.pp_rank, [])
+        self._my_stages = my_stages
+        self.memory_plan = self._plan_memory(self.planned_lanes if graphed else 1)
+        self.recompute_requested = recompute
+        if recompute == "auto":
+            recompute = self.memory_plan["recompute"]
         self.recompute = bool(recompute)
         # ZeRO-1 over DP replicas (MIPIPE_DP_ZERO=0: replicated master / moments, gradient
         # all-reduced): each replica owns 1/dp of every stage arena -- its f32 master and Adam
@@ -516,12 +601,14 @@ class PipelineTrainer:
         # plain GEMMs on hipBLASLt (MIPIPE_GEMM=blas|auto): its stream-K kernels synchronise
         # their workgroups and assume all of them resident; a second lane's kernels holding
         # CUs left a Llama-3 1B step hung in that mode (profiles/r3_model_families_1gpu.txt)
-        from .ops.kernels import GEMM_BACKEND
-        n_lanes = (self._auto_lanes(pp, v, graphs, n_microbatches, mbs, seq_len)
-                   if os.environ.get("MIPIPE_LANES", "auto") == "auto" else max(1, int(os.environ["MIPIPE_LANES"])))
-        if GEMM_BACKEND != "hip" and n_lanes > 1:
-            n_lanes = 1
-        self.lanes = self.runtime.set_lanes(n_lanes)
+        self.lanes = self.runtime.set_lanes(self.planned_lanes)
+        if graphed and self.lanes != self.planned_lanes:
+            # the runtime took fewer lanes than planned: re-plan with the real count
+            self.memory_plan = self._plan_memory(self.lanes)
+            if self.recompute_requested == "auto" and self.memory_plan["recompute"] != self.recompute:
+                raise RuntimeError(f"recompute='auto' planned with {self.planned_lanes} microbatch lanes, but the "
+                                   f"runtime runs {self.lanes}: the HBM plan's decision changes "
+                                   f"({self.recompute} -> {self.memory_plan['recompute']}); set MIPIPE_LANES")
         arenas = [st.arena for st in self.stages]
         if self.dp_zero:
             dp, dr = self.mesh.dp, self.mesh.dp_rank
@@ -607,6 +694,17 @@ class PipelineTrainer:
                 coll.all_reduce(part, "dp").wait()
                 return True
         return [_Chain()]
+
+    def _plan_memory(self, lanes: int) -> dict:
+        """This rank's HBM plan (plan_recompute) for its compute order with ``lanes`` lanes."""
+        head_tokens = (self.head_chunks[self.mesh.pp_rank] if self.head_chunks is not None else
+                       (self.mbs * self.S if (len(self.layer_ranges) - 1) in self._my_stages else 0))
+        mb = self.mem_bound
+        return plan_recompute(self.cfg, self.layer_ranges, self._my_stages, self._order, self.mbs, self.S,
+                              self.device, head_tokens=head_tokens,
+                              head_shards=self.mesh.pp if (self.head_zero and self.mesh.pp > 1) else 1,
+                              stage_shards=self.mesh.dp if self.dp_zero else 1, dtype=mb["dtype"],
+                              graphs=mb["graphs"], lanes=lanes, hbm=mb["hbm"])
 
     def _auto_lanes(self, pp: int, v: int, graphs: bool, m: int, mbs: int, seq_len: int) -> int:
         layers = sum(self.layer_ranges[st.stage_index][1] - self.layer_ranges[st.stage_index][0]

@@ -188,7 +188,8 @@ def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v
                        comm: float = 0.05, lags: Sequence[int] = (0, 1, 2, 3, 4, 6, 8, 12, 16, 24, 32),
                        policies: Sequence[str] = ("head_first", "fill"),
                        regen: Optional[Callable[[int], Dict[int, Sequence[Optional[Action]]]]] = None,
-                       lag_tol: Optional[float] = None, max_lag: Optional[int] = None
+                       lag_tol: Optional[float] = None, max_lag: Optional[int] = None,
+                       fits: Optional[Callable[[Dict[int, List[Action]]], bool]] = None
                        ) -> Tuple[Dict[int, List[Action]], int, float]:
     """Best of ``insert_head_ops`` over the candidate last-stage lags (simulated
     makespan).  Returns (orders, lag, makespan).
@@ -200,7 +201,10 @@ def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v
     (hundreds of MB at GPT-2 scale, cheap next to 288 GB of HBM) -- but not free: a lag of m
     turns 1F1B's stash into GPipe's.  So the plan takes the SMALLEST lag whose makespan is
     within ``lag_tol`` (default 1 %, ``MIPIPE_HEAD_LAG_TOL``) of the best, and never more than
-    ``max_lag`` (``MIPIPE_HEAD_MAX_LAG``; e.g. from an HBM budget).
+    ``max_lag`` (``MIPIPE_HEAD_MAX_LAG``).  ``fits(orders)``: the memory bound -- a placement
+    with a positive lag whose orders it rejects (engine.plan_head_pipeline: the HBM plan of
+    every rank's stash slots over its budget) is not a candidate; lag 0 (the schedule's own
+    warmup depth) always is.
 
     ``regen(lag)``: the schedule regenerated with ``lag`` extra warmup forwards on every
     rank (schedules.generate(..., warmup_extra=lag)).  Tried next to the re-sort of
@@ -233,6 +237,8 @@ def plan_head_schedule(orders: Dict[int, Sequence[Optional[Action]]], pp: int, v
                         regen_cache[lag] = regen(lag)
                     base = regen_cache[lag]
                 o = insert_head_ops(base, pp, v, style, head_costs, stage_costs, lag=ins_lag, comm=comm, policy=pol)
+                if lag > 0 and fits is not None and not fits(o):
+                    continue
                 res = simulate(o, pp, v, style, comm_latency=comm, stage_costs=stage_costs, head_costs=head_costs)
             except (RuntimeError, ValueError):
                 continue

@@ -201,7 +201,8 @@ def test_bench_four_ranks_measures_all_three_schedules():
     env = dict(os.environ, OMP_NUM_THREADS="1", MASTER_PORT=str(free_port()))
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         env.pop(k, None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--base-configs", "0"] + ARGS[:-2]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--base-configs", "0",
+           "--compare-model", "same"] + ARGS[:-2]
     t0 = time.monotonic()
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd="/tmp")
     dt = time.monotonic() - t0
@@ -210,25 +211,37 @@ def test_bench_four_ranks_measures_all_three_schedules():
     assert len(lines) == 1
     out = json.loads(lines[0])
     sch = out["schedules"]
-    assert set(sch) == {"GPipe", "1F1B", "Interleaved1F1B", "ZBH1"}, sch
+    # entries are labelled by what they ran ("<schedule>+lag<k>" with a head lag);
+    # "1F1B" is the reference's warmup depth (head lag capped at 0)
+    by = {}
+    for name, e in sch.items():
+        by.setdefault(e["schedule"], []).append(name)
+        assert name.split(" ")[0] == e["schedule"] + (f"+lag{e['head_lag']}" if e["head_lag"] else ""), (name, e)
+    assert set(by) == {"GPipe", "1F1B", "Interleaved1F1B", "ZBH1"}, sch
+    assert sch["1F1B"]["head_lag"] == 0
     for name, e in sch.items():
         assert e["tok_s"] > 0 and e["bubble_fraction"] is not None and e["analytic_bubble"] is not None, (name, e)
-        assert e["p2p_bytes_per_step"] > 0
+        assert e["p2p_bytes_per_step"] > 0 and len(e["stash_slots_per_rank"]) == 4
+    il = sch[by["Interleaved1F1B"][0]]
+    gp = sch[by["GPipe"][0]]
     # 4 layers over 4 ranks: two chunks per rank would leave virtual stages empty, so
     # interleaved falls back to one chunk -- the reference's own rule when L % 2P != 0
     # (helper:181-183; VERDICT r4: no empty range in any layer split)
-    assert sch["Interleaved1F1B"]["v"] == 1 and sch["GPipe"]["v"] == 1
-    assert sch["Interleaved1F1B"]["analytic_bubble"] == sch["1F1B"]["analytic_bubble"]
+    assert il["v"] == 1 and gp["v"] == 1
+    assert il["analytic_bubble"] == sch["1F1B"]["analytic_bubble"]
     for name, e in sch.items():
         assert all(b > a for a, b in e["layer_split"]), (name, e["layer_split"])
-    assert sch["GPipe"]["speedup_vs_gpipe"] == 1.0
+    assert gp["speedup_vs_gpipe"] == 1.0
     # --schedule auto: the headline is the best-planned schedule, and it is measured once
     head = out["config"]["schedule"]
-    assert out["value"] == sch[head]["tok_s"] and set(out["config"]["schedule_choice"]["auto"]) == set(sch)
+    hl = head + (f"+lag{out['config']['head_lag']}" if out["config"]["head_lag"] else "")
+    assert out["value"] == sch[hl]["tok_s"] and set(out["config"]["schedule_choice"]["auto"]) == set(by)
+    plans = out["config"]["schedule_choice"]["plans"]
+    assert all({"head_lag", "stash_slots_max", "planned_gb_max"} <= set(p) for p in plans.values()), plans
     eff = out["config"]["schedule_choice"]["auto"]
     # the best plan among candidates that beat 1F1B by their margin (3 % with more p2p
     # than 1F1B -- interleaved v > 1 --, 1 % with the same messages), else 1F1B
-    v_of = {k: e["v"] for k, e in sch.items()}
+    v_of = {s: sch[names[0]]["v"] for s, names in by.items()}
     beats = [k for k in eff if k != "1F1B" and eff[k] >= eff["1F1B"] * (1.03 if v_of.get(k, 1) > 1 else 1.01)]
     assert head == (max(beats, key=lambda k: eff[k]) if beats else "1F1B"), (head, eff, v_of)
     assert out["p2p_bytes_per_step"] > 0 and "rccl_ranks" in out
@@ -330,3 +343,38 @@ def test_bench_eight_ranks_reference_at_published_pipeline_sizes():
         else:
             assert "nb_row" not in x
     assert by_p == {P: {"GPipe", "1F1B", "Interleaved1F1B"} for P in (2, 4, 8)}, by_p
+
+
+def test_bench_eight_ranks_compares_the_schedules_it_names():
+    """at N = 8 the schedule comparison runs on a model that interleaves at
+    P = 8 (here gpt2-tiny with 16 layers, CPU/gloo; on the GPU box GPT-2 medium), the
+    Interleaved1F1B entry really runs v = 2, a "1F1B" entry runs the reference's warmup
+    depth (per-rank stash slots <= P - r + lanes - 1), the planner's deeper 1F1B is labelled
+    with its lag, and every entry reports its head lag and per-rank stash slots."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", MIPIPE_BENCH_ATTEMPT_S="240", MASTER_PORT=str(free_port()))
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1", "--warmup", "1", "--mbs", "1",
+           "--seq", "32", "--vocab", "512", "--model", "gpt2-tiny", "--compare-model", "gpt2-tiny:16",
+           "--base-configs", "0", "--ref-fp32", "0", "--no-bubble"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=540, env=env, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert out["schedules_model"] == "gpt2-tiny:16" and "schedules_note" in out
+    sch = out["schedules"]
+    P = 8
+    for name, e in sch.items():
+        assert e["model"] == "gpt2-tiny:16" and e["microbatches"] == 32 and e["micro_batch"] == 1, (name, e)
+        assert "head_lag" in e and len(e["stash_slots_per_rank"]) == P, (name, e)
+    il = [e for e in sch.values() if e["schedule"] == "Interleaved1F1B"]
+    assert il and il[0]["v"] == 2, sch
+    ref = sch["1F1B"]
+    assert ref["head_lag"] == 0 and ref["v"] == 1
+    lanes = max(c["lanes"] for c in out["per_rank_concurrency"])
+    for rank, slots in enumerate(ref["stash_slots_per_rank"]):
+        assert sum(slots.values()) <= P - rank + lanes - 1, (rank, slots)
+    # the planned 1F1B ran too, labelled by its lag (or, if the planner chose lag 0, as a
+    # second "1F1B" entry)
+    planned = [k for k, e in sch.items() if e["schedule"] == "1F1B" and k != "1F1B"]
+    assert planned and all(k.startswith("1F1B+lag") or k.startswith("1F1B (planned)") for k in planned), sch
+    assert {"GPipe", "ZBH1"} <= {e["schedule"] for e in sch.values()}
