@@ -2696,8 +2696,24 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   if (use5 && cfg == 5 && split == 1 && !c_f32_accum && force_cfg < 0) cfg = 8;
   // 15: the four-wave register-staged 256x192 NT engine (gemm8); MIPIPE_GEMM8=1 uses it
   // wherever gemm3's M16 build would run without split-K
-  static const bool use8 = [] { const char* e = getenv("MIPIPE_GEMM8"); return e && e[0] == '1'; }();
-  if (!transA && !transB && (force_cfg == 15 || force_cfg == 16 || (use8 && cfg == 5 && split == 1 && force_cfg < 0))) {
+  // wherever gemm3's M16 build would run without split-K; MIPIPE_GEMM8=auto where its
+  // 256x192 grid fills whole rounds of 256 CUs better than 256x256 does: modelled time =
+  // rounds x tile area / tile efficiency, 0.9 measured per 256x192 tile against gemm3's
+  // 256x256 (profiles/r6_gemm8_engine.md: standalone, the 16K-token N = 768 / 2304 grids run
+  // 1.11-1.15x gemm3 and the 64K-token grids 0.88-0.95x).  Off by default: inside the step
+  // (2 lanes, 16K-token microbatches) auto measured 910K vs 942K tok/s -- the second lane
+  // already fills gemm3's partial rounds, and gemm8 pays its lower per-tile rate
+  static const int use8 = [] {
+    const char* e = getenv("MIPIPE_GEMM8");
+    return (e && e[0] == '1') ? 1 : ((e && e[0] == 'a') ? 2 : 0);
+  }();
+  bool pick8 = use8 == 1;
+  if (use8 == 2 && !transA && !transB && !c_f32_accum && cfg == 5 && split == 1 && force_cfg < 0) {
+    const float r256 = (float)((((M + 255) / 256) * ((N + 255) / 256) + 255) / 256);
+    const float r192 = (float)((((M + 255) / 256) * ((N + 191) / 192) + 255) / 256) * (0.75f / 0.9f);
+    pick8 = r192 < 0.97f * r256;
+  }
+  if (!transA && !transB && (force_cfg == 15 || force_cfg == 16 || (pick8 && cfg == 5 && split == 1 && force_cfg < 0))) {
     *split_out = 1;
     return force_cfg == 16 ? 16 : 15;
   }

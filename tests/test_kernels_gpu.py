@@ -411,7 +411,7 @@ def test_default_build_has_no_probe_engines():
     assert not _probe_engines()
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, pytest.param(8, marks=needs_probe_engines), 9, 10, 11, 12])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, pytest.param(8, marks=needs_probe_engines), 9, 10, 11, 12, 15, 16])
 @pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, "bias_gelu"), (1000, 2304, 256, "bias"), (256, 384, 128, "res"),
                                        (520, 136, 64, "none"), (512, 768, 3072, "dgelu"), (1000, 1000, 640, "none"),
                                        (768, 512, 128, "bias")])
@@ -779,7 +779,7 @@ def test_queue_probe_detects_shared_and_separate_queues():
     print(rep)
 
 
-@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 5])
+@pytest.mark.parametrize("cfg", [-1, 0, 1, 2, 3, 5, 15])
 @pytest.mark.parametrize("epi", ["dgelu", "none", "res"])
 def test_gemm_fused_colsum(cfg, epi):
     """Output column sums accumulated in the GEMM epilogue (the next layer's bias grad);
@@ -797,7 +797,7 @@ def test_gemm_fused_colsum(cfg, epi):
     close(cs, ref, atol=0.05 * (M ** 0.5), rtol=2e-2)
 
 
-@pytest.mark.parametrize("cfg", [-1, 10, 11, 5])
+@pytest.mark.parametrize("cfg", [-1, 10, 11, 5, 15])
 def test_gemm_dropout_epilogues_match_act_kernels(cfg):
     """Reference FFN fusions: linear1 + bias + ReLU + dropout in the GEMM epilogue equals
     linear1 -> act_fwd(relu, p); the linear2 dX GEMM with dReLU x mask (+ the linear1 bias
