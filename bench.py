@@ -789,7 +789,8 @@ def _concurrency_record(trainer) -> dict:
             "stash_slots": {str(k): v for k, v in mp.get("stash_slots", {}).items()},
             "p2p_channels": int(getattr(rt.p2p, "channels", 1)), "collective_placement": rt.coll_placement,
             # first-step cross-rank check of the issued p2p order and collective sequences
-            "comm_audit": None if au is None else (f"ok ({au['entries']} groups)" if au["ok"] else au["problems"])}
+            "comm_audit": None if au is None else ((f"ok ({au['entries']} groups, p2p {au.get('p2p', 'audited')})")
+                                                  if au["ok"] else au["problems"])}
 
 
 def _memory_plan_summary(trainer):
@@ -872,6 +873,9 @@ def run(a) -> None:
         targets = torch.randint(0, cfg.vocab_size, (m * a.mbs, a.seq), device=device, generator=g)
         if a.graphs and gpu:
             trainer.capture_graphs(tokens, targets)   # setup: capture per-microbatch HIP graphs
+        if gpu:
+            # HBM peaks from here on: the training steps, not the setup's eager step
+            torch.cuda.reset_peak_memory_stats(device)
 
     def sync():
         if world > 1:
@@ -995,8 +999,13 @@ def run(a) -> None:
         "bubble_source": src,
         "analytic_bubble": round(analytic_bubble(trainer.schedule, pp, m, trainer.v), 4),
         "model_tflops_per_gpu": round(flops / world / 1e12, 1),
-        "hbm_peak_gb_per_gpu": hbm_peak,   # max over ranks of the caching allocator's allocated peak
+        # max over ranks, GiB, over the training steps after setup: the caching allocator's
+        # RESERVED peak (what the device holds: HIP-graph pools keep freed blocks reserved --
+        # the allocated counter drops when a capture frees them), its allocated peak, and the
+        # device's used bytes at the end (mem_get_info)
+        "hbm_peak_gb_per_gpu": hbm_reserved,
         "hbm_reserved_peak_gb_per_gpu": hbm_reserved,
+        "hbm_allocated_peak_gb_per_gpu": hbm_peak,
         "hbm_device_used_gb_per_gpu": hbm_used,
         "attempt": attempt,
         "attempt_mode": os.environ.get("MIPIPE_BENCH_MODE", "in-process"),

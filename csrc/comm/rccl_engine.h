@@ -277,12 +277,23 @@ class RcclEngine {
     ncclDataType_t type;
     int peer;
   };
+  // ``after`` (optional): for a RECEIVE-ONLY group, order the channel stream after that event
+  // instead of after everything issued so far on the compute stream (a
+  // pre-posted receive then starts at post time, so the peer's matching send is not held
+  // behind this rank's unrelated compute).  The caller guarantees the receive buffers are
+  // free once ``after`` has fired: the native stage runner passes an event recorded at the
+  // start of the step, and every in-step message has a receive slot of its own
+  // (PipelineRuntime._plan_recv_arena).  A group with sends always follows the compute.
   int64_t post_raw(int channel, const std::vector<RawOp>& sends, const std::vector<RawOp>& recvs,
-                   hipStream_t compute) {
+                   hipStream_t compute, hipEvent_t after = nullptr) {
     check_channel(channel);
     hipStream_t cs = stream_[channel];
     ncclComm_t comm = comm_[channel];
-    order_after(compute, cs);
+    if (after != nullptr && sends.empty()) {
+      MP_HIP(hipStreamWaitEvent(cs, after, 0));
+    } else {
+      order_after(compute, cs);
+    }
     MP_NCCL(g_rccl->GroupStart());
     for (const auto& o : sends) {
       TORCH_CHECK(o.peer >= 0 && o.peer < nranks_, "RcclEngine: bad send peer ", o.peer);
@@ -356,7 +367,10 @@ class RcclEngine {
   // names the transfer every rank is stuck in instead of only the Python stack.
   py::list progress() {
     py::list out;
-    if (!trace_on_) return out;
+    // the watchdog thread calls this while the native tape runner (GIL released) records
+    // new groups: entries and head under trace_mu_, nothing once closed
+    std::lock_guard<std::mutex> lk(trace_mu_);
+    if (!trace_on_ || !open_) return out;
     const auto now = std::chrono::steady_clock::now();
     const size_t n = std::min<size_t>(trace_head_, kTrace);
     for (size_t i = trace_head_ - n; i < trace_head_; ++i) {
@@ -374,7 +388,10 @@ class RcclEngine {
     }
     return out;
   }
-  int64_t issued() const { return (int64_t)trace_head_; }
+  int64_t issued() {
+    std::lock_guard<std::mutex> lk(trace_mu_);
+    return (int64_t)trace_head_;
+  }
 
   void synchronize() {
     if (open_)
@@ -432,10 +449,13 @@ class RcclEngine {
   }
 
   void release_events() {
-    for (auto& e : trace_)
-      if (e.ev != nullptr) hipEventDestroy(e.ev);
-    trace_.clear();
-    trace_head_ = 0;
+    {
+      std::lock_guard<std::mutex> lk(trace_mu_);
+      for (auto& e : trace_)
+        if (e.ev != nullptr) hipEventDestroy(e.ev);
+      trace_.clear();
+      trace_head_ = 0;
+    }
     for (auto& kv : pending_) hipEventDestroy(kv.second);
     pending_.clear();
     for (hipEvent_t e : pool_) hipEventDestroy(e);
@@ -472,6 +492,7 @@ class RcclEngine {
   // one extra event record per group (MIPIPE_COMM_TRACE=0: none)
   void trace(int channel, int kind, hipStream_t cs, const std::vector<RawOp>& sends, const std::vector<RawOp>& recvs) {
     if (!trace_on_) return;
+    std::lock_guard<std::mutex> lk(trace_mu_);
     if (trace_.empty()) trace_.resize(kTrace);
     TraceEntry& e = trace_[trace_head_ % kTrace];
     if (e.ev == nullptr) MP_HIP(hipEventCreateWithFlags(&e.ev, hipEventDisableTiming));
@@ -498,6 +519,7 @@ class RcclEngine {
   }();
   std::vector<TraceEntry> trace_;
   size_t trace_head_ = 0;
+  std::mutex trace_mu_;     // trace_ / trace_head_: recorder thread vs watchdog (progress)
 
   std::vector<ncclComm_t> comm_;
   std::vector<hipStream_t> stream_;

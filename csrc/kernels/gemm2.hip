@@ -2723,7 +2723,15 @@ extern "C" int mp_gemm2_plan(int M, int N, int K, int transA, int transB, int c_
   // tail (S = 2) takes 37 vs 23.5 us at K = 768 and 60 vs 55 us at K = 3072; the hand-off of
   // a 256x256 f32 partial (LDS staging + 256 KiB out and back in, sc1 or plain + release
   // alike) costs about what the halved K loop saves (profiles/r5_gemm7_split_tail_null.txt)
+  // Probe-only: a timed-out partial hand-off cannot be reported to the host, so
+  // cfg 14 is reachable only in the A/B probe build (tools/build_ext.py --variant probes
+  // -D MP_PROBE_ENGINES), where test_gemm7_stream_k checks it
+#ifdef MP_PROBE_ENGINES
   static const bool use_sk = [] { const char* e = getenv("MIPIPE_GEMM_SK"); return e && e[0] == '1'; }();
+#else
+  constexpr bool use_sk = false;
+  if (force_cfg == 14) return -1;
+#endif
   // replaces the ping-pong engine's partial rounds and the bf16-output split-K slabs (f32
   // slab round trip through HBM + a reduce pass) of the gemm2 tiles alike
   if (!transA && !transB && !c_f32_accum && (force_cfg == 14 || (use_sk && force_cfg < 0 && cfg != 10 &&

@@ -152,6 +152,10 @@ class StageRunner {
   }
 
   void set_profile(bool on) { profile_ = on; }
+  // receive-only POSTs ordered after the step's start instead of the compute stream
+  // (RcclEngine::post_raw ``after``; PipelineRuntime turns it on with MIPIPE_RECV_EARLY)
+  void set_recv_early(bool on) { recv_early_ = on; }
+  bool recv_early() const { return recv_early_; }
 
   // one step on the current HIP stream of `device`
   void run() {
@@ -167,8 +171,12 @@ class StageRunner {
       sync_ev_.push_back(e);
     }
     auto on = [st](int64_t s) { return s ? reinterpret_cast<hipStream_t>(s) : st; };
+    if (recv_early_ && step_ev_ == nullptr) MP_HIPCHK(hipEventCreateWithFlags(&step_ev_, hipEventDisableTiming));
     py::gil_scoped_release nogil;
     int ng = 0;
+    // everything before this step (the previous step's readers of every receive slot, its
+    // lanes joined back, the optimizer) is ordered before this event
+    if (recv_early_) MP_HIPCHK(hipEventRecord(step_ev_, st));
     if (prof) MP_HIPCHK(hipEventRecord(ev_[0], st));
     for (const Instr& i : tape_) {
       switch (i.kind) {
@@ -189,7 +197,8 @@ class StageRunner {
           MP_HIPCHK(hipStreamWaitEvent(on(i.a), sync_ev_[i.slot], 0));
           break;
         case POST:
-          handles[i.slot] = i.engine->post_raw(i.channel, i.sends, i.recvs, st);
+          handles[i.slot] = i.engine->post_raw(i.channel, i.sends, i.recvs, st,
+                                               (recv_early_ && i.sends.empty()) ? step_ev_ : nullptr);
           engines[i.slot] = i.engine;
           break;
         case COLL:
@@ -313,6 +322,8 @@ class StageRunner {
   std::vector<hipEvent_t> sync_ev_;
   int64_t runs_ = 0;
   bool profile_ = false;
+  bool recv_early_ = false;
+  hipEvent_t step_ev_ = nullptr;
   bool profiled_ = false;
   std::vector<hipEvent_t> ev_;
 };
@@ -331,6 +342,8 @@ void register_runner(py::module& m) {
       .def("add_call", &StageRunner::add_call)
       .def("run", &StageRunner::run)
       .def("set_profile", &StageRunner::set_profile)
+      .def("set_recv_early", &StageRunner::set_recv_early)
+      .def("recv_early", &StageRunner::recv_early)
       .def("timeline", &StageRunner::timeline)
       .def("kinds", &StageRunner::kinds)
       .def("channels", &StageRunner::channels)

@@ -158,14 +158,24 @@ def max_inflight_microbatches(order, stages) -> int:
 def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, seq_len: int, device,
                    head_tokens: int = 0, budget_frac: float = 0.85, head_shards: int = 1,
                    stage_shards: int = 1, dtype=torch.bfloat16, graphs: bool = False, lanes: int = 1,
-                   hbm: Optional[float] = None) -> dict:
+                   hbm: Optional[float] = None, head_split: Optional[bool] = None) -> dict:
     """HBM plan of one pipeline rank and the recompute decision of ``recompute="auto"``:
     recompute only if the activation stash would not fit ``budget_frac`` of the device.
 
     bytes = parameters x 20 (bf16 weights + bf16 W^T copies + f32 master, grad, Adam m, v)
-          + in-flight microbatches x local layers x per-layer stash (config.stash_bytes_per_layer)
-          + logits of one head token chunk (bf16, gradient written in place; the whole
-            microbatch's with MIPIPE_HEAD_CHUNK=0) + 4 GB workspace.
+            + an f32 gradient per extra microbatch lane
+          + per stash slot: local layers x per-layer stash (config.stash_bytes_per_layer),
+            + the deferred weight-gradient inputs with a split backward (ZBH1 / ZBV:
+            config.wgrad_stash_bytes_per_layer, held from I to W)
+          + the last stage's logits per stash slot (kept from F to B, the gradient written
+            in place; one token chunk with MIPIPE_HEAD_CHUNK > 0)
+          + a distributed head's chunk logits: a transient of each captured head graph, so
+            one per microbatch with HIP graphs (each keeps a private pool), one eager
+          + backward temporaries: ~1.3 layer stashes per memory pool that holds them -- each
+            stash slot's graph pool with HIP graphs (a pool keeps its freed blocks reserved),
+            one set eager -- + 0.5 GB of workspace.
+    Reconciled with the RESERVED peak of the caching allocator (what the device actually
+    holds) on one MI355X (profiles/r6_hbm_reserved.md, tests/test_native_runner_gpu.py).
     The distributed head with ZeRO-1 (``head_shards`` = PP) keeps its f32 master and Adam
     moments (12 of the 20 bytes) for 1 / head_shards of the matrix: ``head_optimizer_bytes``
     is that per-rank optimizer state, ``head_state_bytes`` all of the head's.  ZeRO-1 over DP
@@ -173,12 +183,12 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     f32 arenas (the reference's precision): the f32 weights ARE the master, so sharding
     leaves them whole and splits only the Adam moments -- 12 + 8 / shards bytes per
     parameter (head: 12 + 8 / head_shards).
-    Calibrated on Llama-3 8B, seq 8192, PP=1: 186.3 GB measured peak without recompute.
     The stash is counted per stage from the slot plan of the rank's order
     (parallel/stash.py): the in-flight microbatches of each stage -- also with HIP graphs,
     whose captures share one pool per stash slot (``lanes``: slots are per microbatch lane;
     MIPIPE_STASH_RING=0 restores one private pool per graph, i.e. all m stashes).
-    ``hbm``: the device's bytes (default: the device's own; unbounded off the GPU)."""
+    ``hbm``: the device's bytes (default: the device's own; unbounded off the GPU).
+    ``head_split``: whether ``head_tokens`` is a distributed head's chunk (default: inferred)."""
     T = mbs * seq_len
     from .parallel.stash import stash_slots_per_stage
     layers_of = {s: layer_ranges[s][1] - layer_ranges[s][0] for s in my_stages}
@@ -190,19 +200,34 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     head_opt = shard_b * emb / max(1, head_shards) if head_tokens else 0.0
     head_state = (fixed_b * emb if head_tokens else 0.0) + head_opt
     slots = stash_slots_per_stage(order, my_stages, lanes if graphs else 1)
+    n_mb = len({a.mb for a in order if a is not None and a.stage in set(my_stages) and a.op == Op.F})
     if graphs and os.environ.get("MIPIPE_STASH_RING", "1") == "0":
-        n_mb = len({a.mb for a in order if a is not None and a.stage in set(my_stages) and a.op == Op.F})
         slots = {s: n_mb for s in my_stages}
+    split = any(a is not None and a.op == Op.I and a.stage in set(my_stages) for a in order)
     stash_layers = sum(slots.get(s, 1) * layers_of[s] for s in my_stages)   # stash-layer units
     inflight = max(slots.values(), default=1)
     from .models.native import _HEAD_CHUNK
-    logit_rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
+    last = len(layer_ranges) - 1
     logit_b = 4.0 if f32 else 2.0
-    fixed = (fixed_b + shard_b / max(1, stage_shards)) * nparams + head_state + logit_b * logit_rows * \
-        cfg.vocab_padded + 4e9
-    full = fixed + stash_layers * cfg.stash_bytes_per_layer(T, recompute=False)
-    rec = fixed + stash_layers * cfg.stash_bytes_per_layer(T, recompute=True) + \
-        cfg.stash_bytes_per_layer(T, recompute=False)
+    act_b = 2.0 if f32 else 1.0       # stash formulas count bf16 bytes
+    per_layer = act_b * cfg.stash_bytes_per_layer(T, recompute=False)
+    per_layer_rc = act_b * cfg.stash_bytes_per_layer(T, recompute=True)
+    wgrad = act_b * cfg.wgrad_stash_bytes_per_layer(T) if split else 0.0
+    logits = 0.0
+    if head_split is None:       # a distributed head's chunk is not the whole microbatch
+        head_split = bool(head_tokens) and (head_tokens != T or last not in my_stages)
+    if last in my_stages and not head_split:
+        rows = min(T, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else T
+        logits = logit_b * rows * cfg.vocab_padded * slots.get(last, 1)
+    elif head_tokens:
+        rows = min(head_tokens, _HEAD_CHUNK) if _HEAD_CHUNK > 0 else head_tokens
+        logits = logit_b * rows * cfg.vocab_padded * (max(1, n_mb) if graphs else 1)
+    pools = sum(slots.get(s, 1) for s in my_stages) if graphs else 1
+    temps = 1.3 * per_layer * pools + 0.5e9
+    fixed = (fixed_b + shard_b / max(1, stage_shards)) * nparams + head_state + \
+        4.0 * nparams * (max(1, lanes) - 1 if graphs else 0) + logits + temps
+    full = fixed + stash_layers * (per_layer + wgrad)
+    rec = fixed + stash_layers * (per_layer_rc + wgrad) + per_layer
     if hbm is not None:
         total = float(hbm)
     else:
@@ -233,7 +258,7 @@ def plan_rank_memory(cfg: NativeConfig, pp: int, v: int, style: str, layer_range
                                 head_tokens=ht,
                                 head_shards=pp if (head_zero and pp > 1 and chunks is not None) else 1,
                                 stage_shards=dp if dp_zero else 1, dtype=dtype, graphs=graphs, lanes=lanes,
-                                hbm=MI355X_HBM_BYTES if hbm is None else hbm)
+                                hbm=MI355X_HBM_BYTES if hbm is None else hbm, head_split=chunks is not None)
     return out
 
 
@@ -704,7 +729,8 @@ class PipelineTrainer:
                               self.device, head_tokens=head_tokens,
                               head_shards=self.mesh.pp if (self.head_zero and self.mesh.pp > 1) else 1,
                               stage_shards=self.mesh.dp if self.dp_zero else 1, dtype=mb["dtype"],
-                              graphs=mb["graphs"], lanes=lanes, hbm=mb["hbm"])
+                              graphs=mb["graphs"], lanes=lanes, hbm=mb["hbm"],
+                              head_split=self.head_chunks is not None)
 
     def _auto_lanes(self, pp: int, v: int, graphs: bool, m: int, mbs: int, seq_len: int) -> int:
         layers = sum(self.layer_ranges[st.stage_index][1] - self.layer_ranges[st.stage_index][0]
@@ -786,7 +812,11 @@ class PipelineTrainer:
         if self.coll is not None:
             self.coll.audit = None
         ok, problems, n = gather_and_check(audit, self.mesh.world_ctrl)
-        self.comm_audit = {"ok": ok, "entries": n, "problems": problems}
+        # whether this rank's log held its pipeline p2p (an eager step) or only collectives
+        # (a step replayed from the native tape issues p2p from C++, unlogged)
+        p2p_logged = any(e[0] == "p2p" for e in audit.entries)
+        self.comm_audit = {"ok": ok, "entries": n, "problems": problems,
+                           "p2p": "audited" if (p2p_logged or self.mesh.pp == 1) else "not covered (native replay)"}
         if not ok:
             raise RuntimeError("communication issued by the ranks does not match (would hang under RCCL):\n  "
                                + "\n  ".join(problems))
@@ -815,10 +845,33 @@ class PipelineTrainer:
             return
         inputs = [(c,) for c in torch.tensor_split(tokens, self.m, dim=0)] if self.is_first else None
         tg = list(torch.tensor_split(targets, self.m, dim=0)) if self.is_last else None
+        first = True
         while min(st.step_id for st in self.stages) < 2:
-            self.runtime.step(inputs, tg, [], return_outputs=False)
+            if not first and self.device.type == "cuda":
+                # the eager step's activations went back to the caching allocator's default
+                # pool; return them to the device before the graphs take their own pools, or
+                # the device holds both (113.8 vs 58.5 GB reserved on GPT-2 small, 2 x 64K
+                # tokens: profiles/r6_hbm_reserved.md)
+                torch.cuda.empty_cache()
+            first = False
+            # the first (eager) step issues every p2p post through Python: audit it here --
+            # the first train_step after capture replays the native tape, where only the
+            # collectives would be seen
+            audit = self._begin_comm_audit()
+            try:
+                self.runtime.step(inputs, tg, [], return_outputs=False)
+            except BaseException:
+                if audit is not None:
+                    self.runtime.p2p.audit = None
+                    if self.coll is not None:
+                        self.coll.audit = None
+                raise
+            if audit is not None:
+                self._end_comm_audit(audit)
         for a in self.optimizer.arenas:
             a.grad.zero_()
+        if self.device.type == "cuda":
+            torch.cuda.empty_cache()
 
     def bubble(self) -> float:
         return self.runtime.bubble()

@@ -152,6 +152,16 @@ class NativeConfig:
             per_tok += 3 * d + 2 * d
         return 2 * tokens * per_tok
 
+    def wgrad_stash_bytes_per_layer(self, tokens: int) -> int:
+        """bf16 output gradients one layer keeps from its input-gradient half (I) to its
+        weight-gradient half (W) of a split backward (ZBH1 / ZBV; models/native.py deferred
+        ``wjobs``): the GEMMs' dY -- QKV, attention output, FFN in (2 for SwiGLU) and out."""
+        d, f = self.d_model, self.d_ff
+        per_tok = self.qkv_dim + d + (2 * f if self.activation == "swiglu" else f) + d
+        if self.cross_attn:
+            per_tok += 3 * d + d
+        return 2 * tokens * per_tok
+
     def flops_per_token(self, seq_len: int) -> float:
         """Training FLOPs per token (fwd+bwd = 3x fwd), incl. attention and the LM head."""
         d = self.d_model

@@ -328,8 +328,9 @@ def linear(x: torch.Tensor, w: torch.Tensor, bias: Optional[torch.Tensor] = None
     """y = drop(act(x @ w^T + bias)) (+ residual).  x [T,K], w [N,K].  With an activation
     ``aux`` receives what the backward's dX epilogue needs (``linear_dx(act_input=aux)``):
     the pre-activation for ReLU, GELU's derivative at the pre-activation for GELU (one
-    sigmoid serves both here; the backward then multiplies).  ``p_drop`` (ReLU only) applies
-    the fused dropout of the reference FFN.  Returns (y, aux)."""
+    sigmoid serves both here; the backward then multiplies).  Unfused, a GELU aux goes to
+    ``act_bwd(..., saved="grad")``, a ReLU aux to ``act_bwd(..., saved="pre")``.  ``p_drop``
+    (ReLU only) applies the fused dropout of the reference FFN.  Returns (y, aux)."""
     if p_drop > 0 and act != "relu":
         raise ValueError("the fused GEMM dropout follows a ReLU epilogue")
     T, K = x.shape
@@ -703,9 +704,29 @@ def act_fwd(a: torch.Tensor, act: str, p_drop: float = 0.0, seed: int = 0, out=N
 
 
 def act_bwd(dg: torch.Tensor, a: torch.Tensor, act: str, dbias: Optional[torch.Tensor] = None,
-            p_drop: float = 0.0, seed: int = 0, out=None):
+            p_drop: float = 0.0, seed: int = 0, out=None, saved: str = "pre"):
+    """dA = dG * act'(.) (dropout mask regenerated from (seed, element index)), plus the
+    column sums into ``dbias``.  ``saved`` says what ``a`` holds: "pre" -- the pre-activation
+    (act_fwd's input; ReLU's aux from :func:`linear`) -- or "grad" -- act' itself, which is
+    what ``linear(act="gelu_tanh")`` stores in its aux (the two forms are not
+    interchangeable; passing a GELU aux as "pre" would silently give wrong gradients)."""
+    if saved not in ("pre", "grad"):
+        raise ValueError(f"saved must be 'pre' or 'grad', not {saved!r}")
     if out is None:
         out = torch.empty_like(dg)
+    if saved == "grad":
+        d = dg.float() * a.float()
+        if p_drop > 0:
+            if _gpu(dg):
+                raise ValueError("the dropout mask with a saved derivative is fused into linear_dx's epilogue")
+            d = d * _cpu_dropout_mask(a.shape, p_drop, seed, a.device)
+        out.copy_(d.to(out.dtype))
+        if dbias is not None:
+            if _gpu(dg):
+                _ext().colsum(out, dbias)
+            else:
+                dbias += out.float().reshape(-1, out.shape[-1]).sum(0)
+        return out
     if _gpu(dg):
         _ext().act_bwd(dg, a, out, dbias, ACT[act], float(p_drop), int(seed))
         return out

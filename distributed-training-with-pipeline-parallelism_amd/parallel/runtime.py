@@ -226,6 +226,12 @@ class PipelineRuntime:
         model admits raises instead of running."""
         from .simulate import check_lowered
         S = self.num_stages
+        # receive-only posts of the native tape start at post time (ordered after the step's
+        # start, not the compute stream: VERDICT r5 #6); every independent-model proof below
+        # admits that (check_lowered recv_early), the serial one is unaffected by it
+        # (MIPIPE_RECV_EARLY=0: ordered after the compute stream, as before)
+        self.recv_early = (getattr(p2p, "kind", "") == "native" and self.device.type == "cuda"
+                           and os.environ.get("MIPIPE_RECV_EARLY", "1") != "0")
         has_coll = any(isinstance(e, Action) and (e.op == Op.REDUCE_HEAD or (e.op == Op.REDUCE_GRAD and self.dp > 1))
                        for es in program.values() for e in es)
         self.coll_placement = "none"
@@ -251,7 +257,8 @@ class PipelineRuntime:
                 from .comm import agree
                 overlap = agree(overlap, self.vote_group, self.device)
             if overlap:
-                check_lowered(program, S, channels=getattr(p2p, "channels", 1), dp=self.dp)
+                check_lowered(program, S, channels=getattr(p2p, "channels", 1), dp=self.dp,
+                              recv_early=self.recv_early)
                 self.coll_placement = ("overlapped (independent queues, probed)" if kind == "native"
                                        else "overlapped (gloo host transport)")
             else:
@@ -259,7 +266,7 @@ class PipelineRuntime:
                 self.coll_placement = "step end (serial-model proof)"
         if getattr(p2p, "channels", 1) > 1:
             try:
-                check_lowered(program, S, channels=p2p.channels, dp=self.dp)
+                check_lowered(program, S, channels=p2p.channels, dp=self.dp, recv_early=self.recv_early)
             except RuntimeError as e:
                 log.warning("two-channel p2p order not provably safe (%s): single channel", e)
                 p2p.use_single_channel()
@@ -346,7 +353,7 @@ class PipelineRuntime:
             # the exact program with its lane queues, under the model the placement relies on
             from .simulate import check_lowered
             check_lowered(self.program_all, self.num_stages, channels=getattr(self.p2p, "channels", 1), dp=self.dp,
-                          lanes=n)
+                          lanes=n, recv_early=getattr(self, "recv_early", False))
         self.lanes = n
         if self.device.type == "cuda":
             # the f32 split-K planner counts 256 / n CUs per GEMM: the other lanes fill the
@@ -720,6 +727,8 @@ class PipelineRuntime:
         if rec is not None:
             if rec.valid:
                 self.native_runner = rec.runner
+                if getattr(self, "recv_early", False) and hasattr(self.native_runner, "set_recv_early"):
+                    self.native_runner.set_recv_early(True)
                 self._native_outputs = list(out) if (mode and out is not None) else None
                 self.native_reason = f"recorded {rec.runner.size} instructions"
             elif "captured during the recording step" in rec.reason:

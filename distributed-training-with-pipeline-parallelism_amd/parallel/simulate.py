@@ -169,7 +169,7 @@ def message_channel(key: tuple) -> int:
 
 
 def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: int = 1, serial: bool = False,
-                  dp: int = 1, lanes: int = 1) -> None:
+                  dp: int = 1, lanes: int = 1, recv_early: bool = False) -> None:
     """Raise RuntimeError if the lowered program can hang under RCCL semantics.
 
     Queues of a rank (each a FIFO in host issue order = program order):
@@ -199,7 +199,12 @@ def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: in
     every compute issued before it (the runtime orders a post after the lanes whose output
     it sends, a reduction after all of them).  Splitting the compute FIFO only removes
     ordering edges, so a program proven with ``lanes=1`` is safe with any lane count; the
-    parameter lets the runtime prove the exact program it runs."""
+    parameter lets the runtime prove the exact program it runs.
+
+    ``recv_early`` (independent model): a channel part of a comm group that only RECEIVES does
+    not wait for the compute issued before it -- the native stage runner orders such a post
+    after the start of the step instead (RcclEngine::post_raw ``after``, VERDICT r5 #6), so
+    it starts at post time; it still waits for the entries before it on its channel queue."""
     comp_orders = {r: [e for e in es if isinstance(e, Action) and e.op.is_compute] for r, es in program.items()}
     split = uses_split_backward(comp_orders)
     head = head_ranks_of(comp_orders)
@@ -217,7 +222,9 @@ def check_lowered(program: Dict[int, List[Entry]], num_stages: int, channels: in
                 for op in e.ops:
                     by_ch.setdefault(chan(op.key), []).append(op)
                 for ch in sorted(by_ch):
-                    lst.append((0 if serial else ("p", ch), "g", by_ch[ch], ncomp - 1))
+                    only_recv = all(op.action.op.is_recv for op in by_ch[ch])
+                    lst.append((0 if serial else ("p", ch), "g", by_ch[ch],
+                                -1 if (recv_early and not serial and only_recv) else ncomp - 1))
             elif e.op.is_compute:
                 cq = "c" if (lanes <= 1 or e.mb is None) else ("c", e.mb % lanes)
                 lst.append((0 if serial else cq, "c", e, ncomp - 1))

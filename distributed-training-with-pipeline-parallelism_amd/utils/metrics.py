@@ -39,7 +39,10 @@ class MetricsLogger:
         rec = {"step": step, "loss": loss, "lr": lr, "tokens_per_s": tokens / step_s if step_s > 0 else None,
                "step_ms": step_s * 1e3, "grad_norm": grad_norm, "bubble": bubble, "time": time.time()}
         if self.device is not None and self.device.type == "cuda":
-            rec["hbm_peak_gb"] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30
+            # reserved: what the device holds (HIP-graph pools keep freed blocks reserved;
+            # the allocated counter drops when a capture frees them)
+            rec["hbm_peak_gb"] = torch.cuda.max_memory_reserved(self.device) / 2 ** 30
+            rec["hbm_allocated_peak_gb"] = torch.cuda.max_memory_allocated(self.device) / 2 ** 30
         rec.update(extra)
         if self._f is not None:
             self._f.write(json.dumps(rec) + "\n")

@@ -439,6 +439,7 @@ def test_gemm2_configs(cfg, M, N, K, epi):
     close(y, ref)
 
 
+@needs_probe_engines
 @pytest.mark.parametrize("M,N,K,epi", [(8192, 768, 768, "bias"), (4000, 1000, 640, "none"),
                                        (32768, 768, 2304, "bias_gelu"), (24576, 768, 3072, "res"),
                                        (8192, 768, 2304, "dgelu"), (8192, 768, 3072, "colsum")])

@@ -209,17 +209,19 @@ def _train_mem(schedule, ring, m=16, steps=4):
         torch.zeros(1, device=dev)       # initialise the device before its memory stats
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        torch.cuda.reset_peak_memory_stats(dev)
-        base = torch.cuda.memory_allocated(dev)
+        base = torch.cuda.memory_reserved(dev)
         tr = PipelineTrainer(cfg, pp=1, schedule=schedule, n_microbatches=m, mbs=4, seq_len=256, device=dev,
                              seed=3, graphs=True, lr=1e-2)
         g = torch.Generator(device="cuda").manual_seed(7)
         x = torch.randint(0, cfg.vocab_size, (m * 4, 256), device=dev, generator=g)
         y = torch.randint(0, cfg.vocab_size, (m * 4, 256), device=dev, generator=g)
         tr.capture_graphs(x, y)
+        torch.cuda.reset_peak_memory_stats(dev)
         losses = [float(tr.train_step(x, y)) for _ in range(steps)]
         torch.cuda.synchronize()
-        peak = torch.cuda.max_memory_allocated(dev) - base
+        # what the device holds: the reserved peak -- graph pools keep their
+        # freed blocks, so the allocated counter under-reports
+        peak = torch.cuda.max_memory_reserved(dev) - base
         slots = [st.stash_slots() for st in tr.stages] + [tr.lanes]
         del tr
         torch.cuda.empty_cache()
@@ -241,11 +243,46 @@ def test_stash_ring_follows_the_schedule_under_graphs():
     l_on, p_1f1b, s_1f1b = _train_mem("1F1B", True)
     l_off, p_1f1b_off, _ = _train_mem("1F1B", False)
     l_g, p_gpipe, s_gpipe = _train_mem("GPipe", True)
-    assert l_on == pytest.approx(l_off, rel=1e-4)
-    assert l_g == pytest.approx(l_on, rel=1e-4)
+    # (f32 atomics: 1.2e-4 relative seen between GPipe and 1F1B after 4 steps at lr 1e-2;
+    # a backward reading another microbatch's stash moves the loss by percents)
+    assert l_on == pytest.approx(l_off, rel=5e-4)
+    assert l_g == pytest.approx(l_on, rel=5e-4)
     assert abs(l_on[-1] - l_on[0]) > 0.05    # the steps moved the weights a lot (sensitivity)
     lanes = s_1f1b[-1]
     assert s_gpipe[0] == 16 and s_1f1b[0] == lanes and lanes <= 4, (s_gpipe, s_1f1b)
     # the stash difference: GPipe holds 16 stashes, 1F1B one per lane
     assert p_1f1b < 0.75 * p_gpipe, (p_1f1b, p_gpipe)
     assert p_1f1b < 0.75 * p_1f1b_off, (p_1f1b, p_1f1b_off)
+
+
+@pytest.mark.parametrize("schedule", ["GPipe", "1F1B", "ZBH1"])
+@pytest.mark.parametrize("mbs,m", [(8, 2), (16, 8)])
+def test_hbm_plan_matches_the_reserved_peak(schedule, mbs, m):
+    """the HBM plan (engine.plan_recompute) is within 10 % of what the device
+    really holds in training -- the caching allocator's RESERVED peak over steps after the
+    setup -- for GPipe, 1F1B and ZBH1 on one GPU (GPT-2 small, seq 1024, HIP graphs, the
+    trainer's lanes).  At m = 2 every schedule holds one stash per lane; at m = 8 GPipe holds
+    8 and 1F1B / ZBH1 one per lane (ZBH1 also its deferred weight-gradient inputs)."""
+    from mipipe.models.config import NativeConfig
+    cfg = NativeConfig.gpt2("small")
+    dev = torch.device("cuda", 0)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    base = torch.cuda.memory_reserved(dev)
+    tr = PipelineTrainer(cfg, pp=1, schedule=schedule, n_microbatches=m, mbs=mbs, seq_len=1024, device=dev,
+                         seed=0, graphs=True)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randint(0, cfg.vocab_size, (m * mbs, 1024), device=dev, generator=g)
+    y = torch.randint(0, cfg.vocab_size, (m * mbs, 1024), device=dev, generator=g)
+    tr.capture_graphs(x, y)
+    torch.cuda.reset_peak_memory_stats(dev)
+    for _ in range(2):
+        tr.train_step(x, y)
+    torch.cuda.synchronize()
+    reserved = torch.cuda.max_memory_reserved(dev) - base
+    plan = tr.memory_plan["bytes_no_recompute"]
+    slots = sum(tr.memory_plan["stash_slots"].values())
+    del tr
+    torch.cuda.empty_cache()
+    assert slots == (m if schedule == "GPipe" else 2), slots
+    assert 0.9 * reserved <= plan <= 1.1 * reserved, (schedule, mbs, m, plan / 1e9, reserved / 1e9)

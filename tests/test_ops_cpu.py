@@ -108,6 +108,13 @@ def test_linear_family_matches_autograd():
     fused = ops.linear_dx(dz, w2, act_input=aux, act="gelu_tanh")
     unf = ops.act_bwd(ops.linear_dx(dz, w2), p0, "gelu_tanh")
     torch.testing.assert_close(fused, unf, atol=1e-5, rtol=1e-5)
+    # linear's GELU aux is the derivative -- act_bwd takes it only as saved="grad"
+    via_aux = ops.act_bwd(ops.linear_dx(dz, w2), aux, "gelu_tanh", saved="grad")
+    torch.testing.assert_close(via_aux, unf, atol=1e-5, rtol=1e-5)
+    wrong = ops.act_bwd(ops.linear_dx(dz, w2), aux, "gelu_tanh")   # the pre-activation form
+    assert not torch.allclose(wrong, unf, atol=1e-3)
+    with pytest.raises(ValueError):
+        ops.act_bwd(dz, dz, "gelu_tanh", saved="derivative")
     yr, _ = ops.linear(x, w, b, residual=r)
     torch.testing.assert_close(yr, x @ w.t() + b + r, atol=1e-5, rtol=1e-5)
 

@@ -61,8 +61,10 @@ def test_validate_lower_and_no_deadlock(name, P, m, v):
     o = generate(name, P, m, v)
     validate(o, P, v, m)
     prog = lower(o, P, v)  # runs check_lowered (one comm stream per rank)
-    # the native engine's per-direction channels (2 comm streams per rank) must be safe too
+    # the native engine's per-direction channels (2 comm streams per rank) must be safe too,
+    # also with receive-only posts started at post time
     check_lowered(prog, P * v, channels=2)
+    check_lowered(prog, P * v, channels=2, recv_early=True)
     # every send has exactly one matching recv with the same key, posted by the peer
     sends, recvs = {}, {}
     for r, es in prog.items():
@@ -306,8 +308,25 @@ def test_overlapped_programs_proven_with_and_without_lanes(name, v, P, dp):
     prog = add_head_reduce(lower(ho, P, v, "loop", head_costs=hc))
     for ch in (1, 2):
         for lanes in (1, 2):
-            check_lowered(prog, P * v, channels=ch, dp=dp, lanes=lanes)
+            for early in (False, True):
+                check_lowered(prog, P * v, channels=ch, dp=dp, lanes=lanes, recv_early=early)
     check_lowered(defer_collectives(prog), P * v, serial=True, dp=dp)
+
+
+def test_recv_early_lets_a_receive_start_before_earlier_compute():
+    """check_lowered(recv_early=True) models a receive-only post as starting at post time
+    (its start no longer waits for the rank's earlier compute, only for its channel queue).
+    1F1B's lowered program has such pre-posted receives; it is proven with them in the
+    independent model, and the serial model (one FIFO per rank) is unaffected."""
+    from mipipe.parallel.lower import lower as _lower
+    from mipipe.parallel.ir import CommGroup
+    P, m = 2, 4
+    prog = _lower(generate("1F1B", P, m, 1), P, 1)
+    recv_only = [e for es in prog.values() for e in es if isinstance(e, CommGroup)
+                 and all(op.action.op.is_recv for op in e.ops)]
+    assert recv_only, "1F1B's lowered program has receive-only groups (pre-posted receives)"
+    check_lowered(prog, P, channels=2, recv_early=True)
+    check_lowered(prog, P, serial=True, recv_early=True)   # no effect on the serial model
 
 
 def test_microbatch_rate_interpolates_the_measured_table():

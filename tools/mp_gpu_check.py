@@ -49,9 +49,15 @@ def main():
         n = x.shape[0] // dp
         r = tr.mesh.dp_rank
         x, y = x[r * n:(r + 1) * n].contiguous(), y[r * n:(r + 1) * n].contiguous()
-    base = torch.cuda.memory_allocated(device) if a.mem else 0
+    if a.mem:
+        torch.cuda.empty_cache()
+    base = torch.cuda.memory_reserved(device) if a.mem else 0
     if a.graphs:
         tr.capture_graphs(x, y)
+    if a.mem:
+        # the steady state: what the device holds for the training steps (reserved: graph
+        # pools keep their freed blocks), not the setup's eager step
+        torch.cuda.reset_peak_memory_stats(device)
     losses, norms = [], []
     for _ in range(a.steps):
         loss = tr.train_step(x, y)
@@ -65,7 +71,7 @@ def main():
     mem = None
     if a.mem:
         torch.cuda.synchronize()
-        mine = torch.tensor([torch.cuda.max_memory_allocated(device) - base,
+        mine = torch.tensor([torch.cuda.max_memory_reserved(device) - base,
                              float(sum(st.stash_slots() for st in tr.stages))], dtype=torch.float64, device=device)
         allv = [torch.zeros_like(mine) for _ in range(world)] if world > 1 else [mine]
         if world > 1:
