@@ -132,9 +132,11 @@ BASE_CONFIGS = {
     8: [("gpt2-medium Interleaved1F1B PP=8 v=2 (configs/gpt2_medium_interleaved_pp8.yaml)",
          ["--model", "gpt2-medium", "--schedule", "Interleaved1F1B", "--vstages", "2", "--mbs", "8",
           "--microbatches", "16"], 30.0),
+        # selective recompute from the HBM plan: the fewest recomputed layers
+        # per stage that fit (config.recompute_layers in the record), instead of every layer
         ("llama3-8b 1F1B PP=8 recompute (configs/llama3_8b_1f1b_pp8.yaml)",
          ["--model", "llama3-8b", "--schedule", "1F1B", "--mbs", "1", "--microbatches", "16", "--seq", "8192",
-          "--recompute", "1"], 120.0),
+          "--recompute", "auto"], 120.0),
         # (BASELINE.json names recompute only for the PP = 8 config; here the HBM plan decides
         # from the schedule's real in-flight stashes -- parallel/stash.py)
         ("llama3-8b DP=2 x PP=4 recompute auto (configs/llama3_8b_dp2_pp4.yaml)",
@@ -179,8 +181,9 @@ def parse(argv=None):
     # (not "--v": torch.distributed.run's argparse would take it for an abbreviation of
     # its --virtual-local-rank even after the script name)
     ap.add_argument("--vstages", type=int, default=None, help="virtual stages per rank (interleaved)")
-    ap.add_argument("--recompute", nargs="?", const="1", default="0", choices=["0", "1", "auto"],
-                    help="activation recompute: 1 (on), 0 (off), auto (HBM plan: only if the stash does not fit)")
+    ap.add_argument("--recompute", nargs="?", const="1", default="0",
+                    help="activation recompute: 1 (every layer), 0 (off), auto (selective: the fewest layers per "
+                         "stage the HBM plan needs, 0 if the stash fits), or k (the first k layers of every stage)")
     ap.add_argument("--graphs", type=int, default=None,
                     help="replay per-microbatch stage compute as HIP graphs + native tape (default: on with a GPU)")
     ap.add_argument("--no-split-head", action="store_true",
@@ -235,6 +238,20 @@ def compare_model(a, pp: int) -> str:
             if MODEL_LAYERS[cand] >= 2 * pp:
                 return cand
     return a.model
+
+
+def _recompute_arg(v: str):
+    """--recompute: "0" / "1" / "auto" / an int k (selective: the first k layers per stage)."""
+    v = str(v).strip().lower()
+    if v in ("auto", "selective"):
+        return "auto"
+    if v in ("1", "true", "on", "full"):
+        return True
+    if v in ("0", "false", "off", "none"):
+        return False
+    if v.startswith("k=") or v.isdigit():
+        return int(v[2:] if v.startswith("k=") else v)
+    raise SystemExit(f"--recompute: 0, 1, auto or an integer, not {v!r}")
 
 
 def extra_schedules(a) -> list:
@@ -746,7 +763,7 @@ def merge_results(headline: dict, results: dict, a) -> dict:
             if "tok_s" in e:
                 c = r.get("config", {})
                 e.update({k: c.get(k) for k in ("model", "schedule", "v", "parallelism", "micro_batch", "microbatches",
-                                                 "seq_len", "recompute", "global_batch")})
+                                                 "seq_len", "recompute", "recompute_layers", "global_batch")})
             base[name] = e
     if base:
         out["baseline_configs"] = base
@@ -863,7 +880,7 @@ def run(a) -> None:
         dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.dtype or ("bf16" if gpu else "fp32")]
         trainer = PipelineTrainer(cfg, pp=pp, dp=dp, schedule=a.schedule, n_microbatches=m,
                                   mbs=a.mbs, seq_len=a.seq, v=a.vstages, device=device,
-                                  recompute=a.recompute if a.recompute == "auto" else a.recompute == "1", seed=0,
+                                  recompute=_recompute_arg(a.recompute), seed=0,
                                   split_head=False if a.no_split_head else None, graphs=bool(a.graphs) and gpu,
                                   dtype=dtype, head_max_lag=a.head_max_lag)
         describe["fn"] = trainer.describe
@@ -1026,6 +1043,7 @@ def run(a) -> None:
                                        else "f32") if dp > 1 else None,
                    "head_zero": bool(getattr(trainer, "head_zero", False)) and trainer.head is not None,
                    "recompute": trainer.recompute,
+                   "recompute_layers": getattr(trainer, "recompute_layers", None),
                    "memory_plan": _memory_plan_summary(trainer),
                    "recv_arena_mb": round(rt.recv_arena_bytes / 2 ** 20, 1),
                    "plain_gemms": _plain_summary(),

@@ -44,7 +44,9 @@ class TrainSection:
     lr_schedule: str = "cosine"         # cosine | constant
     weight_decay: float = 0.1
     max_grad_norm: float = 1.0
-    recompute: Union[bool, str] = False   # True, False or "auto" (engine.plan_recompute: HBM plan)
+    # True (every layer), False, "auto" (selective: the fewest recomputed layers per stage the
+    # HBM plan needs, engine.plan_recompute) or an int k (the first k layers of every stage)
+    recompute: Union[bool, str, int] = False
     graphs: Optional[bool] = None       # HIP-graph replay + native stage runner (None: on for GPU)
     seed: int = 0
     data: str = "synthetic"             # synthetic | pattern[:K] (learnable permutation walk) | path to a uint16/int32 token file (memory-mapped)

@@ -228,6 +228,21 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
         4.0 * nparams * (max(1, lanes) - 1 if graphs else 0) + logits + temps
     full = fixed + stash_layers * (per_layer + wgrad)
     rec = fixed + stash_layers * (per_layer_rc + wgrad) + per_layer
+
+    def selective(k: int) -> float:
+        """bytes with the first ``k`` local layers of every stage recomputed (their stash is
+        the layer input; one layer's full stash is rebuilt at a time in the backward)."""
+        if k <= 0:
+            return full
+        kept = sum(slots.get(s_, 1) * max(0, layers_of[s_] - k) for s_ in my_stages)
+        rc = sum(slots.get(s_, 1) * min(k, layers_of[s_]) for s_ in my_stages)
+        return fixed + kept * (per_layer + wgrad) + rc * (per_layer_rc + wgrad) + per_layer
+    # selective recompute (VERDICT r5 #4): the fewest recomputed layers per stage whose plan
+    # fits the budget -- 0 if the whole stash fits, every layer if nothing less does
+    max_layers = max(layers_of.values(), default=0)
+    total_ = float(hbm) if hbm is not None else (torch.cuda.get_device_properties(device).total_memory
+                                                 if device.type == "cuda" else float("inf"))
+    k_fit = next((k for k in range(max_layers + 1) if selective(k) <= budget_frac * total_), max_layers)
     if hbm is not None:
         total = float(hbm)
     else:
@@ -235,7 +250,8 @@ def plan_recompute(cfg: NativeConfig, layer_ranges, my_stages, order, mbs: int, 
     return dict(inflight=inflight, stash_slots=slots, layers=nlayers, bytes_no_recompute=full, bytes_recompute=rec,
                 hbm=total,
                 recompute=bool(full > budget_frac * total), head_state_bytes=head_state,
-                head_optimizer_bytes=head_opt)
+                head_optimizer_bytes=head_opt, recompute_layers=k_fit, bytes_selective=selective(k_fit),
+                max_stage_layers=max_layers, selective_fn=selective)
 
 
 # HBM the planners assume off the GPU (CPU tests, the supervisor's plan child): one MI355X
@@ -596,8 +612,18 @@ class PipelineTrainer:
         self._my_stages = my_stages
         self.memory_plan = self._plan_memory(self.planned_lanes if graphed else 1)
         self.recompute_requested = recompute
+        max_layers = self.memory_plan["max_stage_layers"]
         if recompute == "auto":
-            recompute = self.memory_plan["recompute"]
+            # selective: the fewest recomputed layers per stage that fit the HBM budget
+            k = self.memory_plan["recompute_layers"]
+        elif recompute is True:
+            k = max_layers
+        elif recompute is False or recompute is None:
+            k = 0
+        else:
+            k = max(0, min(int(recompute), max_layers))
+        self.recompute_layers = k
+        recompute = k > 0
         self.recompute = bool(recompute)
         # ZeRO-1 over DP replicas (MIPIPE_DP_ZERO=0: replicated master / moments, gradient
         # all-reduced): each replica owns 1/dp of every stage arena -- its f32 master and Adam
@@ -607,7 +633,7 @@ class PipelineTrainer:
         self.stages: List[NativeStage] = []
         for s in my_stages:
             model = NativeModel(cfg, s, num_stages, self.device, layer_range=layer_ranges[s], seed=seed,
-                                recompute=recompute, mbs=mbs, seq_len=seq_len, dtype=dtype, head=self.head,
+                                recompute=self.recompute_layers, mbs=mbs, seq_len=seq_len, dtype=dtype, head=self.head,
                                 arena_multiple=8 * self.mesh.dp if self.dp_zero else 8)
             egroup = self.mesh.embed_group if (tied_pp and (s == 0 or s == num_stages - 1)) else None
             self.stages.append(NativeStage(model, mbs, seq_len, dp_group=self.mesh.dp_group, embed_group=egroup,
@@ -630,10 +656,11 @@ class PipelineTrainer:
         if graphed and self.lanes != self.planned_lanes:
             # the runtime took fewer lanes than planned: re-plan with the real count
             self.memory_plan = self._plan_memory(self.lanes)
-            if self.recompute_requested == "auto" and self.memory_plan["recompute"] != self.recompute:
+            if self.recompute_requested == "auto" and self.memory_plan["recompute_layers"] != self.recompute_layers:
                 raise RuntimeError(f"recompute='auto' planned with {self.planned_lanes} microbatch lanes, but the "
                                    f"runtime runs {self.lanes}: the HBM plan's decision changes "
-                                   f"({self.recompute} -> {self.memory_plan['recompute']}); set MIPIPE_LANES")
+                                   f"({self.recompute_layers} -> {self.memory_plan['recompute_layers']} recomputed "
+                                   f"layers per stage); set MIPIPE_LANES")
         arenas = [st.arena for st in self.stages]
         if self.dp_zero:
             dp, dr = self.mesh.dp, self.mesh.dp_rank

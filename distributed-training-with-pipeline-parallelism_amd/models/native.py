@@ -650,7 +650,7 @@ class Block:
             dk, dv = dkv[:, :d], dkv[:, d:]
         # the in_proj bias grads stay weight-gradient jobs (colsum kernels off the critical
         # path): the attention kernels' fused column sums (dbias=) cost 5 % of the reference
-        # step here (tools/ab_ref_dbias.sh: 574-579K vs 609-610K tok/s, L8H8)
+        # step here (tools/runs/archive/ab_ref_dbias.sh: 574-579K vs 609-610K tok/s, L8H8)
         ops.attn_bwd(q, k, v, o, do, st[key + "lse"], dq, dk, dv, B, S, S, H, H, Dh, False, p_drop=cfg.dropout,
                      seed=seed)
         if self_attn:
@@ -927,10 +927,16 @@ class NativeModel:
         # a side stream measured no concurrency with the other lane's graphs
         self.wgrad_side = True
         self.device = torch.device(device)
-        self.recompute = recompute
         if layer_range is None:
             layer_range = balanced_layer_ranges(cfg, num_stages, seq_len)[stage_index]
         self.layer_range = layer_range
+        # activation recompute: True / False (every layer / none), or an int k -- the first k
+        # local layers keep only their input and rebuild their stash in the backward
+        # (selective, engine.plan_recompute picks k from the HBM plan)
+        n_local = layer_range[1] - layer_range[0]
+        self.recompute_layers = (n_local if recompute is True else 0) if isinstance(recompute, bool) or \
+            recompute is None else max(0, int(recompute))
+        self.recompute = self.recompute_layers > 0
         specs: List[ParamSpec] = []
         d = cfg.d_model
         if self.first:
@@ -995,8 +1001,8 @@ class NativeModel:
             ctx.misc["tokens"] = tokens
         else:
             h = x
-        for blk in self.blocks:
-            h = blk.forward(h, B, S, ctx, recompute=self.recompute)
+        for li, blk in enumerate(self.blocks):
+            h = blk.forward(h, B, S, ctx, recompute=li < self.recompute_layers)
         if not self.last:
             return h
         # final norm + head + fused CE (grad computed now, consumed by the backward)

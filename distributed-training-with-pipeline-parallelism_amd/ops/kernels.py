@@ -21,7 +21,7 @@ LOG2E = 1.4426950408889634
 # dX GEMM shape is timed once on both (outside graph capture) and keeps the faster.
 # hipBLASLt wins some isolated K = 768 - 3072 NT shapes by 5-12 %
 # (profiles/r2_kernel_microbench.json) but not inside the GPT-2 / reference steps
-# (tools/ab_plain_gemm.sh: 883.6K / 889.4K tok/s auto vs 889.9K / 888.1K hip), so "auto"
+# (tools/runs/archive/ab_plain_gemm.sh: 883.6K / 889.4K tok/s auto vs 889.9K / 888.1K hip), so "auto"
 # stays opt-in.  Fused-epilogue GEMMs always use the HIP kernels.
 GEMM_BACKEND = os.environ.get("MIPIPE_GEMM", "hip")
 _PLAIN_BEST: dict = {}

@@ -444,3 +444,64 @@ def test_schedule_margin_depends_on_traffic():
     # interleaved with two chunks per rank sends twice the activations: the full margin
     name_i, eff_i = pick_schedule(cfg, 2, 8, 32, 1024, candidates=("1F1B", "Interleaved1F1B"))
     assert eff_i["Interleaved1F1B"] < eff_i["1F1B"] * 1.03 and name_i == "1F1B", eff_i
+
+
+
+def test_selective_recompute_picks_the_fewest_layers_that_fit():
+    """recompute="auto" recomputes the fewest layers per stage whose plan fits
+    the budget: 0 when the stash fits, every layer only when nothing less does, and the
+    bytes fall monotonically with k.  Llama-3 8B, seq 8192, one MI355X: GPipe m = 4 (4
+    stashes of 32 layers) needs some layers recomputed, 1F1B m = 2 none."""
+    import torch
+    from mipipe.engine import plan_recompute
+    from mipipe.models.config import NativeConfig
+    from mipipe.models.native import balanced_layer_ranges
+    from mipipe.parallel.schedules import generate
+    cfg = NativeConfig.llama3("8b")
+    lr = balanced_layer_ranges(cfg, 1, 8192, head_on_last=True)
+    hbm = 288 * 2 ** 30
+    p1 = plan_recompute(cfg, lr, [0], generate("1F1B", 1, 2, 1)[0], 1, 8192, torch.device("cpu"),
+                        head_tokens=8192, hbm=hbm)
+    assert p1["recompute_layers"] == 0 and not p1["recompute"]
+    p4 = plan_recompute(cfg, lr, [0], generate("GPipe", 1, 4, 1)[0], 1, 8192, torch.device("cpu"),
+                        head_tokens=8192, hbm=hbm)
+    k = p4["recompute_layers"]
+    assert p4["recompute"] and 0 < k < 32, k
+    f = p4["selective_fn"]
+    assert f(k) <= 0.85 * hbm < f(k - 1)
+    assert all(f(i + 1) < f(i) for i in range(32))
+    assert f(32) == pytest.approx(p4["bytes_recompute"]) and f(0) == p4["bytes_no_recompute"]
+    # nothing fits: every layer
+    p_small = plan_recompute(cfg, lr, [0], generate("GPipe", 1, 4, 1)[0], 1, 8192, torch.device("cpu"),
+                             head_tokens=8192, hbm=64 * 2 ** 30)
+    assert p_small["recompute_layers"] == 32
+
+
+def test_pick_schedule_records_lags_and_bounds_the_stash_by_hbm():
+    """every candidate of schedule="auto" is planned under the HBM bound and
+    its record carries the head lag it assumed, its largest per-rank stash and planned GB.
+    GPT-2 small at P = 8 (16K-token microbatches): whatever wins fits with margin.  Llama-3
+    8B at P = 8 on a hypothetical 64 GB device: no candidate keeps a lag whose stash would
+    not fit -- the lag falls back toward the schedule's own depth (ZBH1: <= P + lanes slots)."""
+    from mipipe.engine import pick_schedule
+    from mipipe.models.config import NativeConfig
+    det = {}
+    name, eff = pick_schedule(NativeConfig.gpt2("small"), 8, 64, 16, 1024, details=det)
+    assert set(det) == set(eff) and name in det
+    for c, d in det.items():
+        assert {"head_lag", "stash_slots_max", "planned_gb_max", "efficiency", "v"} <= set(d), d
+        assert d["planned_gb_max"] <= 0.85 * 288 * 2 ** 30 / 1e9, (c, d)
+    cfg = NativeConfig.llama3("8b")
+    bound = {"hbm": 64 * 2 ** 30, "lanes": 2}
+    det8 = {}
+    pick_schedule(cfg, 8, 16, 1, 8192, candidates=("1F1B", "ZBH1"), mem_bound=bound, details=det8)
+    free = {}
+    pick_schedule(cfg, 8, 16, 1, 8192, candidates=("1F1B", "ZBH1"), details=free)
+    for c in ("1F1B", "ZBH1"):
+        d, f = det8[c], free[c]
+        assert d["head_lag"] <= f["head_lag"], (c, d, f)
+        fits = d["planned_gb_max"] <= 0.85 * 64 * 2 ** 30 / 1e9
+        # either the plan fits the small device, or it could not shrink below the schedule's
+        # own warmup depth (lag 0)
+        assert fits or d["head_lag"] == 0, (c, d)
+    assert det8["ZBH1"]["head_lag"] == 0 or det8["ZBH1"]["stash_slots_max"] <= 8 + 2, det8

@@ -286,3 +286,26 @@ def test_hbm_plan_matches_the_reserved_peak(schedule, mbs, m):
     torch.cuda.empty_cache()
     assert slots == (m if schedule == "GPipe" else 2), slots
     assert 0.9 * reserved <= plan <= 1.1 * reserved, (schedule, mbs, m, plan / 1e9, reserved / 1e9)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_selective_recompute_trains_like_no_recompute(graphs):
+    """recomputing the first k layers of a stage (selective) or all of them
+    trains like keeping every stash -- same kernels, the recomputed activations are the same
+    values -- eager and replayed from HIP graphs."""
+    cfg = NativeConfig.gpt2("small", n_layers=4, vocab_size=4096)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    x = torch.randint(0, cfg.vocab_size, (4, 256), device=dev, generator=g)
+    y = torch.randint(0, cfg.vocab_size, (4, 256), device=dev, generator=g)
+    losses = {}
+    for rc, want in ((False, 0), (2, 2), (True, 4)):
+        tr = PipelineTrainer(cfg, pp=1, schedule="1F1B", n_microbatches=2, mbs=2, seq_len=256, device=dev, seed=1,
+                             graphs=graphs, recompute=rc, lr=1e-3)
+        assert tr.recompute_layers == want and tr.stages[0].model.recompute_layers == want
+        if graphs:
+            tr.capture_graphs(x, y)
+        losses[want] = [float(tr.train_step(x, y)) for _ in range(3)]
+        del tr
+    assert losses[2] == pytest.approx(losses[0], rel=1e-3), losses
+    assert losses[4] == pytest.approx(losses[0], rel=1e-3), losses
