@@ -44,6 +44,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -211,7 +212,20 @@ class RcclEngine {
     for (auto& c : comm_)
       if (c != nullptr) g_rccl->CommAbort(c);
     std::fill(comm_.begin(), comm_.end(), nullptr);
-    pending_.clear();  // events leaked on purpose: their streams may still be unwinding
+    // events kept (not destroyed) on purpose: their streams may still be unwinding; parked
+    // where they stay reachable so the engine itself owns nothing afterwards
+    std::vector<hipEvent_t>& park = abandoned_events();
+    for (auto& kv : pending_) park.push_back(kv.second);
+    pending_.clear();
+    for (hipEvent_t e : pool_) park.push_back(e);
+    pool_.clear();
+    {
+      std::lock_guard<std::mutex> lk(trace_mu_);
+      for (auto& e : trace_)
+        if (e.ev != nullptr) park.push_back(e.ev);
+      trace_.clear();
+      trace_head_ = 0;
+    }
     open_ = false;
   }
 
@@ -287,6 +301,10 @@ class RcclEngine {
   int64_t post_raw(int channel, const std::vector<RawOp>& sends, const std::vector<RawOp>& recvs,
                    hipStream_t compute, hipEvent_t after = nullptr) {
     check_channel(channel);
+    // peers checked before anything is issued: a throw inside the group would leave this
+    // thread's RCCL group open and fold the next post into it (csrc/tests/host_asan_test.cpp)
+    for (const auto& o : sends) TORCH_CHECK(o.peer >= 0 && o.peer < nranks_, "RcclEngine: bad send peer ", o.peer);
+    for (const auto& o : recvs) TORCH_CHECK(o.peer >= 0 && o.peer < nranks_, "RcclEngine: bad recv peer ", o.peer);
     hipStream_t cs = stream_[channel];
     ncclComm_t comm = comm_[channel];
     if (after != nullptr && sends.empty()) {
@@ -295,14 +313,8 @@ class RcclEngine {
       order_after(compute, cs);
     }
     MP_NCCL(g_rccl->GroupStart());
-    for (const auto& o : sends) {
-      TORCH_CHECK(o.peer >= 0 && o.peer < nranks_, "RcclEngine: bad send peer ", o.peer);
-      MP_NCCL(g_rccl->Send(o.ptr, o.count, o.type, o.peer, comm, cs));
-    }
-    for (const auto& o : recvs) {
-      TORCH_CHECK(o.peer >= 0 && o.peer < nranks_, "RcclEngine: bad recv peer ", o.peer);
-      MP_NCCL(g_rccl->Recv(o.ptr, o.count, o.type, o.peer, comm, cs));
-    }
+    for (const auto& o : sends) MP_NCCL(g_rccl->Send(o.ptr, o.count, o.type, o.peer, comm, cs));
+    for (const auto& o : recvs) MP_NCCL(g_rccl->Recv(o.ptr, o.count, o.type, o.peer, comm, cs));
     MP_NCCL(g_rccl->GroupEnd());
     const int64_t h = finish(cs);
     trace(channel, -1, cs, sends, recvs);
@@ -462,6 +474,11 @@ class RcclEngine {
     pool_.clear();
   }
 
+  static std::vector<hipEvent_t>& abandoned_events() {
+    static std::vector<hipEvent_t> v;
+    return v;
+  }
+
   static constexpr size_t kTrace = 256;
   static constexpr int kPeers = 8;
   struct TraceEntry {
@@ -525,7 +542,7 @@ class RcclEngine {
   std::vector<hipStream_t> stream_;
   std::vector<int> slot_;
   std::vector<c10::hip::HIPStream> hstream_;
-  bool open_ = true;
+  std::atomic<bool> open_{true};   // read by the watchdog thread (progress / async_error)
   int nranks_, rank_, device_;
   int64_t next_ = 1;
   std::unordered_map<int64_t, hipEvent_t> pending_;

@@ -67,6 +67,14 @@ class StageRunner {
   enum Kind { GRAPH = 0, COPY = 1, POST = 2, WAIT = 3, CALL = 4, SYNC = 5, COLL = 6 };
 
   explicit StageRunner(int device) : device_(device) {}
+  StageRunner(const StageRunner&) = delete;
+  StageRunner& operator=(const StageRunner&) = delete;
+  // the SYNC / step / timing events (a still-pending event is released by HIP once it fired)
+  ~StageRunner() {
+    for (hipEvent_t e : sync_ev_) hipEventDestroy(e);
+    for (hipEvent_t e : ev_) hipEventDestroy(e);
+    if (step_ev_ != nullptr) hipEventDestroy(step_ev_);
+  }
 
   void add_graph(int64_t graph_exec, const std::string& label, int64_t stream) {
     TORCH_CHECK(graph_exec != 0, "stage runner: null graph exec");

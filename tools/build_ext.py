@@ -1,6 +1,8 @@
 """Build the mipipe HIP extension for gfx950 in-tree (no hipify, no JIT cache).
 
     python tools/build_ext.py [--force] [-j N]
+    python tools/build_ext.py --asan-host     # host runtime under ASan/UBSan, built and run
+
 
 Each ``csrc/kernels/*.hip`` is compiled by ``hipcc --offload-arch=gfx950`` into an
 object (plain HIP, no torch headers: seconds per file); ``csrc/bindings.cpp`` is the only
@@ -94,6 +96,32 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, variant: st
     return OUT
 
 
+def asan_host(run: bool = True) -> int:
+    """The native runtime (csrc/runtime/stage_runner.cpp + csrc/comm/rccl_engine.h) built with
+    g++ for the host under AddressSanitizer + UndefinedBehaviorSanitizer against the stand-in
+    HIP / RCCL / torch headers of csrc/tests/host_stubs, and csrc/tests/host_asan_test.cpp run:
+    two ranks replay tapes through an in-process fabric.  GPU sanitizers are not available on
+    the MI355X pool, so this is where heap misuse, leaks and UB in the runtime are caught.
+    Returns the test's exit status (0: clean)."""
+    src = os.path.join(CSRC, "tests", "host_asan_test.cpp")
+    exe = os.path.join(ROOT, "build", "host_asan_test")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    deps = [src] + glob.glob(os.path.join(CSRC, "tests", "host_stubs", "**", "*.h"), recursive=True) + [
+        os.path.join(CSRC, "runtime", "stage_runner.cpp")] + glob.glob(os.path.join(CSRC, "comm", "*.h"))
+    if _newer(deps, exe):
+        _run([os.environ.get("CXX", "g++"), "-std=c++17", "-g", "-O1", "-fsanitize=address,undefined",
+              "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer", "-Wall", "-Wno-unused-variable",
+              "-I", os.path.join(CSRC, "tests", "host_stubs"), src, "-o", exe, "-lpthread", "-ldl"])
+    if not run:
+        return 0
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+               UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+    r = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=600)
+    sys.stdout.write(r.stdout)
+    sys.stderr.write(r.stderr)
+    return r.returncode
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
@@ -101,7 +129,11 @@ if __name__ == "__main__":
     ap.add_argument("-v", action="store_true")
     ap.add_argument("--variant", default="", help="A/B build name: writes _C_<variant>.so")
     ap.add_argument("-D", dest="defines", action="append", default=[], help="extra define for a --variant build")
+    ap.add_argument("--asan-host", action="store_true",
+                    help="build + run the host runtime test under ASan/UBSan (no GPU, no hipcc)")
     a = ap.parse_args()
+    if a.asan_host:
+        sys.exit(asan_host())
     if a.defines and not a.variant:
         ap.error("-D needs --variant (the default _C.so is always the plain build)")
     print(build(a.force, a.j, a.v, a.variant, a.defines))
