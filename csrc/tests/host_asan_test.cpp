@@ -394,6 +394,38 @@ static void abort_in_flight() {
   fabric::mail.clear();
 }
 
+// with receive-early a receive-only POST does not wait for the compute the
+// tape issued before it.  Rank 1's tape is [GRAPH (held running)] [POST recv] [WAIT]; rank 0
+// sends.  The receive lands while the graph is still running only with receive-early on.
+static void recv_early_semantics(bool early) {
+  const int N = 512;
+  const pybind11::bytes uid = ids(1);
+  auto e0 = std::make_shared<RcclEngine>(uid, 2, 0, 0, std::vector<int64_t>{0});
+  auto e1 = std::make_shared<RcclEngine>(uid, 2, 1, 1, std::vector<int64_t>{0});
+  std::vector<float> act0(N, 7.f), act1(N, 0.f);
+  bool running = true;
+  hipGraphExec_t long_graph = reinterpret_cast<hipGraphExec_t>(0xbeef);
+  fake_hip::graph_body = [&](hipGraphExec_t g) { return g != long_graph || !running; };
+  {
+    StageRunner r0(0), r1(1);
+    r0.add_post(pybind11::object::of(e0), 0, {{h(act0.data()), N, 6, 1}}, {});
+    r1.add_graph(h(long_graph), "F0", 0);
+    const int64_t s = r1.add_post(pybind11::object::of(e1), 0, {}, {{h(act1.data()), N, 6, 0}});
+    r1.add_wait(s, 0);
+    r1.set_recv_early(early);
+    r0.run();
+    r1.run();
+    EXPECT(!fake_hip::drain());          // rank 1's compute stream is held by the graph
+    EXPECT((act1[3] == 7.f) == early);   // ... yet the receive landed iff receive-early
+    running = false;
+    EXPECT(fake_hip::drain());
+    EXPECT(act1[3] == 7.f);
+  }
+  fake_hip::graph_body = [](hipGraphExec_t) { return true; };
+  e0->close();
+  e1->close();
+}
+
 int main() {
   install_fake_rccl();
   pipeline(false, false, 40);
@@ -401,6 +433,8 @@ int main() {
   collectives();
   runner_errors();
   abort_in_flight();
+  recv_early_semantics(false);
+  recv_early_semantics(true);
   for (int i = 0; i < 3; ++i) pipeline(i % 2 == 0, i == 1, 10);
   EXPECT(fabric::colls.empty());
   // leak check now, while the process-wide statics (comm streams, parked events) still hold

@@ -115,9 +115,14 @@ inline hipError_t hipStreamSynchronize(hipStream_t) {
   fake_hip::drain();
   return hipSuccess;
 }
-inline hipError_t hipGraphLaunch(hipGraphExec_t, hipStream_t s) {
+namespace fake_hip {
+// the body of a replayed graph: returns false while it is still "running" (a test holds a
+// long kernel on a stream this way); default: completes at once
+inline std::function<bool(hipGraphExec_t)> graph_body = [](hipGraphExec_t) { return true; };
+}  // namespace fake_hip
+inline hipError_t hipGraphLaunch(hipGraphExec_t g, hipStream_t s) {
   ++fake_hip::graph_launches;
-  s->work.push_back([] { return true; });
+  s->work.push_back([g] { return fake_hip::graph_body(g); });
   return hipSuccess;
 }
 inline hipError_t hipMemcpyAsync(void* d, const void* src, size_t n, hipMemcpyKind, hipStream_t s) {
