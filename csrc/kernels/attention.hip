@@ -569,6 +569,258 @@ __device__ __forceinline__ void attn_wait_vmcnt() {
 }
 
 // ==========================================================================================
+// forward v2: paired query blocks, LDS-DMA K/V ring, lazy rescale (the default at d_h 64)
+// ==========================================================================================
+// Same tile structure as attn_fwd_kernel (4 waves x 32 queries, 64-key tiles, swapped
+// S^T = K Q^T with P^T kept in registers), with the per-tile VALU cut and the grid reshaped
+// (the forward issued ~18 VALU per MFMA at 0.26 MFMA busy, profiles/r5_attention_pmc.md):
+//   * K/V tiles stream through a 3-deep LDS ring by buffer-load-to-LDS DMA (GTile's piece
+//     layout; 32-bit per-lane offsets fixed at entry + a scalar per-tile offset; rows past
+//     the key end read as zero): two tiles in flight, counted vmcnt, one raw barrier per tile.  v1 staged one
+//     tile ahead through registers, so every tile waited out a full load latency (v1 -> v2
+//     with register staging kept: 2-4 %; the dQ kernel, on the ring, ran 1.5x v1's MFMA
+//     work per tile in less time).
+//   * causal / key-end mask: one compare against a per-lane limit and one select per score
+//     (the key's in-tile position is a compile-time constant per accumulator register).
+//   * cross-half max / sum by v_permlane32_swap instead of an LDS bpermute.
+//   * lazy rescale: the subtracted row maximum moves only when a lane's tile maximum exceeds
+//     it by more than 2^8 (wave-uniform branch); otherwise O and l are not rescaled (P stays
+//     <= 2^8, exact in f32 sums and bf16 products).
+//   * causal: one workgroup runs query block nmb-1-p and then block p of the same (b, h), so
+//     every workgroup does the same number of tiles (no heavy-first tail); the pairs of one
+//     (b, h) sit on one XCD (workgroup id mod 8) next to each other, so their K/V tiles are
+//     read while the others still hold them in that XCD's L2.
+__device__ __forceinline__ float xhalf_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return max3_raw(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xhalf_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+// GTile's 1 KiB-piece layout issued as buffer_load ... lds: the per-lane byte offset of each
+// piece is fixed at kernel entry (32-bit), the tile's row offset is a scalar, and rows past
+// the buffer's range (keys >= Sk) land as zeros -- no 64-bit address math per tile
+template <int DP>
+struct BTile {
+  static constexpr int CPR = DP / 8, PR = 1024 / (DP * 2), PPW = (64 / PR) / 4;
+  int voff[PPW];
+  __device__ __forceinline__ void init(int64_t stride, int D, int wave) {
+    const int lane = threadIdx.x & 63, lr = lane / CPR, phys = lane % CPR;
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int row = (wave + 4 * i) * PR + lr;
+      const int chunk = (phys & ~15) | ((phys & 15) ^ chunk_swz<DP>(row));
+      const int col = chunk * 8 < D ? chunk * 8 : 0;
+      voff[i] = (int)(((int64_t)row * stride + col) * 2);
+    }
+  }
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, int soff, char* img, int wave) const {
+    // (the builtin exists for the gfx950 pass only; the host pass would drop the kernel's stubs)
+#if defined(__HIP_DEVICE_COMPILE__)
+#pragma unroll
+    for (int i = 0; i < PPW; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)(img + (wave + 4 * i) * 1024),
+                                               16, voff[i], soff, 0, 0);
+#endif
+  }
+};
+
+// in-tile key offset of accumulator register r (lane half hl adds 4)
+__device__ __forceinline__ constexpr int key_of(int r) { return (r & 3) + 8 * (r >> 2); }
+
+template <int DP, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(256, DROP ? 2 : 3) attn_fwd2_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V, bf16_t* __restrict__ O,
+    float* __restrict__ LSE, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
+    int64_t os, float scale, float p_drop, uint64_t seed) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;
+  constexpr float TAU = 8.f;   // lazy-rescale threshold (log2 units)
+  const int nmb = (Sq + 127) / 128;
+  const int npair = CAUSAL ? (nmb + 1) / 2 : nmb;   // workgroups per (b, h)
+  const int nbh = B * H;
+  // workgroup -> (bh, p): the npair workgroups of one bh are consecutive on one XCD
+  const int lin = (int)blockIdx.x;
+  int bh, p;
+  if ((nbh & 7) == 0) {
+    const int xcd = lin & 7, j = lin >> 3;
+    bh = (j / npair) * 8 + xcd;
+    p = j % npair;
+  } else {
+    bh = lin / npair;
+    p = lin % npair;
+  }
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const bf16_t* Qb = Q + (int64_t)b * Sq * qs + (int64_t)h * D;
+  // range: through the last valid row's head slice (the launcher keeps it below 2^31)
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(K + (int64_t)b * Sk * ks + (int64_t)hk * D), 0, (int)(((int64_t)(Sk - 1) * ks + D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(V + (int64_t)b * Sk * vs + (int64_t)hk * D), 0, (int)(((int64_t)(Sk - 1) * vs + D) * 2), 0x00020000);
+  // K / V ring: NBUF buffers of (K tile, V tile), LOOK tiles in flight
+  constexpr int NBUF = 3, LOOK = NBUF - 1, BUFB = 2 * TILE;
+  constexpr int PER_TILE = 2 * BTile<DP>::PPW;   // DMA instructions per tile per wave
+  BTile<DP> kt, vt;
+  kt.init(ks, D, w);
+  vt.init(vs, D, w);
+  const int kstep = (int)(64 * ks * 2), vstep = (int)(64 * vs * 2);
+  auto issue = [&](int t) {
+    char* buf = smem + (t % NBUF) * BUFB;
+    kt.issue(krs, t * kstep, buf, w);
+    vt.issue(vrs, t * vstep, buf + TILE, w);
+  };
+  const float c = scale * LOG2E;
+  const DropKey dkey = drop_key(seed, (uint32_t)bh);
+  const uint32_t dthr = drop_thr(p_drop);
+  const float dinv = 1.0f / (1.0f - p_drop);
+  const int shift = Sk - Sq;
+  const int npass = CAUSAL && (nmb - 1 - p) != p ? 2 : 1;
+
+  for (int pass = 0; pass < npass; ++pass) {
+    const int mb = CAUSAL ? (pass == 0 ? nmb - 1 - p : p) : p;
+    const int m0 = mb * 128;
+    const int qrow = m0 + 32 * w + l32;
+    const bool qvalid = qrow < Sq;
+    bf16x8 qf[DP / 16];
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s)
+      qf[s] = __builtin_bit_cast(bf16x8, gload8(Qb + (int64_t)qrow * qs, 16 * s + 8 * hl, D, qvalid));
+    const uint32_t qoff = (uint32_t)qrow * (uint32_t)Sk;
+    f32x16 o[DP / 32];
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) o[d] = {};
+    float m_run = -INFINITY;   // running maximum (log2 units) ...
+    float m_sub = 0.f;         // ... and the finite value the probabilities subtract
+    float l_run = 0.f;
+    int n_end = Sk;
+    if (CAUSAL) n_end = min(Sk, m0 + 128 + shift);
+    const int ntiles = n_end > 0 ? (n_end + 63) / 64 : 0;
+    const int wave_last_q = m0 + 32 * w + 31 + shift;
+    // per-lane mask limit: a key of in-tile offset k (+4 hl) is kept iff k <= lim - n0
+    const int lim0 = (CAUSAL ? min(qrow + shift, Sk - 1) : Sk - 1) - 4 * hl;
+
+    if (pass > 0) {   // every wave has read the previous pass's last tiles
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int i = 0; i < LOOK; ++i)
+      if (i < ntiles) issue(i);
+    for (int t = 0; t < ntiles; ++t) {
+      const int n0 = t * 64;
+      // tile t landed (the younger one may stay in flight), then publish it to all waves
+      if (t + 1 < ntiles) attn_wait_vmcnt<PER_TILE>();
+      else attn_wait_vmcnt<0>();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      // every wave is done with tile t-1: its buffer takes tile t+LOOK
+      if (t + LOOK < ntiles) issue(t + LOOK);
+      const bool skip = CAUSAL && n0 > wave_last_q;
+      if (!skip) {
+        const char* kb = smem + (t % NBUF) * BUFB;
+        const char* vb = kb + TILE;
+        f32x16 s0 = {}, s1 = {};
+#pragma unroll
+        for (int s = 0; s < DP / 16; ++s) {
+          bf16x8 a0 = lds_row8<DP>(kb, l32, 2 * s + hl);
+          bf16x8 a1 = lds_row8<DP>(kb, 32 + l32, 2 * s + hl);
+          s0 = mfma32(a0, qf[s], s0);
+          s1 = mfma32(a1, qf[s], s1);
+        }
+        const bool edge = (n0 + 64 > Sk) || (CAUSAL && n0 + 63 > m0 + 32 * w + shift);
+        if (edge) {
+          const int lim = lim0 - n0;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            s0[r] = key_of(r) > lim ? -INFINITY : s0[r];
+            s1[r] = key_of(r) + 32 > lim ? -INFINITY : s1[r];
+          }
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = max3_raw(mx, s0[r], s1[r]);
+        mx = xhalf_max(mx);
+        const float mxc = mx * c;
+        // lazy rescale: wave-uniform, taken on the first tile and when a maximum jumps
+        if (__builtin_amdgcn_ballot_w64(mxc > m_run + TAU)) {
+          const float m_new = fmaxf(m_run, mxc);
+          const float s_new = m_new == -INFINITY ? 0.f : m_new;
+          const float alpha = m_run == -INFINITY ? 0.f : __builtin_amdgcn_exp2f(m_sub - s_new);
+#pragma unroll
+          for (int d = 0; d < DP / 32; ++d) o[d] *= alpha;
+          l_run *= alpha;
+          m_run = m_new;
+          m_sub = s_new;
+        }
+        uint32_t keep = 0xffffffffu;
+        if (DROP) {
+          keep = 0;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t kr = (uint32_t)(n0 + key_of(r) + 4 * hl);
+            keep |= (hash_lo(dkey, qoff + kr) >= dthr ? 1u : 0u) << r;
+            keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
+          }
+        }
+        float rs = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], c, -m_sub));
+          float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c, -m_sub));
+          rs += p0 + p1;
+          if (DROP) {
+            p0 = (keep >> r) & 1u ? p0 * dinv : 0.f;
+            p1 = (keep >> (16 + r)) & 1u ? p1 * dinv : 0.f;
+          }
+          s0[r] = p0;
+          s1[r] = p1;
+        }
+        l_run += xhalf_sum(rs);
+        const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
+#pragma unroll
+        for (int d = 0; d < DP / 32; ++d) {
+          const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
+          bf16x8 a;
+          a = cat44(lds_tr4<DP>(vb, 0 + 4 * hl, c0), lds_tr4<DP>(vb, 8 + 4 * hl, c0));
+          o[d] = mfma32(a, p00, o[d]);
+          a = cat44(lds_tr4<DP>(vb, 16 + 4 * hl, c0), lds_tr4<DP>(vb, 24 + 4 * hl, c0));
+          o[d] = mfma32(a, p01, o[d]);
+          a = cat44(lds_tr4<DP>(vb, 32 + 4 * hl, c0), lds_tr4<DP>(vb, 40 + 4 * hl, c0));
+          o[d] = mfma32(a, p10, o[d]);
+          a = cat44(lds_tr4<DP>(vb, 48 + 4 * hl, c0), lds_tr4<DP>(vb, 56 + 4 * hl, c0));
+          o[d] = mfma32(a, p11, o[d]);
+        }
+      }
+    }
+    if (qvalid) {
+      const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+      bf16_t* orow = O + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int col = 32 * d + 8 * g + 4 * hl;
+          if (col < D) {
+            u16x4 pk;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pk[e] = f2bf(o[d][4 * g + e] * inv);
+            *reinterpret_cast<u16x4*>(orow + col) = pk;
+          }
+        }
+      }
+      if (hl == 0) LSE[(int64_t)bh * Sq + qrow] = l_run > 0.f ? m_sub + log2f(l_run) : INFINITY;
+    }
+  }
+}
+
+// ==========================================================================================
 // backward dK / dV: workgroup = 128 keys (4 waves x 32) of one (b, kv head)
 // ==========================================================================================
 // Q / dO tiles and the per-row LSE / delta stream through an NBUF-deep LDS ring by
@@ -1365,6 +1617,19 @@ static int launch_fwd(const void* q, const void* k, const void* v, void* o, floa
     }
   }
   const size_t lds = 4 * 64 * DP * 2;
+  // v2 (default at d_h 64); MIPIPE_ATTN_FWD=1 selects v1 (A/B)
+  static const bool v1 = [] { const char* e = getenv("MIPIPE_ATTN_FWD"); return e && e[0] == '1'; }();
+  if constexpr (DP == 64) {
+  if (!v1 && (int64_t)(Sk + 128) * ks * 2 < (1ll << 31) && (int64_t)(Sk + 128) * vs * 2 < (1ll << 31)) {
+    // (d_h 128 / 256 spill at 3 waves per SIMD)
+    const int nmb = (Sq + 127) / 128;
+    const int npair = CAUSAL ? (nmb + 1) / 2 : nmb;
+    hipLaunchKernelGGL((attn_fwd2_kernel<DP, CAUSAL, DROP>), dim3(npair * B * H), dim3(256), 3 * 2 * 64 * 64 * 2, st,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, (bf16_t*)o, lse, B, Sq, Sk, H, Hkv, D, qs,
+                       ks, vs, os, scale, p, seed);
+    return (int)hipGetLastError();
+  }
+  }
   auto kern = attn_fwd_kernel<DP, CAUSAL, DROP>;
   if (lds > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   dim3 grid((Sq + 127) / 128, B * H);

@@ -215,7 +215,10 @@ ATTN = [  # B, S, H, Hkv, D, causal
     (2, 128, 8, 8, 96, False), (1, 256, 4, 2, 128, True), (1, 128, 4, 4, 192, False), (1, 1024, 2, 2, 64, True),
     (1, 200, 4, 2, 128, True), (2, 136, 4, 4, 64, False),
     # short non-causal (one-launch backward): partial second tile, one tile only, GQA (two-kernel path)
-    (3, 100, 4, 4, 64, False), (2, 64, 4, 4, 128, False), (2, 128, 4, 2, 96, False)]
+    (3, 100, 4, 4, 64, False), (2, 64, 4, 4, 128, False), (2, 128, 4, 2, 96, False),
+    # forward v2 (d_h 64): paired causal blocks with the XCD grouping (B*H % 8 == 0), an odd
+    # block count without it, a ragged last block, and a non-causal grid of >= 256 blocks
+    (2, 1280, 4, 4, 64, True), (3, 640, 4, 2, 64, True), (1, 1000, 6, 3, 64, True), (8, 512, 8, 8, 64, False)]
 
 
 @pytest.mark.parametrize("B,S,H,Hkv,D,causal", ATTN)
@@ -243,6 +246,29 @@ def test_attention_fwd_bwd(B, S, H, Hkv, D, causal):
     # the kernels' column sums agree with the sums of the gradients they wrote
     close(res[DEV][3], res[DEV][2].float().sum(0).cpu() + 0.25, atol=0.05 * T ** 0.5, rtol=2e-2)
     close(res[DEV][3], res["cpu"][3], atol=0.1 * T ** 0.5, rtol=5e-2)
+
+
+@pytest.mark.parametrize("Sq,Sk", [(384, 512), (512, 384), (200, 328)])
+def test_attention_cross_lengths_causal_d64(Sq, Sk):
+    """Causal attention with Sq != Sk (query i sees keys <= i + Sk - Sq): with Sk < Sq the
+    first queries see no key at all (zero output, LSE +inf) -- the forward v2 lazy rescale
+    must keep those rows finite-free of NaN while later rows start from a fully masked
+    running maximum."""
+    torch.manual_seed(0)
+    B, H, D = 2, 4, 64
+    q, do = rnd(B * Sq, H * D), rnd(B * Sq, H * D)
+    k, v = rnd(B * Sk, H * D), rnd(B * Sk, H * D)
+    res = {}
+    for dev in ("cpu", DEV):
+        o = torch.empty(B * Sq, H * D, dtype=torch.bfloat16, device=dev)
+        lse = torch.empty(B * H * Sq, device=dev)
+        ops.attn_fwd(q.to(dev), k.to(dev), v.to(dev), o, lse, B, Sq, Sk, H, H, D, True)
+        res[dev] = (o.float().cpu().nan_to_num(0.0), lse.cpu())   # (the f32 softmax of no key is NaN)
+    assert torch.isfinite(res[DEV][0]).all()
+    close(res[DEV][0], res["cpu"][0], atol=2e-2, rtol=2e-2)
+    fin = torch.isfinite(res["cpu"][1])
+    assert torch.equal(fin, torch.isfinite(res[DEV][1]))
+    close(res[DEV][1][fin], res["cpu"][1][fin], atol=2e-2, rtol=1e-3)
 
 
 def test_attention_dropout_consistency():

@@ -193,6 +193,11 @@ def test_gemm_planner_split_tail_is_opt_in(monkeypatch):
         pytest.skip("extension not built")
     # default: off (a measured null, gemm2.hip); force_cfg 14 plans it where it applies
     assert e.gemm2_plan(8192, 768, 768, False, False, False, -1)[0] != 14
+    if not e.gemm2_has_probe_engines():
+        # the default _C.so does not carry the probe engines (tools/build_ext.py --variant
+        # probes -D MP_PROBE_ENGINES): the planner refuses to plan one it cannot launch
+        assert e.gemm2_plan(8192, 768, 768, False, False, False, 14)[0] == -1
+        return
     assert e.gemm2_plan(8192, 768, 768, False, False, False, 14)[0] == 14
     plan = lambda M, N, Kd, ta=False, tb=False, acc=False: e.gemm2_plan(M, N, Kd, ta, tb, acc, 14)[0]  # noqa: E731
     for M, N, Kd in ((8192, 768, 768), (8192, 768, 3072), (32768, 768, 3072), (32768, 768, 2304)):

@@ -93,6 +93,13 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, variant: st
             "-L", tlib, "-lc10", "-ltorch", "-ltorch_cpu", "-ltorch_python", "-lc10_hip", "-ltorch_hip",
             "-ldl", f"-Wl,-rpath,{tlib}"]
         _run(link)
+        # every symbol resolves (a kernel template whose host stub the compiler dropped links
+        # fine and only fails at import -- or, worse, on the GPU box)
+        import ctypes
+        try:
+            ctypes.CDLL(OUT, mode=os.RTLD_NOW | os.RTLD_LOCAL)
+        except OSError as e:
+            raise RuntimeError(f"{OUT} does not load: {e}") from None
     return OUT
 
 
