@@ -664,11 +664,29 @@ __global__ void __launch_bounds__(256, DROP ? 2 : 3) attn_fwd2_kernel(
       (void*)(V + (int64_t)b * Sk * vs + (int64_t)hk * D), 0, (int)(((int64_t)(Sk - 1) * vs + D) * 2), 0x00020000);
   // K / V ring: NBUF buffers of (K tile, V tile), LOOK tiles in flight
   constexpr int NBUF = 3, LOOK = NBUF - 1, BUFB = 2 * TILE;
+  static_assert(NBUF == 3, "the tile loop below is unrolled by NBUF = 3");
   constexpr int PER_TILE = 2 * BTile<DP>::PPW;   // DMA instructions per tile per wave
   BTile<DP> kt, vt;
   kt.init(ks, D, w);
   vt.init(vs, D, w);
   const int kstep = (int)(64 * ks * 2), vstep = (int)(64 * vs * 2);
+  // per-lane LDS byte offsets of the fragment reads inside a tile (swizzle included; the rows
+  // a lane reads 32 / 16 apart share the swizzle, so the rest are immediate offsets):
+  //   K rows l32 (+32: +4096) at chunk 2s + hl;  V^T transposed reads of rows 8j + 4hl + q
+  //   at column 32d + 16 (lane>>4 & 1) + 4p: j = jp + 2m is voff[d][jp] + 2048 m
+  int koff[DP / 16], vtoff[DP / 32][2];
+  {
+    const int i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) koff[s] = lds_off<DP>(l32, 2 * s + hl);
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int row = 8 * jp + 4 * hl + q, col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * pp;
+        vtoff[d][jp] = lds_off<DP>(row, col >> 3) + ((col & 7) << 1);
+      }
+  }
   auto issue = [&](int t) {
     char* buf = smem + (t % NBUF) * BUFB;
     kt.issue(krs, t * kstep, buf, w);
@@ -712,7 +730,10 @@ __global__ void __launch_bounds__(256, DROP ? 2 : 3) attn_fwd2_kernel(
 #pragma unroll
     for (int i = 0; i < LOOK; ++i)
       if (i < ntiles) issue(i);
-    for (int t = 0; t < ntiles; ++t) {
+    // one tile on ring buffer BUF (a compile-time constant: every LDS address of the tile is
+    // an immediate offset, and the refill target (BUF + LOOK) % NBUF too)
+    auto tile = [&](auto bufc, int t) {
+      constexpr int BUF = decltype(bufc)::value;
       const int n0 = t * 64;
       // tile t landed (the younger one may stay in flight), then publish it to all waves
       if (t + 1 < ntiles) attn_wait_vmcnt<PER_TILE>();
@@ -721,16 +742,20 @@ __global__ void __launch_bounds__(256, DROP ? 2 : 3) attn_fwd2_kernel(
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       // every wave is done with tile t-1: its buffer takes tile t+LOOK
-      if (t + LOOK < ntiles) issue(t + LOOK);
+      if (t + LOOK < ntiles) {
+        char* buf = smem + ((BUF + LOOK) % NBUF) * BUFB;
+        kt.issue(krs, (t + LOOK) * kstep, buf, w);
+        vt.issue(vrs, (t + LOOK) * vstep, buf + TILE, w);
+      }
       const bool skip = CAUSAL && n0 > wave_last_q;
       if (!skip) {
-        const char* kb = smem + (t % NBUF) * BUFB;
+        const char* kb = smem + BUF * BUFB;
         const char* vb = kb + TILE;
         f32x16 s0 = {}, s1 = {};
 #pragma unroll
         for (int s = 0; s < DP / 16; ++s) {
-          bf16x8 a0 = lds_row8<DP>(kb, l32, 2 * s + hl);
-          bf16x8 a1 = lds_row8<DP>(kb, 32 + l32, 2 * s + hl);
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(kb + koff[s]);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(kb + koff[s] + 32 * DP * 2);
           s0 = mfma32(a0, qf[s], s0);
           s1 = mfma32(a1, qf[s], s1);
         }
@@ -769,12 +794,14 @@ __global__ void __launch_bounds__(256, DROP ? 2 : 3) attn_fwd2_kernel(
             keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
           }
         }
-        float rs = 0.f;
+        float rs0 = 0.f, rs1 = 0.f;   // two independent add chains (plain v_add_f32: the file is
+                                      // built without SLP packing, see tools/build_ext.py)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], c, -m_sub));
           float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c, -m_sub));
-          rs += p0 + p1;
+          rs0 += p0;
+          rs1 += p1;
           if (DROP) {
             p0 = (keep >> r) & 1u ? p0 * dinv : 0.f;
             p1 = (keep >> (16 + r)) & 1u ? p1 * dinv : 0.f;
@@ -782,22 +809,25 @@ __global__ void __launch_bounds__(256, DROP ? 2 : 3) attn_fwd2_kernel(
           s0[r] = p0;
           s1[r] = p1;
         }
-        l_run += xhalf_sum(rs);
+        l_run += xhalf_sum(rs0 + rs1);
         const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
 #pragma unroll
         for (int d = 0; d < DP / 32; ++d) {
-          const int c0 = 32 * d + 16 * ((lane >> 4) & 1);
-          bf16x8 a;
-          a = cat44(lds_tr4<DP>(vb, 0 + 4 * hl, c0), lds_tr4<DP>(vb, 8 + 4 * hl, c0));
-          o[d] = mfma32(a, p00, o[d]);
-          a = cat44(lds_tr4<DP>(vb, 16 + 4 * hl, c0), lds_tr4<DP>(vb, 24 + 4 * hl, c0));
-          o[d] = mfma32(a, p01, o[d]);
-          a = cat44(lds_tr4<DP>(vb, 32 + 4 * hl, c0), lds_tr4<DP>(vb, 40 + 4 * hl, c0));
-          o[d] = mfma32(a, p10, o[d]);
-          a = cat44(lds_tr4<DP>(vb, 48 + 4 * hl, c0), lds_tr4<DP>(vb, 56 + 4 * hl, c0));
-          o[d] = mfma32(a, p11, o[d]);
+          auto tr = [&](int jp, int m) {
+            return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(vb + vtoff[d][jp] + 16 * DP * 2 * m));
+          };
+          o[d] = mfma32(cat44(tr(0, 0), tr(1, 0)), p00, o[d]);
+          o[d] = mfma32(cat44(tr(0, 1), tr(1, 1)), p01, o[d]);
+          o[d] = mfma32(cat44(tr(0, 2), tr(1, 2)), p10, o[d]);
+          o[d] = mfma32(cat44(tr(0, 3), tr(1, 3)), p11, o[d]);
         }
       }
+    };
+    for (int t0 = 0; t0 < ntiles; t0 += NBUF) {
+      tile(std::integral_constant<int, 0>{}, t0);
+      if (t0 + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t0 + 1);
+      if (t0 + 2 < ntiles) tile(std::integral_constant<int, 2>{}, t0 + 2);
     }
     if (qvalid) {
       const float inv = l_run > 0.f ? 1.f / l_run : 0.f;

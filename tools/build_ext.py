@@ -30,6 +30,12 @@ ARCH = os.environ.get("MIPIPE_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 
+# per-file compile flags.  attention.hip: no SLP packing -- -O3 pairs the softmax's independent
+# f32 adds / multiplies into v_pk_*_f32, which beside MFMAs cost more issue cycles than the
+# scalar ops they replace (MI355X_MICROARCH.md, 'price of one filler beside MFMAs')
+FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+
+
 def _torch_paths():
     import torch
     from torch.utils import cpp_extension as ce
@@ -68,7 +74,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, variant: st
         o = os.path.join(OBJ, os.path.basename(k) + ".o")
         objs.append(o)
         if force or _newer([k] + headers, o):
-            jobs_list.append(base + ["-c", k, "-o", o])
+            jobs_list.append(base + FILE_FLAGS.get(os.path.basename(k), []) + ["-c", k, "-o", o])
     incs, tlib, abi = _torch_paths()
     # translation units that include torch: the pybind module, the native RCCL engine, the stage runner
     host_hdrs = glob.glob(os.path.join(CSRC, "comm", "*.h"))
