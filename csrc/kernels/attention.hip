@@ -1533,10 +1533,7 @@ __global__ void __launch_bounds__(256, DP <= 64 ? 2 : 1) attn_bwd_dq_kernel(
 // machinery -- buffer-load-to-LDS K/V ring with entry-time lane offsets, the tile loop
 // unrolled over the 4-deep ring (immediate LDS offsets), one-compare masks
 template <int DP, bool CAUSAL, bool DROP>
-#ifndef MP_DQ2_HALVES
-#define MP_DQ2_HALVES 0
-#endif
-__global__ void __launch_bounds__(256, (MP_DQ2_HALVES && !DROP) ? 3 : 2) attn_bwd_dq2_kernel(
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq2_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     float* __restrict__ DELTA,
@@ -1648,58 +1645,6 @@ __global__ void __launch_bounds__(256, (MP_DQ2_HALVES && !DROP) ? 3 : 2) attn_bw
     if (!(CAUSAL && n0 > wave_last_q)) {
       const char* kb = smem + BUF * BUFB;
       const char* vb = kb + TILE;
-#if MP_DQ2_HALVES
-      // one 32-key half at a time: S, dP, the element math and dQ += K^T dS for half 0, then
-      // half 1 -- half the S / dP registers live (3 waves per SIMD instead of 2)
-      uint32_t keep = 0xffffffffu;
-      if (DROP) {
-        keep = 0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const uint32_t kr = (uint32_t)(n0 + (r & 3) + 8 * (r >> 2) + 4 * hl);
-          keep |= (hash_lo(dkey, qoff + kr) >= dthr ? 1u : 0u) << r;
-          keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
-        }
-      }
-      const bool edge = (n0 + 64 > Sk) || (CAUSAL && n0 + 63 > m0 + 32 * w + shift);
-#pragma unroll
-      for (int half = 0; half < 2; ++half) {
-        f32x16 sh = {}, ph = {};
-#pragma unroll
-        for (int s = 0; s < DP / 16; ++s) {
-          const bf16x8 ak = *reinterpret_cast<const bf16x8*>(kb + koff[s] + half * 32 * DP * 2);
-          const bf16x8 av = *reinterpret_cast<const bf16x8*>(vb + koff[s] + half * 32 * DP * 2);
-          sh = mfma32(ak, qf[s], sh);
-          ph = mfma32(av, gf[s], ph);
-        }
-        auto elems = [&](auto masked) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sh[r], c, -lse));
-            if constexpr (decltype(masked)::value) {
-              if (key_of(r) + 32 * half > lim0 - n0) p = 0.f;
-            }
-            float dpv = ph[r];
-            if (DROP) dpv = (keep >> (16 * half + r)) & 1u ? dpv * dinv : 0.f;
-            sh[r] = p * (dpv - dlt);
-          }
-        };
-        if (edge) elems(std::true_type{});
-        else elems(std::false_type{});
-        const bf16x8 dlo = pack8(sh, 0), dhi = pack8(sh, 1);
-#pragma unroll
-        for (int d = 0; d < DP / 32; ++d) {
-          auto tr = [&](int jp, int m) {
-            return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(kb + ktoff[d][jp] + 16 * DP * 2 * m));
-          };
-          dq[d] = mfma32(cat44(tr(0, 2 * half), tr(1, 2 * half)), dlo, dq[d]);
-          dq[d] = mfma32(cat44(tr(0, 2 * half + 1), tr(1, 2 * half + 1)), dhi, dq[d]);
-        }
-      }
-    }
-  };
-#else
       f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
 #pragma unroll
       for (int s = 0; s < DP / 16; ++s) {
@@ -1761,7 +1706,6 @@ __global__ void __launch_bounds__(256, (MP_DQ2_HALVES && !DROP) ? 3 : 2) attn_bw
       }
     }
   };
-#endif
   for (int t0 = 0; t0 < ntiles; t0 += NBUF) {
     tile(std::integral_constant<int, 0>{}, t0);
     if (t0 + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t0 + 1);
