@@ -890,6 +890,7 @@ __global__ void __launch_bounds__(256, DROP ? 2 : (MP_FWD_NBUF == 2 ? 4 : 3)) at
   }
 }
 
+
 // ==========================================================================================
 // backward dK / dV: workgroup = 128 keys (4 waves x 32) of one (b, kv head)
 // ==========================================================================================
