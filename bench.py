@@ -357,7 +357,9 @@ def child_env(base: dict, p2p: str, attempt: int, port: int, budget: float, res_
     if p2p == "gloo":
         env.update(MIPIPE_DIST_BACKEND="gloo", MIPIPE_P2P="auto")
     if p2p.endswith("-safe"):
-        env.update(MIPIPE_COLL_OVERLAP="0", MIPIPE_PP_LANES="0")
+        # the second attempt drops what a first multi-GPU run has never exercised: collective
+        # overlap, lanes at PP > 1 and receive-only posts ahead of the compute (recv-early)
+        env.update(MIPIPE_COLL_OVERLAP="0", MIPIPE_PP_LANES="0", MIPIPE_RECV_EARLY="0")
     env.pop("TORCHELASTIC_USE_AGENT_STORE", None)   # fresh rendezvous store per child
     return env
 

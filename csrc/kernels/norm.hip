@@ -329,7 +329,13 @@ static int norm_bwd_blocks(int rows) {
     const int v = e ? atoi(e) : 8;
     return v > 0 ? v : 8;
   }();
-  int nblk = rows < 512 ? (rows + 3) / 4 : 512;
+  // workgroup cap (MIPIPE_NORM_BWD_BLOCKS, A/B): 512 = 2 per CU, one row in flight per wave
+  static const int max_blk = [] {
+    const char* e = getenv("MIPIPE_NORM_BWD_BLOCKS");
+    const int v = e ? atoi(e) : 512;
+    return v > 0 ? v : 512;
+  }();
+  int nblk = rows < max_blk ? (rows + 3) / 4 : max_blk;
   if ((rows + nblk - 1) / nblk < min_rpb) nblk = (rows + min_rpb - 1) / min_rpb;
   return nblk < 1 ? 1 : nblk;
 }

@@ -119,6 +119,7 @@ def test_attempt_modes_and_last_resort_gloo():
     assert "TORCHELASTIC_USE_AGENT_STORE" not in e and e["MASTER_PORT"] == "29600"
     e = bench.child_env(base, "auto-safe", 1, 29601, 120.0, "/tmp/x.json")
     assert e["MIPIPE_P2P"] == "auto" and e["MIPIPE_COLL_OVERLAP"] == "0" and e["MIPIPE_PP_LANES"] == "0"
+    assert e["MIPIPE_RECV_EARLY"] == "0"
     assert "MIPIPE_DIST_BACKEND" not in e
     e = bench.child_env(base, "torch", 2, 29602, 120.0, "/tmp/x.json")
     assert e["MIPIPE_P2P"] == "torch" and "MIPIPE_COLL_OVERLAP" not in e

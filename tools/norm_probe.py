@@ -23,7 +23,8 @@ def t(fn, n=20):
     return s.elapsed_time(e) / n * 1e3
 
 
-for kind, T, D, cols in [("layernorm", 16384, 768, True), ("layernorm", 16384, 768, False), ("rmsnorm", 8192, 4096, False)]:
+TOK = int(os.environ.get("NORM_PROBE_T", "16384"))
+for kind, T, D, cols in [("layernorm", TOK, 768, True), ("layernorm", TOK, 768, False), ("rmsnorm", 8192, 4096, False)]:
     dy = torch.randn(T, D, device="cuda").to(torch.bfloat16)
     s_ = torch.randn(T, D, device="cuda").to(torch.bfloat16)
     dres = torch.randn(T, D, device="cuda").to(torch.bfloat16)
