@@ -752,7 +752,8 @@ __global__ void __launch_bounds__(256, DROP ? 2 : (MP_FWD_NBUF == 2 ? 4 : 3)) at
     for (int d = 0; d < DP / 32; ++d) o[d] = {};
     float m_run = -INFINITY;   // running maximum (log2 units) ...
     float m_sub = 0.f;         // ... and the finite value the probabilities subtract
-    f32x16 lsum = {};          // running row sum (every register: this lane's query)
+    f32x16 lsum = {};          // running row sum (every register: this lane's query) ...
+    float l_drop = 0.f;        // ... or, with dropout, the pre-mask sum on the VALU
     int n_end = Sk;
     if (CAUSAL) n_end = min(Sk, m0 + 128 + shift);
     const int ntiles = n_end > 0 ? (n_end + 63) / 64 : 0;
@@ -817,6 +818,7 @@ __global__ void __launch_bounds__(256, DROP ? 2 : (MP_FWD_NBUF == 2 ? 4 : 3)) at
 #pragma unroll
           for (int d = 0; d < DP / 32; ++d) o[d] *= alpha;
           lsum *= alpha;
+          l_drop *= alpha;
           m_run = m_new;
           m_sub = s_new;
         }
@@ -830,11 +832,14 @@ __global__ void __launch_bounds__(256, DROP ? 2 : (MP_FWD_NBUF == 2 ? 4 : 3)) at
             keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
           }
         }
+        float rs0 = 0.f, rs1 = 0.f;   // dropout: the normaliser sums P BEFORE the mask
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float p0 = __builtin_amdgcn_exp2f(__builtin_fmaf(s0[r], c, -m_sub));
           float p1 = __builtin_amdgcn_exp2f(__builtin_fmaf(s1[r], c, -m_sub));
           if (DROP) {
+            rs0 += p0;
+            rs1 += p1;
             p0 = (keep >> r) & 1u ? p0 * dinv : 0.f;
             p1 = (keep >> (16 + r)) & 1u ? p1 * dinv : 0.f;
           }
@@ -842,13 +847,17 @@ __global__ void __launch_bounds__(256, DROP ? 2 : (MP_FWD_NBUF == 2 ? 4 : 3)) at
           s1[r] = p1;
         }
         const bf16x8 p00 = pack8(s0, 0), p01 = pack8(s0, 1), p10 = pack8(s1, 0), p11 = pack8(s1, 1);
-        // row sums on the matrix cores: ones^T . P^T puts sum_k P[q][k] (of the bf16 P that
-        // the PV product uses) in every register of lane q -- 4 MFMAs in place of 32 adds and
-        // a cross-half exchange on the VALU, which is the busier pipe here
-        lsum = mfma32(ones, p00, lsum);
-        lsum = mfma32(ones, p01, lsum);
-        lsum = mfma32(ones, p10, lsum);
-        lsum = mfma32(ones, p11, lsum);
+        if constexpr (DROP) {
+          l_drop += xhalf_sum(rs0 + rs1);
+        } else {
+          // row sums on the matrix cores: ones^T . P^T puts sum_k P[q][k] (of the bf16 P that
+          // the PV product uses) in every register of lane q -- 4 MFMAs in place of 32 adds
+          // and a cross-half exchange on the VALU, which is the busier pipe here
+          lsum = mfma32(ones, p00, lsum);
+          lsum = mfma32(ones, p01, lsum);
+          lsum = mfma32(ones, p10, lsum);
+          lsum = mfma32(ones, p11, lsum);
+        }
 #pragma unroll
         for (int d = 0; d < DP / 32; ++d) {
           auto tr = [&](int jp, int m) {
@@ -868,7 +877,7 @@ __global__ void __launch_bounds__(256, DROP ? 2 : (MP_FWD_NBUF == 2 ? 4 : 3)) at
       if constexpr (NBUF == 3)
         if (t0 + 2 < ntiles) tile(std::integral_constant<int, 2 % NBUF>{}, t0 + 2);
     }
-    const float l_run = lsum[0];
+    const float l_run = DROP ? l_drop : lsum[0];
     if (qvalid) {
       const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
       bf16_t* orow = O + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;

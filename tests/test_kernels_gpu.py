@@ -328,31 +328,42 @@ def test_attention_dropout_mask_exact(p):
     assert not torch.equal(m_f[0], m_f[1])
 
 
-@pytest.mark.parametrize("S,D", [(128, 128), (96, 96), (64, 64)])
-def test_attention_dropout_bwd_matches_reference(S, D):
+@pytest.mark.parametrize("S,D,causal,B", [(128, 128, False, 2), (96, 96, False, 2), (64, 64, False, 2),
+                                          (64, 64, True, 2), (64, 64, False, 64)])
+def test_attention_dropout_bwd_matches_reference(S, D, causal, B):
     """Dropout attention forward + backward against an f32 reference that uses the kernels'
     own mask (recovered exactly as in test_attention_dropout_mask_exact: q = k = 0, V = I).
-    Non-causal S <= 128 runs the one-launch short backward (dQ and dK/dV roles in one grid)."""
+    Non-causal S <= 128 runs the one-launch short backward (dQ and dK/dV roles in one grid);
+    causal, and non-causal grids of >= 256 blocks (B 64), run the d_h-64 v2 kernels, whose
+    softmax normaliser must sum P before the dropout mask (with V = I the kept entries carry
+    exactly dinv / (number of visible keys))."""
     torch.manual_seed(0)
-    B, H, p, seed = 2, 4, 0.1, 4321
+    H, p, seed = 4, 0.1, 4321
     T = B * S
     z = torch.zeros(T, H * D, dtype=torch.bfloat16, device=DEV)
     eye = torch.eye(S, D, dtype=torch.bfloat16, device=DEV).repeat(B, H)
     om = torch.empty_like(z)
     lse = torch.empty(B * H * S, device=DEV)
-    ops.attn_fwd(z, z, eye, om, lse, B, S, S, H, H, D, False, p_drop=p, seed=seed)
-    keep = (om.float().view(B, S, H, S) > 0).permute(0, 2, 1, 3).float().cpu() / (1 - p)   # [B, H, q, k]
+    ops.attn_fwd(z, z, eye, om, lse, B, S, S, H, H, D, causal, p_drop=p, seed=seed)
+    omf = om.float().view(B, S, H, S).permute(0, 2, 1, 3).cpu()                          # [B, H, q, k]
+    keep = (omf > 0).float() / (1 - p)
+    seen = torch.arange(1, S + 1).view(S, 1).float() if causal else torch.full((S, 1), float(S))
+    kept = omf[omf > 0]
+    torch.testing.assert_close(kept, ((keep / seen.view(1, 1, S, 1).expand_as(keep)))[omf > 0], rtol=1e-2, atol=0)
     q, k, v, do = (rnd(T, H * D).to(DEV) for _ in range(4))
     o = torch.empty_like(q)
-    ops.attn_fwd(q, k, v, o, lse, B, S, S, H, H, D, False, p_drop=p, seed=seed)
+    ops.attn_fwd(q, k, v, o, lse, B, S, S, H, H, D, causal, p_drop=p, seed=seed)
     dq, dk, dv = torch.zeros_like(q), torch.zeros_like(q), torch.zeros_like(q)
     dbias = torch.zeros(3 * H * D, device=DEV)
-    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, S, H, H, D, False, p_drop=p, seed=seed, dbias=dbias)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, B, S, S, H, H, D, causal, p_drop=p, seed=seed, dbias=dbias)
     torch.cuda.synchronize()
     hd = lambda t: t.float().cpu().view(B, S, H, D).permute(0, 2, 1, 3)   # noqa: E731
     Q, K, V, dO, O = hd(q), hd(k), hd(v), hd(do), hd(o)
     sc = 1.0 / math.sqrt(D)
-    P = torch.softmax(Q @ K.transpose(-1, -2) * sc, -1)
+    sco = Q @ K.transpose(-1, -2) * sc
+    if causal:
+        sco = sco.masked_fill(torch.ones(S, S).triu(1).bool(), float("-inf"))
+    P = torch.softmax(sco, -1)
     O_ref = (P * keep) @ V
     dV = (P * keep).transpose(-1, -2) @ dO
     dP = (dO @ V.transpose(-1, -2)) * keep
