@@ -6,4 +6,4 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout
 rc=$?
 tail -15 gpurun_out/r6_gpu_suite.log
 [ $rc -eq 0 ] || exit $rc
-bash tools/runs/r6_attn_dkdv_tedge.sh
+bash tools/runs/r6/r6_attn_dkdv_tedge.sh
