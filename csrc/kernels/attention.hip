@@ -1359,6 +1359,266 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dkdv2_kernel(
   }
 }
 
+// dK / dV v3 (the default; MIPIPE_ATTN_BWD_DKDV=2 selects v2): v2 with paired causal key blocks
+// on one XCD
+template <int DP, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dkdv3_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ dO, const float* __restrict__ LSE, const float* __restrict__ DELTA,
+    bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs,
+    int64_t ks, int64_t vs, int64_t os, int64_t dks, int64_t dvs, float scale, float p_drop, uint64_t seed,
+    float* __restrict__ CSK, float* __restrict__ CSV) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;
+  constexpr int BUFB = 2 * TILE + 512;               // Q, dO, lse[64], delta[64]
+  // ring depth: MIPIPE-tunable at build time (MP_DKDV_NBUF); 4 buffers keep 3 tiles in flight
+#ifndef MP_DKDV_NBUF
+#define MP_DKDV_NBUF 4
+#endif
+  constexpr int NBUF = 4;
+  constexpr int LOOK = NBUF - 1;                     // tiles issued ahead
+
+  // causal: one workgroup runs key block p (it sees the most queries) and then block
+  // nkb-1-p of the same (b, kv head), so every workgroup does about the same work; the pairs
+  // of one (b, kv head) are consecutive on one XCD (workgroup id mod 8), so their Q / dO tiles
+  // are read while the others still hold them in that XCD's L2 (the forward v2 mapping)
+  const int nkb = (Sk + 127) / 128;
+  const int npair = CAUSAL ? (nkb + 1) / 2 : nkb;
+  const int nbhk = B * Hkv;
+  const int lin = (int)blockIdx.x;
+  int bhk, p;
+  if ((nbhk & 7) == 0) {
+    const int xcd = lin & 7, j = lin >> 3;
+    bhk = (j / npair) * 8 + xcd;
+    p = j % npair;
+  } else {
+    bhk = lin / npair;
+    p = lin % npair;
+  }
+  const int b = bhk / Hkv, hk = bhk % Hkv;
+  const int grp = H / Hkv;
+  const int lane = threadIdx.x & 63, hl = lane >> 5, l32 = lane & 31;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int shift = Sk - Sq;
+  const float c = scale * LOG2E;
+  const uint32_t dthr = drop_thr(p_drop);
+  const float dinv = 1.0f / (1.0f - p_drop);
+  BTile<DP> qt, gt2;
+  qt.init(qs, D, w);
+  gt2.init(os, D, w);
+  // per-lane fragment offsets (see attn_fwd2_kernel): row reads of rows 32u + l32 at chunk
+  // 2s + hl; transposed reads of rows 32u + 8j + 4hl + q at column 32d + 16 (lane>>4 & 1) + 4p
+  int roff[DP / 16], troff[DP / 32][2];
+  {
+    const int i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) roff[s] = lds_off<DP>(l32, 2 * s + hl);
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int row = 8 * jp + 4 * hl + q, col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * pp;
+        troff[d][jp] = lds_off<DP>(row, col >> 3) + ((col & 7) << 1);
+      }
+  }
+  const int npass = CAUSAL && (nkb - 1 - p) != p ? 2 : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+  const int kb = CAUSAL ? (pass == 0 ? p : nkb - 1 - p) : p;
+  const int k0 = kb * 128;
+  const int key = k0 + 32 * w + l32;  // this lane's key (MFMA column)
+  const bool kvalid = key < Sk;
+  if (pass > 0) {   // the ring and the column-sum scratch of the previous pass are free
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  // K and V of this wave's 32 keys as B operands: lane holds K[key][16s + 8hl + j]
+  bf16x8 kf[DP / 16], vf[DP / 16];
+  const bf16_t* Krow = K + ((int64_t)b * Sk + key) * ks + (int64_t)hk * D;
+  const bf16_t* Vrow = V + ((int64_t)b * Sk + key) * vs + (int64_t)hk * D;
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    kf[s] = __builtin_bit_cast(bf16x8, gload8(Krow, 16 * s + 8 * hl, D, kvalid));
+    vf[s] = __builtin_bit_cast(bf16x8, gload8(Vrow, 16 * s + 8 * hl, D, kvalid));
+  }
+  f32x16 dk[DP / 32], dv[DP / 32];
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d) {
+    dk[d] = {};
+    dv[d] = {};
+  }
+  // first query that can see key k0: q >= k0 - shift
+  const int q_begin = CAUSAL ? max(0, ((k0 - shift) / 64) * 64) : 0;
+  const int ntq = (Sq - q_begin + 63) / 64;
+  const int total = ntq * grp;
+
+  // Q / dO tiles by buffer-load-to-LDS DMA (the forward v2 scheme): per-lane offsets fixed
+  // here, the tile's row offset a scalar, one buffer resource per query head (rows past Sq
+  // land as zeros); the loop below is unrolled over the ring, so LDS addresses are immediates
+  auto issue_to = [&](int it, char* buf) {
+    const int hq = hk * grp + it / ntq;
+    const int q0 = q_begin + (it % ntq) * 64;
+    const __amdgpu_buffer_rsrc_t qrs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(Q + (int64_t)b * Sq * qs + (int64_t)hq * D), 0, (int)(((int64_t)(Sq - 1) * qs + D) * 2), 0x00020000);
+    const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(dO + (int64_t)b * Sq * os + (int64_t)hq * D), 0, (int)(((int64_t)(Sq - 1) * os + D) * 2), 0x00020000);
+    qt.issue(qrs, (int)((int64_t)q0 * qs * 2), buf, w);
+    gt2.issue(grs, (int)((int64_t)q0 * os * 2), buf + TILE, w);
+    if (w == 0) {  // per-row stats, 4 bytes per lane (rows past Sq are masked in the math)
+      const int q = min(q0 + lane, Sq - 1);
+      const int64_t idx = ((int64_t)b * H + hq) * Sq + q;
+      __builtin_amdgcn_global_load_lds((const void*)(LSE + idx),
+                                       (__attribute__((address_space(3))) void*)(buf + 2 * TILE), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((const void*)(DELTA + idx),
+                                       (__attribute__((address_space(3))) void*)(buf + 2 * TILE + 256), 4, 0, 0);
+    }
+  };
+  constexpr int PER_TILE = 2 * BTile<DP>::PPW;  // DMA instructions per tile per wave (+2 on wave 0)
+#pragma unroll
+  for (int i = 0; i < LOOK; ++i)
+    if (i < total) issue_to(i, smem + i * BUFB);
+  auto tile = [&](auto bufc, int it) {
+    constexpr int BUF = decltype(bufc)::value;
+    const int hq = hk * grp + it / ntq;
+    const int q0 = q_begin + (it % ntq) * 64;
+    const int bhq = b * H + hq;
+    const DropKey dkey = drop_key(seed, (uint32_t)bhq);
+    // tile `it` landed (up to LOOK-1 younger tiles may stay in flight), then publish to all
+    // waves; wave 0 issues 2 extra DMAs per tile (the row stats)
+    if (LOOK >= 3 && it + 2 < total) {
+      if (w == 0) attn_wait_vmcnt<2 * (PER_TILE + 2)>(); else attn_wait_vmcnt<2 * PER_TILE>();
+    } else if (LOOK >= 2 && it + 1 < total) {
+      if (w == 0) attn_wait_vmcnt<PER_TILE + 2>(); else attn_wait_vmcnt<PER_TILE>();
+    } else {
+      attn_wait_vmcnt<0>();
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // the buffer of tile it-1 is free now: refill it with tile it+LOOK
+    if (it + LOOK < total) issue_to(it + LOOK, smem + ((BUF + LOOK) % NBUF) * BUFB);
+    const char* qb = smem + BUF * BUFB;
+    const char* gb = qb + TILE;
+    const float* ls = reinterpret_cast<const float*>(qb + 2 * TILE);
+    const float* dl = ls + 64;
+    const bool skip = CAUSAL && (k0 + 32 * w > q0 + 63 + shift);  // all of this wave's keys masked
+    if (!skip) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        // S[q][key] = Q K^T, dP[q][key] = dO V^T   (query rows u*32.. in registers, key on lane)
+        f32x16 sacc = {}, pacc = {};
+#pragma unroll
+        for (int s = 0; s < DP / 16; ++s) {
+          const bf16x8 aq = *reinterpret_cast<const bf16x8*>(qb + roff[s] + u * 32 * DP * 2);
+          const bf16x8 ag = *reinterpret_cast<const bf16x8*>(gb + roff[s] + u * 32 * DP * 2);
+          sacc = mfma32(aq, kf[s], sacc);
+          pacc = mfma32(ag, vf[s], pacc);
+        }
+        f32x16 pm, ds;
+        // per-row stats: rows 32u + 8g + 4hl + 0..3 are contiguous -> one 16-byte LDS read
+        float4 lsv[4], dlv[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          lsv[g] = *reinterpret_cast<const float4*>(ls + 32 * u + 8 * g + 4 * hl);
+          dlv[g] = *reinterpret_cast<const float4*>(dl + 32 * u + 8 * g + 4 * hl);
+        }
+        // masks only where needed: the causal diagonal and query rows past Sq (their
+        // stats were clamped); keys past Sk only feed their own unwritten outputs
+        const bool edge = (q0 + 64 > Sq) || (CAUSAL && (k0 + 32 * w + 31 > q0 + 32 * u + shift));
+        // the element math twice, masked and unmasked, behind one wave-uniform branch: as a
+        // per-element select the mask's index compares and cndmasks were issued on every
+        // tile (~half of the loop's VALU, profiles/r2_attention_pmc_counters.json)
+        // dropout keep bits first (only the mask stays live across the hashes)
+        uint32_t keep = 0xffffu;
+        if (DROP) {
+          keep = 0;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const uint32_t q = (uint32_t)(q0 + 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl);
+            keep |= (hash_lo(dkey, q * (uint32_t)Sk + (uint32_t)key) >= dthr ? 1u : 0u) << r;
+          }
+        }
+        auto elems = [&](auto masked) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int qr = 32 * u + (r & 3) + 8 * (r >> 2) + 4 * hl;
+            const int q = q0 + qr;
+            const float lv = (&lsv[r >> 2].x)[r & 3], dv_ = (&dlv[r >> 2].x)[r & 3];
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[r], c, -lv));
+            if constexpr (decltype(masked)::value) {
+              if (q >= Sq || (CAUSAL && key > q + shift)) p = 0.f;
+            }
+            float dpv = pacc[r];
+            float pd = p;
+            if (DROP) {
+              const float msk = (keep >> r) & 1u ? dinv : 0.f;
+              pd = p * msk;
+              dpv = dpv * msk;
+            }
+            pm[r] = pd;                      // dropped P for dV
+            ds[r] = p * (dpv - dv_);         // dS
+          }
+        };
+        if (edge) elems(std::true_type{});
+        else elems(std::false_type{});
+        // dV^T += dO^T P ;  dK^T += Q^T dS     (A via transposed LDS reads of the row images)
+        const bf16x8 pb0 = pack8(pm, 0), pb1 = pack8(pm, 1);
+        const bf16x8 db0 = pack8(ds, 0), db1 = pack8(ds, 1);
+#pragma unroll
+        for (int d = 0; d < DP / 32; ++d) {
+          auto tr = [&](const char* img, int jp, int m) {
+            return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(img + troff[d][jp] + u * 32 * DP * 2 + 16 * DP * 2 * m));
+          };
+          dv[d] = mfma32(cat44(tr(gb, 0, 0), tr(gb, 1, 0)), pb0, dv[d]);
+          dv[d] = mfma32(cat44(tr(gb, 0, 1), tr(gb, 1, 1)), pb1, dv[d]);
+          dk[d] = mfma32(cat44(tr(qb, 0, 0), tr(qb, 1, 0)), db0, dk[d]);
+          dk[d] = mfma32(cat44(tr(qb, 0, 1), tr(qb, 1, 1)), db1, dk[d]);
+        }
+      }
+    }
+  };
+  for (int t0 = 0; t0 < total; t0 += NBUF) {
+    tile(std::integral_constant<int, 0>{}, t0);
+    if (t0 + 1 < total) tile(std::integral_constant<int, 1>{}, t0 + 1);
+    if (t0 + 2 < total) tile(std::integral_constant<int, 2>{}, t0 + 2);
+    if (t0 + 3 < total) tile(std::integral_constant<int, 3>{}, t0 + 3);
+  }
+  // ---- fused bias-gradient column sums of dK (scaled) and dV
+  if (CSK != nullptr) {
+    __syncthreads();   // the Q / dO ring is free
+    float* red = reinterpret_cast<float*>(smem);
+    wg_colsum_atomic<DP>(dk, scale, kvalid, red, CSK + (int64_t)hk * D, D);
+    __syncthreads();
+    wg_colsum_atomic<DP>(dv, 1.f, kvalid, red, CSV + (int64_t)hk * D, D);
+  }
+  // ---- epilogue: lane = key, registers = d
+  if (kvalid) {
+    bf16_t* dkrow = dK + ((int64_t)b * Sk + key) * dks + (int64_t)hk * D;
+    bf16_t* dvrow = dV + ((int64_t)b * Sk + key) * dvs + (int64_t)hk * D;
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 32 * d + 8 * g + 4 * hl;
+        if (col < D) {
+          u16x4 a, bb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a[e] = f2bf(dk[d][4 * g + e] * scale);
+            bb[e] = f2bf(dv[d][4 * g + e]);
+          }
+          *reinterpret_cast<u16x4*>(dkrow + col) = a;
+          *reinterpret_cast<u16x4*>(dvrow + col) = bb;
+        }
+      }
+    }
+  }
+  }
+}
+
 // ==========================================================================================
 // backward dQ: workgroup = 128 queries of one (b, h) (forward structure)
 // ==========================================================================================
@@ -1741,6 +2001,225 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq2_kernel(
         }
       }
     }
+  }
+}
+
+// dQ v3 (MIPIPE_ATTN_BWD_DQ=3, A/B): v2 with paired causal query blocks on one XCD
+template <int DP, bool CAUSAL, bool DROP>
+__global__ void __launch_bounds__(256, 2) attn_bwd_dq3_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const bf16_t* __restrict__ O, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
+    float* __restrict__ DELTA,
+    bf16_t* __restrict__ dQ, int B, int Sq, int Sk, int H, int Hkv, int D, int64_t qs, int64_t ks, int64_t vs,
+    int64_t os, int64_t dqs, float scale, float p_drop, uint64_t seed, float* __restrict__ CSQ) {
+  if (p_drop > 0.f) seed = step_seed(seed);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int TILE = 64 * DP * 2;
+  const int nmb = (Sq + 127) / 128;
+  // causal: one workgroup runs query block nmb-1-p and then block p of the same (b, h), the
+  // pairs of one (b, h) consecutive on one XCD (the forward v2 mapping)
+  const int npair = CAUSAL ? (nmb + 1) / 2 : nmb;
+  const int nbh = B * H;
+  const int lin = (int)blockIdx.x;
+  int bh, p;
+  if ((nbh & 7) == 0) {
+    const int xcd = lin & 7, j = lin >> 3;
+    bh = (j / npair) * 8 + xcd;
+    p = j % npair;
+  } else {
+    bh = lin / npair;
+    p = lin % npair;
+  }
+  const int b = bh / H, h = bh % H, hk = h / (H / Hkv);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hl = lane >> 5, l32 = lane & 31;
+  const int npass = CAUSAL && (nmb - 1 - p) != p ? 2 : 1;
+  for (int pass = 0; pass < npass; ++pass) {
+  const int mb = CAUSAL ? (pass == 0 ? nmb - 1 - p : p) : p;
+  if (pass > 0) {   // the ring and the column-sum scratch of the previous pass are free
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  const int m0 = mb * 128;
+  const int qrow = m0 + 32 * w + l32;
+  const bool qvalid = qrow < Sq;
+  const int shift = Sk - Sq;
+  const bf16_t* Kb = K + (int64_t)b * Sk * ks + (int64_t)hk * D;
+  const bf16_t* Vb = V + (int64_t)b * Sk * vs + (int64_t)hk * D;
+  bf16x8 qf[DP / 16], gf[DP / 16];
+  const bf16_t* Qrow = Q + ((int64_t)b * Sq + qrow) * qs + (int64_t)h * D;
+  const bf16_t* Grow = dO + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;
+#pragma unroll
+  for (int s = 0; s < DP / 16; ++s) {
+    qf[s] = __builtin_bit_cast(bf16x8, gload8(Qrow, 16 * s + 8 * hl, D, qvalid));
+    gf[s] = __builtin_bit_cast(bf16x8, gload8(Grow, 16 * s + 8 * hl, D, qvalid));
+  }
+  const int64_t sidx = (int64_t)bh * Sq + qrow;
+  const float lse = qvalid ? LSE[sidx] : INFINITY;
+  // delta = rowsum(dO * O), fused here (each lane holds half of the row's d range)
+  float dlt = 0.f;
+  {
+    const bf16_t* Orow = O + ((int64_t)b * Sq + qrow) * os + (int64_t)h * D;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) {
+      const u16x8 ov = gload8(Orow, 16 * s + 8 * hl, D, qvalid);
+      const bf16x8 g = gf[s];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dlt += bf2f(ov[j]) * (float)g[j];
+    }
+    dlt += __shfl_xor(dlt, 32, 64);
+    if (qvalid && hl == 0) DELTA[sidx] = dlt;
+  }
+  const float c = scale * LOG2E;
+  const DropKey dkey = drop_key(seed, (uint32_t)bh);
+  const uint32_t dthr = drop_thr(p_drop), qoff = (uint32_t)qrow * (uint32_t)Sk;
+  const float dinv = 1.0f / (1.0f - p_drop);
+  f32x16 dq[DP / 32];
+#pragma unroll
+  for (int d = 0; d < DP / 32; ++d) dq[d] = {};
+  int n_end = Sk;
+  if (CAUSAL) n_end = min(Sk, m0 + 128 + shift);
+  const int ntiles = (n_end + 63) / 64;
+  // K / V tiles stream through an NBUF-deep LDS ring by LDS-DMA (the dK/dV kernel's
+  // scheme): LOOK tiles in flight, counted vmcnt, one raw barrier per tile
+  // K / V ring (the forward v2 scheme): NBUF buffers, LOOK tiles in flight, buffer-load-to-LDS
+  // DMA with per-lane offsets fixed here and a scalar tile offset; the tile loop is unrolled
+  // over the ring so every LDS address is an immediate
+  constexpr int NBUF = 4, LOOK = NBUF - 1, BUFB = 2 * TILE;
+  constexpr int PER_TILE = 2 * BTile<DP>::PPW;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+  const __amdgpu_buffer_rsrc_t krs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Kb, 0, (int)(((int64_t)(Sk - 1) * ks + D) * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)Vb, 0, (int)(((int64_t)(Sk - 1) * vs + D) * 2), 0x00020000);
+  BTile<DP> kt, vt;
+  kt.init(ks, D, wv);
+  vt.init(vs, D, wv);
+  const int kstep = (int)(64 * ks * 2), vstep = (int)(64 * vs * 2);
+  auto issue_to = [&](int t, char* buf) {
+    kt.issue(krs, t * kstep, buf, wv);
+    vt.issue(vrs, t * vstep, buf + TILE, wv);
+  };
+  int koff[DP / 16], ktoff[DP / 32][2];   // (see attn_fwd2_kernel)
+  {
+    const int i16 = lane & 15, q = i16 >> 2, pp = i16 & 3;
+#pragma unroll
+    for (int s = 0; s < DP / 16; ++s) koff[s] = lds_off<DP>(l32, 2 * s + hl);
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d)
+#pragma unroll
+      for (int jp = 0; jp < 2; ++jp) {
+        const int row = 8 * jp + 4 * hl + q, col = 32 * d + 16 * ((lane >> 4) & 1) + 4 * pp;
+        ktoff[d][jp] = lds_off<DP>(row, col >> 3) + ((col & 7) << 1);
+      }
+  }
+  // per-lane mask limit (see attn_fwd2_kernel): key k (+4 hl) of a tile at n0 is kept iff k <= lim0 - n0
+  const int lim0 = (CAUSAL ? min(qrow + shift, Sk - 1) : Sk - 1) - 4 * hl;
+#pragma unroll
+  for (int i = 0; i < LOOK; ++i)
+    if (i < ntiles) issue_to(i, smem + i * BUFB);
+  const int wave_last_q = m0 + 32 * w + 31 + shift;
+  auto tile = [&](auto bufc, int t) {
+    constexpr int BUF = decltype(bufc)::value;
+    const int n0 = t * 64;
+    if (t + 2 < ntiles) attn_wait_vmcnt<2 * PER_TILE>();
+    else if (t + 1 < ntiles) attn_wait_vmcnt<PER_TILE>();
+    else attn_wait_vmcnt<0>();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // every wave is done with tile t-1: its buffer takes tile t+LOOK
+    if (t + LOOK < ntiles) issue_to(t + LOOK, smem + ((BUF + LOOK) % NBUF) * BUFB);
+    if (!(CAUSAL && n0 > wave_last_q)) {
+      const char* kb = smem + BUF * BUFB;
+      const char* vb = kb + TILE;
+      f32x16 s0 = {}, s1 = {}, p0 = {}, p1 = {};
+#pragma unroll
+      for (int s = 0; s < DP / 16; ++s) {
+        const bf16x8 ak0 = *reinterpret_cast<const bf16x8*>(kb + koff[s]);
+        const bf16x8 ak1 = *reinterpret_cast<const bf16x8*>(kb + koff[s] + 32 * DP * 2);
+        const bf16x8 av0 = *reinterpret_cast<const bf16x8*>(vb + koff[s]);
+        const bf16x8 av1 = *reinterpret_cast<const bf16x8*>(vb + koff[s] + 32 * DP * 2);
+        s0 = mfma32(ak0, qf[s], s0);
+        s1 = mfma32(ak1, qf[s], s1);
+        p0 = mfma32(av0, gf[s], p0);  // dP^T = V dO^T
+        p1 = mfma32(av1, gf[s], p1);
+      }
+      // causal / key-end mask only on edge tiles; invalid query rows have lse = +inf
+      const bool edge = (n0 + 64 > Sk) || (CAUSAL && n0 + 63 > m0 + 32 * w + shift);
+      // masked / unmasked element math behind one wave-uniform branch (see the dK/dV kernel)
+      // dropout keep bits first (only the mask stays live across the hashes)
+      uint32_t keep = 0xffffffffu;
+      if (DROP) {
+        keep = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const uint32_t kr = (uint32_t)(n0 + (r & 3) + 8 * (r >> 2) + 4 * hl);
+          keep |= (hash_lo(dkey, qoff + kr) >= dthr ? 1u : 0u) << r;
+          keep |= (hash_lo(dkey, qoff + kr + 32u) >= dthr ? 1u : 0u) << (16 + r);
+        }
+      }
+      auto elems = [&](auto masked) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int kr = (r & 3) + 8 * (r >> 2) + 4 * hl;
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int kk = n0 + 32 * half + kr;
+            float sv = half ? s1[r] : s0[r];
+            float dpv = half ? p1[r] : p0[r];
+            float p = __builtin_amdgcn_exp2f(__builtin_fmaf(sv, c, -lse));
+            if constexpr (decltype(masked)::value) {
+              if (key_of(r) + 32 * half > lim0 - n0) p = 0.f;
+            }
+            if (DROP) dpv = (keep >> (16 * half + r)) & 1u ? dpv * dinv : 0.f;
+            const float dsv = p * (dpv - dlt);
+            if (half) s1[r] = dsv; else s0[r] = dsv;
+          }
+        }
+      };
+      if (edge) elems(std::true_type{});
+      else elems(std::false_type{});
+      const bf16x8 d00 = pack8(s0, 0), d01 = pack8(s0, 1), d10 = pack8(s1, 0), d11 = pack8(s1, 1);
+#pragma unroll
+      for (int d = 0; d < DP / 32; ++d) {
+        auto tr = [&](int jp, int m) {
+          return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(kb + ktoff[d][jp] + 16 * DP * 2 * m));
+        };
+        dq[d] = mfma32(cat44(tr(0, 0), tr(1, 0)), d00, dq[d]);
+        dq[d] = mfma32(cat44(tr(0, 1), tr(1, 1)), d01, dq[d]);
+        dq[d] = mfma32(cat44(tr(0, 2), tr(1, 2)), d10, dq[d]);
+        dq[d] = mfma32(cat44(tr(0, 3), tr(1, 3)), d11, dq[d]);
+      }
+    }
+  };
+  for (int t0 = 0; t0 < ntiles; t0 += NBUF) {
+    tile(std::integral_constant<int, 0>{}, t0);
+    if (t0 + 1 < ntiles) tile(std::integral_constant<int, 1>{}, t0 + 1);
+    if (t0 + 2 < ntiles) tile(std::integral_constant<int, 2>{}, t0 + 2);
+    if (t0 + 3 < ntiles) tile(std::integral_constant<int, 3>{}, t0 + 3);
+  }
+  if (CSQ != nullptr) {
+    __syncthreads();   // K / V tiles no longer read
+    wg_colsum_atomic<DP>(dq, scale, qvalid, reinterpret_cast<float*>(smem), CSQ + (int64_t)h * D, D);
+  }
+  if (qvalid) {
+    bf16_t* drow = dQ + ((int64_t)b * Sq + qrow) * dqs + (int64_t)h * D;
+#pragma unroll
+    for (int d = 0; d < DP / 32; ++d) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int col = 32 * d + 8 * g + 4 * hl;
+        if (col < D) {
+          u16x4 pk;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) pk[e] = f2bf(dq[d][4 * g + e] * scale);
+          *reinterpret_cast<u16x4*>(drow + col) = pk;
+        }
+      }
+    }
+  }
   }
 }
 
@@ -2184,13 +2663,22 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
     }
   }
   static const bool dq1 = [] { const char* e = getenv("MIPIPE_ATTN_BWD_DQ"); return e && e[0] == '1'; }();
+  static const bool dq3 = [] { const char* e = getenv("MIPIPE_ATTN_BWD_DQ"); return e && e[0] == '3'; }();
   bool dq_done = false;
   if constexpr (DP == 64) {
     if (!dq1 && (int64_t)(Sk + 128) * ks * 2 < (1ll << 31) && (int64_t)(Sk + 128) * vs * 2 < (1ll << 31)) {
-      hipLaunchKernelGGL((attn_bwd_dq2_kernel<DP, CAUSAL, DROP>), dim3((Sq + 127) / 128, B * H), dim3(256),
-                         4 * 2 * 64 * DP * 2, st, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
-                         (const bf16_t*)o, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, Sq, Sk, H, Hkv, D, qs, ks,
-                         vs, os, dqs, scale, p, seed, csq);
+      if (dq3) {
+        const int nmb = (Sq + 127) / 128;
+        hipLaunchKernelGGL((attn_bwd_dq3_kernel<DP, CAUSAL, DROP>), dim3((CAUSAL ? (nmb + 1) / 2 : nmb) * B * H),
+                           dim3(256), 4 * 2 * 64 * DP * 2, st, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                           (const bf16_t*)o, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, Sq, Sk, H, Hkv, D, qs,
+                           ks, vs, os, dqs, scale, p, seed, csq);
+      } else {
+        hipLaunchKernelGGL((attn_bwd_dq2_kernel<DP, CAUSAL, DROP>), dim3((Sq + 127) / 128, B * H), dim3(256),
+                           4 * 2 * 64 * DP * 2, st, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
+                           (const bf16_t*)o, (const bf16_t*)dout, lse, delta, (bf16_t*)dq, B, Sq, Sk, H, Hkv, D, qs,
+                           ks, vs, os, dqs, scale, p, seed, csq);
+      }
       dq_done = true;
     }
   }
@@ -2204,9 +2692,20 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
                                  dqs, scale, p, seed, csq);
   }
   static const bool dkdv1 = [] { const char* e = getenv("MIPIPE_ATTN_BWD_DKDV"); return e && e[0] == '1'; }();
+  // v3 (paired key blocks on one XCD) by default: +0.4 % on the step over v2 (2 same-box runs
+  // each, profiles/r6_attention_v2.md); MIPIPE_ATTN_BWD_DKDV=2 / 1 select v2 / v1
+  static const bool dkdv3 = [] { const char* e = getenv("MIPIPE_ATTN_BWD_DKDV"); return !(e && e[0] == '2'); }();
   bool dkdv_done = false;
   if constexpr (DP == 64) {
     if (!dkdv1 && (int64_t)(Sq + 128) * qs * 2 < (1ll << 31) && (int64_t)(Sq + 128) * os * 2 < (1ll << 31)) {
+      if (dkdv3) {
+        const int nkb = (Sk + 127) / 128;
+        hipLaunchKernelGGL((attn_bwd_dkdv3_kernel<DP, CAUSAL, DROP>), dim3((CAUSAL ? (nkb + 1) / 2 : nkb) * B * Hkv),
+                           dim3(256), 4 * (2 * 64 * DP * 2 + 512), st, (const bf16_t*)q, (const bf16_t*)k,
+                           (const bf16_t*)v, (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, H,
+                           Hkv, D, qs, ks, vs, os, dks, dvs, scale, p, seed, csk, csv);
+        return (int)hipGetLastError();
+      }
       hipLaunchKernelGGL((attn_bwd_dkdv2_kernel<DP, CAUSAL, DROP>), dim3((Sk + 127) / 128, B * Hkv), dim3(256),
                          4 * (2 * 64 * DP * 2 + 512), st, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v,
                          (const bf16_t*)dout, lse, delta, (bf16_t*)dk, (bf16_t*)dv, B, Sq, Sk, H, Hkv, D, qs, ks, vs, os,
