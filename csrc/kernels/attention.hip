@@ -2004,7 +2004,8 @@ __global__ void __launch_bounds__(256, 2) attn_bwd_dq2_kernel(
   }
 }
 
-// dQ v3 (MIPIPE_ATTN_BWD_DQ=3, A/B): v2 with paired causal query blocks on one XCD
+// dQ v3 (the default; MIPIPE_ATTN_BWD_DQ=2 selects v2): v2 with paired causal query blocks on
+// one XCD
 template <int DP, bool CAUSAL, bool DROP>
 __global__ void __launch_bounds__(256, 2) attn_bwd_dq3_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
@@ -2663,7 +2664,9 @@ static int launch_bwd(const void* q, const void* k, const void* v, const void* o
     }
   }
   static const bool dq1 = [] { const char* e = getenv("MIPIPE_ATTN_BWD_DQ"); return e && e[0] == '1'; }();
-  static const bool dq3 = [] { const char* e = getenv("MIPIPE_ATTN_BWD_DQ"); return e && e[0] == '3'; }();
+  // v3 (paired query blocks on one XCD) by default: +0.35 % on the step over v2 (2 same-box
+  // runs each); MIPIPE_ATTN_BWD_DQ=2 / 1 select v2 / v1
+  static const bool dq3 = [] { const char* e = getenv("MIPIPE_ATTN_BWD_DQ"); return !(e && e[0] == '2'); }();
   bool dq_done = false;
   if constexpr (DP == 64) {
     if (!dq1 && (int64_t)(Sk + 128) * ks * 2 < (1ll << 31) && (int64_t)(Sk + 128) * vs * 2 < (1ll << 31)) {
